@@ -1,0 +1,146 @@
+/*
+ * rnnlogic_hip.h — C-ABI of the MI355X (gfx950) reasoning-predictor hot path.
+ *
+ * Drop-in boundary for RNNLogic's PredictorPlus forward.  Every entry point
+ * takes plain pointers and sizes (device pointers unless marked "host") and an
+ * opaque hipStream_t passed as void*.  No torch types cross this line; the
+ * Python side (rnnlogic_amd/, ctypes) mirrors the reference's
+ * src/{data,predictors,layers,embedding}.py API on top of it.
+ *
+ * The reference has no FFI on this path: it runs PyTorch eager ops plus
+ * torch_scatter.  Each function below names the reference code it replaces.
+ *
+ * Conventions
+ *   - return value: RNNL_OK (0) or an RNNL_ERR_* code; rnnl_last_error()
+ *     gives a thread-local message.
+ *   - handles (rnnl_graph, rnnl_rules) are immutable after creation and may be
+ *     used from several streams at once; one set per GPU / rank.
+ *   - all launches are asynchronous on `stream` and capture-safe (no
+ *     allocation or synchronisation inside), except the *_create calls.
+ */
+#ifndef RNNLOGIC_HIP_H
+#define RNNLOGIC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RNNL_OK 0
+#define RNNL_ERR_INVALID 1   /* bad argument / shape */
+#define RNNL_ERR_HIP 2       /* HIP runtime error */
+#define RNNL_ERR_OVERFLOW 3  /* workspace capacity exceeded: retry with a larger workspace */
+#define RNNL_ERR_NOMEM 4
+
+#define RNNL_AGG_SUM 0       /* FuncToNodeSum   (reference src/layers.py:53-77)  */
+#define RNNL_AGG_PNA 1       /* FuncToNode, pna (reference src/layers.py:79-126) */
+
+#define RNNL_FEATURE_ADD 0   /* score = base + mlp  (entity_feature bias / RotatE) */
+#define RNNL_FEATURE_NONE 1  /* score = mlp at candidates, base elsewhere (-inf)  */
+
+typedef struct rnnl_graph_s *rnnl_graph;
+typedef struct rnnl_rules_s *rnnl_rules;
+
+const char *rnnl_last_error(void);
+int rnnl_version(void);
+
+/* ---------------------------------------------------------------- graph --
+ * Replaces KnowledgeGraph.__init__'s adjacency (reference src/data.py:39-106):
+ * relation2adjacency / relation2ht2index.  Builds a vertex-major CSR
+ * (edges of (head v, relation r) contiguous, train-file order inside) and the
+ * per-relation edge tables used to resolve `edges_to_remove` ids
+ * (relation-local, file order == data.py:68).  train_hrt is host (n_train x 3).
+ */
+int rnnl_graph_create(const int32_t *train_hrt, int64_t n_train, int32_t n_entities, int32_t n_relations,
+                      rnnl_graph *out);
+int rnnl_graph_destroy(rnnl_graph g);
+/* host out: {n_entities, n_relations, n_edges_lo, n_edges_hi} */
+int rnnl_graph_info(rnnl_graph g, int32_t *info4);
+
+/* ---------------------------------------------------------------- rules --
+ * Replaces PredictorPlus.set_rules (reference src/predictors.py:165-199).
+ * rule_tokens/rule_ptr (host): rule i is tokens[ptr[i] .. ptr[i+1]) =
+ * (head, body...).  Builds, per head relation, a prefix trie of the rule
+ * bodies (shared prefixes are grounded once; the result is identical).
+ */
+int rnnl_rules_create(rnnl_graph g, const int32_t *rule_tokens, const int64_t *rule_ptr, int32_t n_rules,
+                      rnnl_rules *out);
+int rnnl_rules_destroy(rnnl_rules r);
+/* host out: {n_rules, n_nodes, max_depth, node record bytes (sum), node record bytes (pna)} */
+int rnnl_rules_info(rnnl_rules r, int32_t *info5);
+
+/* Per-node aggregate of rule embeddings (device): rule_emb is n_rules x H
+ * (row stride `ld` floats), H == 16.  Writes node_w: n_nodes records of
+ * info5[3 + aggregator] bytes.
+ *   SUM record: int64 fix(sum x)[16]
+ *   PNA record: int64 fix(sum x)[16] | int64 fix(sum x^2)[16] | f32 min x[16] | f32 max x[16]
+ * where fix(v) = round(v * 2^28).  Members are summed in rule-id order (fp32),
+ * and the per-candidate sums over nodes are then exact integer arithmetic, so
+ * every score is a deterministic function of its per-rule path counts. */
+int rnnl_node_weights(rnnl_rules r, const float *rule_emb, int32_t ld, int32_t aggregator, void *node_w,
+                      void *stream);
+
+/* ------------------------------------------------------------- forward --
+ * Replaces the body of PredictorPlus.forward (reference
+ * src/predictors.py:210-271) for n_queries rows — one reference batch, or
+ * many batches at once — including grounding/propagate (src/data.py:136-173),
+ * torch_scatter's scatter-sum, the rule->entity aggregator (src/layers.py)
+ * and score_model (src/layers.py:9-51 MLP(32,[128,1])).
+ *
+ * score (n_queries x E, row-major) must hold the base score on entry
+ * (bias row, RotatE scores or -inf; see rnnl_fill_* / rnnl_rotate_score);
+ * candidate entries are updated in place.  mask (nullable, n_queries x E
+ * bytes, zeroed by the caller) receives 1 at candidates.  n_cand (nullable)
+ * receives the candidate count per query; digest (nullable) an
+ * order-independent integer fingerprint of the per-rule path counts
+ * (tests only; see oracle/ground_oracle.c).
+ */
+typedef struct {
+  int32_t aggregator;      /* RNNL_AGG_* */
+  int32_t feature;         /* RNNL_FEATURE_* */
+  const void *node_w;      /* rnnl_node_weights output */
+  const float *add_w;      /* rule_to_entity.add_model.layers.0.weight (16 x 16 | 16 x 192) */
+  const float *add_b;      /* (16) */
+  const float *ln_w;       /* rule_to_entity.layer_norm.weight (16) */
+  const float *ln_b;       /* (16) */
+  const float *s0_w;       /* score_model.layers.0.weight (128 x 32) */
+  const float *s0_b;       /* (128) */
+  const float *s1_w;       /* score_model.layers.1.weight (1 x 128) */
+  const float *s1_b;       /* (1) */
+  const float *rel_emb;    /* relation_emb.weight (R x 16) */
+} rnnl_predictor_params;
+
+/* Workspace bytes for one launch of rnnl_predictorplus_forward (host). */
+int rnnl_forward_workspace_size(rnnl_graph g, rnnl_rules r, int32_t n_queries, int32_t capacity_scale,
+                                size_t *bytes);
+int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p, const int64_t *all_h,
+                               const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries,
+                               float *score, uint8_t *mask, int32_t *n_cand, uint64_t *digest, void *workspace,
+                               size_t workspace_bytes, int32_t capacity_scale, void *stream);
+/* After a forward: RNNL_OK, or RNNL_ERR_OVERFLOW if any query exceeded the
+ * workspace (those rows are incomplete; rerun with a larger capacity_scale).
+ * Synchronises `stream`. */
+int rnnl_forward_status(void *workspace, void *stream);
+
+/* --------------------------------------------------------- entity feature --
+ * Base-score fills (reference src/predictors.py:260-269). */
+int rnnl_fill_rows(const float *row, int32_t n_queries, int32_t n_entities, float *score, void *stream);
+int rnnl_fill_value(float value, int64_t n, float *score, void *stream);
+
+/* RotatE entity feature (reference src/embedding.py:28-70):
+ * score[q][e] = gamma - sum_d |(h_q o r_q)_d - e_d|, complex entries stored
+ * [re(0:D) | im(D:2D)]; relation ids >= n_rel_fwd use the negated half
+ * (embedding.py:26).  eemb_t is the entity table transposed to 2D x E
+ * (rnnl_rotate_transpose), remb is (n_rel_total x D).  accumulate != 0 adds
+ * into score instead of overwriting. */
+int rnnl_rotate_transpose(const float *eemb, int32_t n_entities, int32_t dim2, float *eemb_t, void *stream);
+int rnnl_rotate_score(const float *eemb, const float *eemb_t, const float *remb, int32_t dim, float gamma,
+                      const int64_t *all_h, const int64_t *all_r, int32_t n_queries, int32_t n_entities,
+                      float *score, int32_t accumulate, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RNNLOGIC_HIP_H */

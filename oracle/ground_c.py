@@ -1,0 +1,145 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front-end of oracle/ground_oracle.c and of
+the reference-miner shim oracle/_ref/libref_miner.so.
+
+Builds its own vertex-major CSR from the train triples with NumPy (independent
+of the product's builder in rnnlogic_amd/), so a layout bug in the product
+cannot hide behind a shared helper.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libground_oracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libref_miner.so")
+
+_P = ctypes.c_void_p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+    if os.path.isdir("/root/reference/miner"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def _lib():
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    lib.oracle_digests.restype = ctypes.c_int
+    lib.oracle_query_candidates.restype = ctypes.c_int
+    lib.oracle_mix64.restype = ctypes.c_uint64
+    lib.oracle_mix64.argtypes = [ctypes.c_uint64]
+    return lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_P) if a is not None else None
+
+
+class CGraph:
+    """Vertex-major CSR (edges of (v, rel) contiguous, file order inside)."""
+
+    def __init__(self, n_entities, n_relations, train):
+        train = np.asarray(train, dtype=np.int64).reshape(-1, 3)
+        E, R = int(n_entities), int(n_relations)
+        key = train[:, 0] * R + train[:, 1]
+        order = np.argsort(key, kind="stable")
+        self.col = train[order, 2].astype(np.int32)
+        counts = np.bincount(key, minlength=E * R)
+        self.off = np.zeros(E * R + 1, np.int64)
+        np.cumsum(counts, out=self.off[1:])
+        self.E, self.R = E, R
+
+
+class CRules:
+    """Rules grouped by head in file order; returns global rule ids."""
+
+    def __init__(self, rules, n_relations):
+        heads = np.asarray([hd for hd, _ in rules], dtype=np.int64)
+        self.order = np.argsort(heads, kind="stable")  # file order inside each head
+        self.rh_ptr = np.zeros(n_relations + 1, np.int32)
+        np.cumsum(np.bincount(heads, minlength=n_relations), out=self.rh_ptr[1:])
+        # ids must be global rule ids: keep rules in head-sorted order but remember ids
+        bodies = [rules[i][1] for i in self.order]
+        self.bptr = np.zeros(len(rules) + 1, np.int32)
+        np.cumsum([len(b) for b in bodies], out=self.bptr[1:])
+        self.body = np.asarray([x for b in bodies for x in b] or [0], dtype=np.int32)
+        self.ids = self.order.astype(np.int32)
+
+
+def mix64(x):
+    return int(_lib().oracle_mix64(ctypes.c_uint64(int(x) & 0xFFFFFFFFFFFFFFFF)))
+
+
+class Oracle:
+    def __init__(self, cgraph, rules, n_relations):
+        self.g = cgraph
+        self.rules = CRules(rules, n_relations)
+        self.lib = _lib()
+
+    def _args(self):
+        g, r = self.g, self.rules
+        return [_ptr(g.off), _ptr(g.col), ctypes.c_int(g.R), ctypes.c_int(g.E), _ptr(r.rh_ptr), _ptr(r.bptr),
+                _ptr(r.body), _ptr(r.ids)]
+
+    def candidates(self, h, r, rm_src=-1, rm_dst=-1):
+        """Sorted candidates of one query: (t, sum of counts, rule fingerprint)."""
+        cap = self.g.E
+        t = np.empty(cap, np.int32)
+        s = np.empty(cap, np.int64)
+        f = np.empty(cap, np.uint64)
+        n = self.lib.oracle_query_candidates(*self._args(), int(h), int(r), int(rm_src), int(rm_dst), _ptr(t),
+                                             _ptr(s), _ptr(f), ctypes.c_int(cap))
+        assert n >= 0
+        return t[:n], s[:n], f[:n]
+
+    def digests(self, h, r, rm_src=None, rm_dst=None, threads=None, work=False):
+        h = np.ascontiguousarray(h, dtype=np.int32)
+        r = np.ascontiguousarray(r, dtype=np.int32)
+        rs = np.ascontiguousarray(rm_src, dtype=np.int32) if rm_src is not None else None
+        rd = np.ascontiguousarray(rm_dst, dtype=np.int32) if rm_dst is not None else None
+        n = len(h)
+        d = np.zeros(n, np.uint64)
+        c = np.zeros(n, np.int32)
+        w = np.zeros((n, 3), np.int64) if work else None
+        rc = self.lib.oracle_digests(*self._args(), _ptr(h), _ptr(r), _ptr(rs), _ptr(rd), ctypes.c_int(n),
+                                     ctypes.c_int(threads or os.cpu_count() or 1), _ptr(d), _ptr(c), _ptr(w))
+        assert rc == 0
+        return (d, c, w) if work else (d, c)
+
+
+class RefMiner:
+    """The reference's own C++ path counter (miner/rnnlogic.cpp), via oracle/_ref."""
+
+    def __init__(self, data_path):
+        if not os.path.exists(REF_LIB):
+            build()
+        self.lib = ctypes.CDLL(REF_LIB)
+        self.lib.ref_kg_load.restype = _P
+        self.lib.ref_out_test_timed.restype = ctypes.c_double
+        self.kg = self.lib.ref_kg_load(data_path.encode())
+
+    def rule_destination(self, e, body, rm=(-1, -1, -1), cap=1 << 20):
+        b = np.asarray(body, dtype=np.int32)
+        d = np.empty(cap, np.int32)
+        c = np.empty(cap, np.int32)
+        n = self.lib.ref_rule_destination(_P(self.kg), int(e), _ptr(b), len(b), int(rm[0]), int(rm[1]),
+                                          int(rm[2]), _ptr(d), _ptr(c), cap)
+        assert n >= 0
+        return d[:n], c[:n]
+
+    def out_test_timed(self, rules, threads, sample):
+        flat = []
+        for hd, body in rules:
+            flat += [hd, len(body)] + list(body)
+        f = np.asarray(flat, dtype=np.int32)
+        n = ctypes.c_longlong(0)
+        sec = self.lib.ref_out_test_timed(_P(self.kg), _ptr(f), len(rules), int(threads), int(sample),
+                                          ctypes.byref(n))
+        return sec, n.value
+
+    def close(self):
+        self.lib.ref_kg_free(_P(self.kg))

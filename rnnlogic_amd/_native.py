@@ -1,0 +1,92 @@
+"""ctypes binding of the C-ABI library (include/rnnlogic_hip.h).
+
+This is the only door from Python into the HIP path.  The library is built
+in-tree (rnnlogic_amd/_build/librnnlogic_hip.so, see build()); if it is
+missing, every GPU entry point raises — there is no silent fallback.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
+
+RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM = 0, 1, 2, 3, 4
+AGG_SUM, AGG_PNA = 0, 1
+FEATURE_ADD, FEATURE_NONE = 0, 1
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F32 = ctypes.c_float
+
+# (name, restype, argtypes) for every symbol declared in include/rnnlogic_hip.h
+SIGNATURES = [
+    ("rnnl_last_error", ctypes.c_char_p, []),
+    ("rnnl_version", ctypes.c_int, []),
+    ("rnnl_graph_create", ctypes.c_int, [_P, _I64, _I32, _I32, _P]),
+    ("rnnl_graph_destroy", ctypes.c_int, [_P]),
+    ("rnnl_graph_info", ctypes.c_int, [_P, _P]),
+    ("rnnl_rules_create", ctypes.c_int, [_P, _P, _P, _I32, _P]),
+    ("rnnl_rules_destroy", ctypes.c_int, [_P]),
+    ("rnnl_rules_info", ctypes.c_int, [_P, _P]),
+    ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P]),
+    ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),
+    ("rnnl_predictorplus_forward", ctypes.c_int,
+     [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
+    ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
+    ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
+    ("rnnl_rotate_transpose", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    ("rnnl_rotate_score", ctypes.c_int, [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _P]),
+]
+
+
+class PredictorParams(ctypes.Structure):
+    """rnnl_predictor_params (include/rnnlogic_hip.h)."""
+    _fields_ = [("aggregator", _I32), ("feature", _I32), ("node_w", _P), ("add_w", _P), ("add_b", _P),
+                ("ln_w", _P), ("ln_b", _P), ("s0_w", _P), ("s0_b", _P), ("s1_w", _P), ("s1_b", _P),
+                ("rel_emb", _P)]
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("rnnlogic_hip error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def build(verbose=False):
+    """Compile the library for gfx950 with hipcc (cross-compiles without a GPU)."""
+    out = subprocess.run(["make", "-C", os.path.join(HERE, "csrc"), "-j4"], capture_output=not verbose, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("building librnnlogic_hip.so failed:\n%s%s" % (out.stdout or "", out.stderr or ""))
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("HIP library %s is missing: run rnnlogic_amd._native.build() "
+                               "(or __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != RNNL_OK:
+        raise NativeError(rc, lib().rnnl_last_error().decode(errors="replace"))
+    return rc
+
+
+def call(name, *args):
+    return check(getattr(lib(), name)(*args))

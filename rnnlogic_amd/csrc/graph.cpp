@@ -1,0 +1,247 @@
+// Host-side builders for the device-resident knowledge graph and rule tries.
+//
+//   rnnl_graph_create  <- KnowledgeGraph.__init__ adjacency (ref src/data.py:39-106)
+//   rnnl_rules_create  <- PredictorPlus.set_rules           (ref src/predictors.py:165-199)
+//
+// Both run once per process / rule set, upload immutable arrays and return a
+// handle; nothing here is on the timed path.
+#include <algorithm>
+#include <map>
+#include <vector>
+
+#include "internal.h"
+
+namespace rnnl {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+static inline uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+template <typename T>
+static int upload(const std::vector<T> &h, void **slot, const T **dst) {
+  size_t bytes = std::max<size_t>(h.size(), 1) * sizeof(T);
+  RNNL_HIP_CHECK(hipMalloc(slot, bytes));
+  if (!h.empty()) RNNL_HIP_CHECK(hipMemcpy(*slot, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  *dst = static_cast<const T *>(*slot);
+  return RNNL_OK;
+}
+
+}  // namespace rnnl
+
+using namespace rnnl;
+
+extern "C" {
+
+const char *rnnl_last_error(void) { return g_err.c_str(); }
+int rnnl_version(void) { return 1; }
+
+int rnnl_graph_create(const int32_t *hrt, int64_t n, int32_t E, int32_t R, rnnl_graph *out) {
+  if (!out || E <= 0 || R <= 0 || n < 0 || (n > 0 && !hrt)) {
+    set_error("rnnl_graph_create: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if ((int64_t)E * R + 1 > (int64_t)INT32_MAX * 64 || n >= INT32_MAX) {
+    set_error("rnnl_graph_create: graph too large for 32-bit offsets");
+    return RNNL_ERR_INVALID;
+  }
+  const int64_t ER = (int64_t)E * R;
+  std::vector<int32_t> off(ER + 1, 0), col(n), ebase(R + 1, 0), esrc(n), edst(n);
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t h = hrt[3 * i], r = hrt[3 * i + 1], t = hrt[3 * i + 2];
+    if (h < 0 || h >= E || t < 0 || t >= E || r < 0 || r >= R) {
+      set_error("rnnl_graph_create: triple id out of range");
+      return RNNL_ERR_INVALID;
+    }
+    off[(int64_t)h * R + r + 1]++;
+    ebase[r + 1]++;
+  }
+  for (int64_t i = 0; i < ER; ++i) off[i + 1] += off[i];
+  for (int r = 0; r < R; ++r) ebase[r + 1] += ebase[r];
+  std::vector<int32_t> fill(off.begin(), off.end() - 1), efill(ebase.begin(), ebase.end() - 1);
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t h = hrt[3 * i], r = hrt[3 * i + 1], t = hrt[3 * i + 2];
+    col[fill[(int64_t)h * R + r]++] = t;  // train-file order inside (h, r)
+    const int32_t e = efill[r]++;         // relation-local id == reference edge id
+    esrc[e] = h;
+    edst[e] = t;
+  }
+  auto *g = new rnnl_graph_s;
+  (void)hipGetDevice(&g->device);
+  g->d.E = E;
+  g->d.R = R;
+  g->d.n_edges = n;
+  int rc = RNNL_OK;
+  if ((rc = upload(off, &g->mem[0], &g->d.off)) || (rc = upload(col, &g->mem[1], &g->d.col)) ||
+      (rc = upload(ebase, &g->mem[2], &g->d.edge_base)) || (rc = upload(esrc, &g->mem[3], &g->d.edge_src)) ||
+      (rc = upload(edst, &g->mem[4], &g->d.edge_dst))) {
+    rnnl_graph_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return RNNL_OK;
+}
+
+int rnnl_graph_destroy(rnnl_graph g) {
+  if (!g) return RNNL_OK;
+  for (void *p : g->mem)
+    if (p) (void)hipFree(p);
+  delete g;
+  return RNNL_OK;
+}
+
+int rnnl_graph_info(rnnl_graph g, int32_t *info) {
+  if (!g || !info) return RNNL_ERR_INVALID;
+  info[0] = g->d.E;
+  info[1] = g->d.R;
+  info[2] = (int32_t)(g->d.n_edges & 0x7fffffff);
+  info[3] = (int32_t)(g->d.n_edges >> 31);
+  return RNNL_OK;
+}
+
+int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int32_t n_rules, rnnl_rules *out) {
+  if (!g || !out || n_rules < 0 || (n_rules > 0 && (!tok || !ptr))) {
+    set_error("rnnl_rules_create: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const int R = g->d.R;
+  // per head: trie with nodes keyed by (parent, relation); rules in file order
+  struct TNode {
+    int parent, rel, depth;
+    std::vector<int> rules;
+    std::map<int, int> child;  // relation -> local node (ordered: deterministic BFS)
+  };
+  std::vector<std::vector<TNode>> tries(R);
+  for (int32_t i = 0; i < n_rules; ++i) {
+    const int64_t b = ptr[i], e = ptr[i + 1];
+    if (e <= b) {
+      set_error("rnnl_rules_create: empty rule");
+      return RNNL_ERR_INVALID;
+    }
+    const int head = tok[b];
+    if (head < 0 || head >= R) {
+      set_error("rnnl_rules_create: head relation out of range");
+      return RNNL_ERR_INVALID;
+    }
+    auto &t = tries[head];
+    if (t.empty()) t.push_back(TNode{-1, -1, 0, {}, {}});
+    int cur = 0;
+    for (int64_t k = b + 1; k < e; ++k) {
+      const int rel = tok[k];
+      if (rel < 0 || rel >= R) {
+        set_error("rnnl_rules_create: body relation out of range");
+        return RNNL_ERR_INVALID;
+      }
+      auto it = t[cur].child.find(rel);
+      if (it == t[cur].child.end()) {
+        const int id = (int)t.size();
+        const int depth = t[cur].depth + 1;
+        t.push_back(TNode{cur, rel, depth, {}, {}});
+        t[cur].child[rel] = id;
+        cur = id;
+      } else {
+        cur = it->second;
+      }
+    }
+    t[cur].rules.push_back(i);
+  }
+  // breadth-first renumbering, heads in relation order
+  std::vector<int32_t> head_root(R, -1), head_depth(R, 0), head_nodes(R, 0);
+  std::vector<int32_t> node_rel, node_child, node_nchild, node_nrules, node_rule_ptr(1, 0), node_rules;
+  std::vector<uint64_t> node_fp;
+  int max_depth = 0;
+  for (int r = 0; r < R; ++r) {
+    auto &t = tries[r];
+    if (t.empty()) continue;
+    const int base = (int)node_rel.size();
+    std::vector<int> order;  // local ids in BFS order
+    std::vector<int> newid(t.size(), -1);
+    order.push_back(0);
+    for (size_t q = 0; q < order.size(); ++q)
+      for (auto &kv : t[order[q]].child) order.push_back(kv.second);
+    for (size_t q = 0; q < order.size(); ++q) newid[order[q]] = base + (int)q;
+    head_root[r] = base;
+    head_nodes[r] = (int)order.size();
+    for (int loc : order) {
+      const TNode &nd = t[loc];
+      node_rel.push_back(nd.rel);
+      node_child.push_back(nd.child.empty() ? 0 : newid[nd.child.begin()->second]);
+      node_nchild.push_back((int)nd.child.size());
+      node_nrules.push_back((int)nd.rules.size());
+      uint64_t fp = 0;
+      for (int rid : nd.rules) {
+        node_rules.push_back(rid);
+        fp += mix64((uint64_t)rid);
+      }
+      node_fp.push_back(fp);
+      node_rule_ptr.push_back((int32_t)node_rules.size());
+      head_depth[r] = std::max(head_depth[r], nd.depth);
+    }
+    max_depth = std::max(max_depth, head_depth[r]);
+    // children of a node must be contiguous in the new numbering (BFS gives it)
+    for (int loc : order) {
+      int prev = -1;
+      for (auto &kv : t[loc].child) {
+        const int id = newid[kv.second];
+        if (prev >= 0 && id != prev + 1) {
+          set_error("rnnl_rules_create: internal BFS numbering error");
+          return RNNL_ERR_INVALID;
+        }
+        prev = id;
+      }
+    }
+    if ((int64_t)head_nodes[r] * g->d.E >= INT32_MAX) {
+      set_error("rnnl_rules_create: trie too large for 32-bit (node, entity) keys");
+      return RNNL_ERR_INVALID;
+    }
+  }
+  auto *rs = new rnnl_rules_s;
+  (void)hipGetDevice(&rs->device);
+  rs->R = R;
+  rs->E = g->d.E;
+  rs->d.n_rules = n_rules;
+  rs->d.n_nodes = (int32_t)node_rel.size();
+  rs->d.max_depth = max_depth;
+  rs->d.n_heads = R;
+  int rc = RNNL_OK;
+  if ((rc = upload(head_root, &rs->mem[0], &rs->d.head_root)) ||
+      (rc = upload(head_depth, &rs->mem[1], &rs->d.head_depth)) ||
+      (rc = upload(head_nodes, &rs->mem[2], &rs->d.head_nodes)) ||
+      (rc = upload(node_rel, &rs->mem[3], &rs->d.node_rel)) ||
+      (rc = upload(node_child, &rs->mem[4], &rs->d.node_child)) ||
+      (rc = upload(node_nchild, &rs->mem[5], &rs->d.node_nchild)) ||
+      (rc = upload(node_nrules, &rs->mem[6], &rs->d.node_nrules)) ||
+      (rc = upload(node_rule_ptr, &rs->mem[7], &rs->d.node_rule_ptr)) ||
+      (rc = upload(node_rules, &rs->mem[8], &rs->d.node_rules)) ||
+      (rc = upload(node_fp, &rs->mem[9], &rs->d.node_fp))) {
+    rnnl_rules_destroy(rs);
+    return rc;
+  }
+  *out = rs;
+  return RNNL_OK;
+}
+
+int rnnl_rules_destroy(rnnl_rules r) {
+  if (!r) return RNNL_OK;
+  for (void *p : r->mem)
+    if (p) (void)hipFree(p);
+  delete r;
+  return RNNL_OK;
+}
+
+int rnnl_rules_info(rnnl_rules r, int32_t *info) {
+  if (!r || !info) return RNNL_ERR_INVALID;
+  info[0] = r->d.n_rules;
+  info[1] = r->d.n_nodes;
+  info[2] = r->d.max_depth;
+  info[3] = kStrideSum;
+  info[4] = kStridePna;
+  return RNNL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,801 @@
+// Fused PredictorPlus forward for gfx950 (MI355X).
+//
+// One persistent workgroup (256 lanes = 4 waves) owns one query at a time,
+// dequeued from a device counter, and runs the whole reference forward for
+// that row of the batch:
+//
+//   grounding / propagate (ref src/data.py:136-173, torch_scatter scatter-sum)
+//       -> level-synchronous walk of the head relation's rule-prefix trie over
+//          the vertex-major CSR; every (trie node, entity) path count lives in
+//          an LDS hash (integer, exact); the query's own edge is skipped on
+//          hops of the query relation (data.py:164-169).
+//   candidate set + rule_count stack (ref src/predictors.py:221-244)
+//       -> leaf contributions (entity, node, count) bucketed per candidate
+//          entity through an LDS hash.
+//   rule_to_entity (ref src/layers.py:53-126) + score_model (layers.py:9-51)
+//       -> one lane per candidate: node sums in exact fixed point, then
+//          Linear/LayerNorm/ReLU and the 32->128->1 MLP in fp32 registers;
+//          the result is added into the pre-filled base score (bias/RotatE)
+//          or written (entity_feature none).
+//
+// Memory: the graph (CSR ~ E*R*4 B + edges*4 B) and the node tables are
+// read-only and L2/MALL resident; per-slot scratch in HBM holds the frontier
+// lists, contributions and buckets of the query in flight.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+
+namespace rnnl {
+
+constexpr int BS = 256;      // threads per workgroup
+constexpr int NW = BS / 64;  // waves
+constexpr int HCAP = 4096;   // phase A hash slots ((node, entity) -> count)
+constexpr int HC = 2048;     // phase B hash slots (entity -> candidate slot)
+constexpr int MAXC = 1024;   // candidates per phase-B pass
+constexpr int WG_PER_CU = 3;
+constexpr int NUM_CU = 256;
+constexpr int EMPTY = -1;
+constexpr int HDR_BYTES = 256;  // workspace header: [0] status, [1] dequeue counter
+
+// Per-slot scratch geometry (entries); scaled by capacity_scale.
+constexpr int64_t FCAP_BASE = 1 << 16;
+constexpr int64_t PCAP_BASE = 1 << 16;
+
+struct KParams {
+  GraphDev g;
+  RulesDev rl;
+  int32_t agg, feature;
+  const unsigned char *node_w;
+  const float *add_w, *add_b, *ln_w, *ln_b, *s0_w, *s0_b, *s1_w, *s1_b, *rel_emb;
+  const int64_t *all_h, *all_r, *etr;
+  int32_t nq;
+  float *score;
+  uint8_t *mask;
+  int32_t *n_cand;
+  uint64_t *digest;
+  unsigned char *ws;
+  int64_t fcap, pcap;
+  int32_t nslots;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t k) { return k * 2654435761u; }
+
+struct Slot {
+  int32_t *fn[2], *fv[2];
+  uint32_t *fc[2];
+  int32_t *ct, *cn;
+  uint32_t *cc;
+  int32_t *bn;
+  uint32_t *bc;
+};
+
+__host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) {
+  return 2 * fcap * 12 + pcap * 12 + pcap * 8;
+}
+
+__device__ inline Slot make_slot(unsigned char *ws, int slot, int64_t fcap, int64_t pcap) {
+  unsigned char *b = ws + HDR_BYTES + (int64_t)slot * slot_bytes(fcap, pcap);
+  Slot s;
+  for (int k = 0; k < 2; ++k) {
+    s.fn[k] = reinterpret_cast<int32_t *>(b);
+    b += fcap * 4;
+    s.fv[k] = reinterpret_cast<int32_t *>(b);
+    b += fcap * 4;
+    s.fc[k] = reinterpret_cast<uint32_t *>(b);
+    b += fcap * 4;
+  }
+  s.ct = reinterpret_cast<int32_t *>(b);
+  b += pcap * 4;
+  s.cn = reinterpret_cast<int32_t *>(b);
+  b += pcap * 4;
+  s.cc = reinterpret_cast<uint32_t *>(b);
+  b += pcap * 4;
+  s.bn = reinterpret_cast<int32_t *>(b);
+  b += pcap * 4;
+  s.bc = reinterpret_cast<uint32_t *>(b);
+  return s;
+}
+
+// Exclusive block scan of one int per thread; `total` gets the block sum.
+__device__ __forceinline__ int block_scan(int x, int *s_ws, int &total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) s_ws[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < NW; ++w) {
+      int t = s_ws[w];
+      s_ws[w] = acc;
+      acc += t;
+    }
+    s_ws[NW] = acc;
+  }
+  __syncthreads();
+  const int res = v - x + s_ws[wid];
+  total = s_ws[NW];
+  __syncthreads();
+  return res;
+}
+
+// Largest i in [0, n) with a[i] <= k (a non-decreasing, a[0] == 0 <= k).
+__device__ __forceinline__ int upper_idx(const int *a, int n, int k) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (a[mid] <= k)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+struct __align__(16) Smem {
+  union {
+    struct {
+      int key[HCAP];
+      uint32_t val[HCAP];
+    } a;
+    struct {
+      int key[HC];
+      int slot[HC];
+      int st[MAXC];
+      uint32_t cnt[MAXC];
+      int off[MAXC];
+    } b;
+  } u;
+  int ent_v[BS], ent_fch[BS], item_off[BS];
+  uint32_t ent_c[BS];
+  int it_child[BS], it_beg[BS], it_v[BS], it_rel[BS], it_flags[BS], edge_off[BS];
+  uint32_t it_c[BS];
+  float relb[128];
+  int ws[NW + 1];
+  int q, nd, np, ovf, fail, nc, sp;
+  int stk_lo[32], stk_hi[32];
+  unsigned long long sumlog, dig;
+};
+
+__device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pcap, int t, int node, uint32_t c) {
+  const int pos = atomicAdd(&S.np, 1);
+  if (pos < pcap) {
+    sl.ct[pos] = t;
+    sl.cn[pos] = node;
+    sl.cc[pos] = c;
+  } else {
+    S.ovf = 1;
+  }
+}
+
+__device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, int64_t fcap, int node, int v,
+                                              uint32_t c) {
+  const int pos = atomicAdd(&S.nd, 1);
+  if (pos < fcap) {
+    sl.fn[buf][pos] = node;
+    sl.fv[buf][pos] = v;
+    sl.fc[buf][pos] = c;
+  } else {
+    S.ovf = 1;
+  }
+}
+
+// (node, entity) += c in the phase-A hash; false if the table is full.
+__device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
+  uint32_t h = hash32((uint32_t)key) >> (32 - 12);
+#pragma unroll 1
+  for (int probe = 0; probe < 64; ++probe) {
+    const int k = atomicCAS(&S.u.a.key[h], EMPTY, key);
+    if (k == EMPTY || k == key) {
+      atomicAdd(&S.u.a.val[h], c);
+      return true;
+    }
+    h = (h + 1) & (HCAP - 1);
+  }
+  return false;
+}
+
+__device__ __forceinline__ int cand_find(const Smem &S, int t) {
+  uint32_t h = hash32((uint32_t)t) >> (32 - 11);
+  while (S.u.b.key[h] != t) h = (h + 1) & (HC - 1);
+  return h;
+}
+
+// ---------------------------------------------------------------- per candidate
+template <int AGG>
+__device__ void score_candidate(const KParams &p, Smem &S, const Slot &sl, int q, int t, int beg, int cnt,
+                                float mean_scale) {
+  constexpr int STRIDE = AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna;
+  long long a1[16];
+  long long a2[AGG == RNNL_AGG_PNA ? 16 : 1];
+  float mn[AGG == RNNL_AGG_PNA ? 16 : 1], mx[AGG == RNNL_AGG_PNA ? 16 : 1];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) a1[d] = 0;
+  if constexpr (AGG == RNNL_AGG_PNA) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a2[d] = 0;
+      mn[d] = __builtin_huge_valf();
+      mx[d] = -__builtin_huge_valf();
+    }
+  }
+  long long deg = 0;
+  uint64_t fp = 0;
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int n = sl.bn[e];
+    const long long c = sl.bc[e];
+    const long long *rec = reinterpret_cast<const long long *>(p.node_w + (int64_t)n * STRIDE);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) a1[d] += c * rec[d];
+    const int k = p.rl.node_nrules[n];
+    deg += c * k;
+    if (p.digest) fp += (uint64_t)c * p.rl.node_fp[n];
+    if constexpr (AGG == RNNL_AGG_PNA) {
+#pragma unroll
+      for (int d = 0; d < 16; ++d) a2[d] += c * rec[16 + d];
+      const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        mn[d] = fminf(mn[d], fr[d]);
+        mx[d] = fmaxf(mx[d], fr[16 + d]);
+      }
+    }
+  }
+  if (p.digest) {
+    const uint64_t dg = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+    atomicAdd(&S.dig, (unsigned long long)dg);
+  }
+  constexpr float inv_fix = 1.0f / (float)(1 << kFixShift);
+  float x1[16];
+  if constexpr (AGG == RNNL_AGG_SUM) {
+    // FuncToNodeSum: Linear(16,16) on the rule-weighted sum (layers.py:68-74)
+    float f[16];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) f[d] = (float)((double)a1[d] * (double)inv_fix);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc = fmaf(f[i], p.add_w[o * 16 + i], acc);
+      x1[o] = acc + p.add_b[o];
+    }
+  } else {
+    // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123)
+    const float degf = (float)(deg + 1);
+    const float dcl = fmaxf(degf, 1e-6f);
+    float feat[64];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      const float s = (float)((double)a1[d] * (double)inv_fix);
+      const float sq = (float)((double)a2[d] * (double)inv_fix);
+      const float mean = s / dcl;
+      const float sqm = sq / dcl;
+      feat[d] = mean;
+      feat[16 + d] = mn[d];
+      feat[32 + d] = mx[d];
+      feat[48 + d] = sqrtf(fmaxf(sqm - mean * mean, 1e-6f));
+    }
+    float scale = logf(degf);
+    scale = scale / fmaxf(mean_scale, 1e-6f);
+    const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      float acc = 0.f;
+      for (int f = 0; f < 64; ++f) {
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) acc = fmaf(feat[f] * sc[s3], p.add_w[o * 192 + f * 3 + s3], acc);
+      }
+      x1[o] = acc + p.add_b[o];
+    }
+  }
+  // LayerNorm(16) + ReLU (layers.py:74-75 / 124-125)
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * p.ln_w[d] + p.ln_b[d], 0.f);
+  // score_model: Linear(32,128) [relation half folded into relb], ReLU, Linear(128,1)
+  float out = 0.f;
+#pragma unroll 4
+  for (int o = 0; o < 128; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], p.s0_w[o * 32 + i], acc);
+    acc = fmaxf(acc + S.relb[o], 0.f);
+    out = fmaf(acc, p.s1_w[o], out);
+  }
+  out += p.s1_b[0];
+  const int64_t idx = (int64_t)q * p.g.E + t;
+  if (p.feature == RNNL_FEATURE_NONE)
+    p.score[idx] = out;
+  else
+    p.score[idx] = out + p.score[idx];
+  if (p.mask) p.mask[idx] = 1;
+}
+
+// ---------------------------------------------------------------- phase B
+// Buckets the query's leaf contributions per candidate entity and scores
+// every candidate.  When `degree_only` (PNA sweep 1), only accumulates
+// sum(log degree) over the candidates.  Returns false on hash overflow
+// (caller doubles the pass count).
+template <int AGG>
+__device__ bool candidates_pass(const KParams &p, Smem &S, const Slot &sl, int q, int P, int t_lo, int t_hi,
+                                bool degree_only, float mean_scale) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < HC; i += BS) S.u.b.key[i] = EMPTY;
+  for (int i = tid; i < MAXC; i += BS) S.u.b.cnt[i] = 0;
+  if (tid == 0) {
+    S.nc = 0;
+    S.fail = 0;
+  }
+  __syncthreads();
+  // B1: insert entity keys
+  for (int i = tid; i < P; i += BS) {
+    const int t = sl.ct[i];
+    if (t < t_lo || t >= t_hi) continue;
+    uint32_t h = hash32((uint32_t)t) >> (32 - 11);
+    int probe = 0;
+    for (; probe < HC; ++probe) {
+      const int k = atomicCAS(&S.u.b.key[h], EMPTY, t);
+      if (k == EMPTY || k == t) break;
+      h = (h + 1) & (HC - 1);
+    }
+    if (probe == HC) S.fail = 1;
+  }
+  __syncthreads();
+  if (S.fail) return false;
+  // B2: slot ids
+  for (int h = tid; h < HC; h += BS) {
+    const int k = S.u.b.key[h];
+    if (k != EMPTY) {
+      const int s = atomicAdd(&S.nc, 1);
+      if (s < MAXC) {
+        S.u.b.slot[h] = s;
+        S.u.b.st[s] = k;
+      } else {
+        S.fail = 1;
+      }
+    }
+  }
+  __syncthreads();
+  if (S.fail) return false;
+  const int nc = S.nc;
+  // B3: bucket sizes
+  for (int i = tid; i < P; i += BS) {
+    const int t = sl.ct[i];
+    if (t < t_lo || t >= t_hi) continue;
+    atomicAdd(&S.u.b.cnt[S.u.b.slot[cand_find(S, t)]], 1u);
+  }
+  __syncthreads();
+  // B4: exclusive scan of cnt[0..nc) (MAXC / BS = 4 per thread, contiguous)
+  {
+    constexpr int PER = MAXC / BS;
+    int loc[PER];
+    int sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = tid * PER + j;
+      loc[j] = idx < nc ? (int)S.u.b.cnt[idx] : 0;
+      sum += loc[j];
+    }
+    int total;
+    int base = block_scan(sum, S.ws, total);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = tid * PER + j;
+      S.u.b.off[idx] = base;
+      base += loc[j];
+    }
+    __syncthreads();
+  }
+  if (degree_only) {
+    // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate.
+    // B5': accumulate degree per slot directly (no bucket scatter needed).
+    for (int i = tid; i < MAXC; i += BS) S.u.b.cnt[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < P; i += BS) {
+      const int t = sl.ct[i];
+      if (t < t_lo || t >= t_hi) continue;
+      const int s = S.u.b.slot[cand_find(S, t)];
+      atomicAdd(&S.u.b.cnt[s], sl.cc[i] * (uint32_t)p.rl.node_nrules[sl.cn[i]]);
+    }
+    __syncthreads();
+    for (int s = tid; s < nc; s += BS) {
+      const float degf = (float)((double)S.u.b.cnt[s] + 1.0);
+      const double fx = (double)logf(degf) * 4294967296.0;  // 2^32 fixed point
+      atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint(fx));
+    }
+    __syncthreads();
+    return true;
+  }
+  // B5: scatter (node, count) into buckets
+  for (int i = tid; i < MAXC; i += BS) S.u.b.cnt[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < P; i += BS) {
+    const int t = sl.ct[i];
+    if (t < t_lo || t >= t_hi) continue;
+    const int s = S.u.b.slot[cand_find(S, t)];
+    const int pos = S.u.b.off[s] + (int)atomicAdd(&S.u.b.cnt[s], 1u);
+    sl.bn[pos] = sl.cn[i];
+    sl.bc[pos] = sl.cc[i];
+  }
+  __syncthreads();
+  // B6: one lane per candidate
+  for (int s = tid; s < nc; s += BS)
+    score_candidate<AGG>(p, S, sl, q, S.u.b.st[s], S.u.b.off[s], (int)S.u.b.cnt[s], mean_scale);
+  __syncthreads();
+  return true;
+}
+
+// Runs candidates_pass over entity ranges [0, E) split into np pieces; a
+// range whose candidates overflow the LDS tables (detected before anything is
+// written) is split in two and redone.  Returns the number of candidates.
+template <int AGG>
+__device__ int run_passes(const KParams &p, Smem &S, const Slot &sl, int q, int P, int np, bool degree_only,
+                          float mean_scale) {
+  const int tid = threadIdx.x;
+  if (tid == 0) S.sp = 0;
+  int next = 0, cnt = 0;
+#pragma unroll 1
+  while (true) {
+    __syncthreads();
+    const int sp = S.sp;
+    int lo, hi;
+    if (sp > 0) {
+      lo = S.stk_lo[sp - 1];
+      hi = S.stk_hi[sp - 1];
+    } else if (next < np) {
+      lo = (int)((int64_t)next * p.g.E / np);
+      hi = (int)((int64_t)(next + 1) * p.g.E / np);
+      ++next;
+    } else {
+      break;
+    }
+    __syncthreads();
+    if (tid == 0 && sp > 0) S.sp = sp - 1;
+    const bool ok = candidates_pass<AGG>(p, S, sl, q, P, lo, hi, degree_only, mean_scale);
+    if (ok) {
+      cnt += S.nc;
+    } else if (tid == 0) {
+      const int mid = lo + (hi - lo) / 2;
+      if (S.sp + 2 <= 32 && hi - lo > 1) {
+        S.stk_lo[S.sp] = mid;
+        S.stk_hi[S.sp] = hi;
+        S.stk_lo[S.sp + 1] = lo;
+        S.stk_hi[S.sp + 1] = mid;
+        S.sp += 2;
+      } else {
+        S.ovf = 1;
+      }
+    }
+  }
+  return cnt;
+}
+
+// ---------------------------------------------------------------- phase A
+__device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, int h, int r, int root, int rm_src,
+                             int rm_dst) {
+  const int tid = threadIdx.x;
+  const int E = p.g.E, R = p.g.R;
+  const int depth = p.rl.head_depth[r];
+  if (tid == 0) {
+    sl.fn[0][0] = root;
+    sl.fv[0][0] = h;
+    sl.fc[0][0] = 1u;
+    if (p.rl.node_nrules[root] > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
+  }
+  __syncthreads();
+  int cur = 0, n_prev = 1;
+  for (int d = 1; d <= depth; ++d) {
+    const int nxt = cur ^ 1;
+    for (int cb = 0; cb < n_prev; cb += BS) {
+      const int ne = min(BS, n_prev - cb);
+      int nch = 0;
+      if (tid < ne) {
+        const int node = sl.fn[cur][cb + tid];
+        S.ent_v[tid] = sl.fv[cur][cb + tid];
+        S.ent_c[tid] = sl.fc[cur][cb + tid];
+        S.ent_fch[tid] = p.rl.node_child[node];
+        nch = p.rl.node_nchild[node];
+      }
+      int NI;
+      const int ioff = block_scan(nch, S.ws, NI);
+      S.item_off[tid] = ioff;
+      __syncthreads();
+      for (int ib = 0; ib < NI; ib += BS) {
+        const int k = ib + tid;
+        int deg = 0;
+        if (k < NI) {
+          const int ent = upper_idx(S.item_off, ne, k);
+          const int child = S.ent_fch[ent] + (k - S.item_off[ent]);
+          const int rel = p.rl.node_rel[child];
+          const int v = S.ent_v[ent];
+          const int64_t o = (int64_t)v * R + rel;
+          const int beg = p.g.off[o];
+          deg = p.g.off[o + 1] - beg;
+          S.it_child[tid] = child;
+          S.it_beg[tid] = beg;
+          S.it_v[tid] = v;
+          S.it_rel[tid] = rel;
+          S.it_c[tid] = S.ent_c[ent];
+          S.it_flags[tid] = (p.rl.node_nrules[child] > 0 ? 1 : 0) | (p.rl.node_nchild[child] > 0 ? 2 : 0);
+        }
+        int NE;
+        const int eoff = block_scan(deg, S.ws, NE);
+        S.edge_off[tid] = eoff;
+        __syncthreads();
+        const int nit = min(BS, NI - ib);
+        for (int eb = 0; eb < NE; eb += BS) {
+          const int j = eb + tid;
+          if (j < NE) {
+            const int it = upper_idx(S.edge_off, nit, j);
+            const int tt = p.g.col[S.it_beg[it] + (j - S.edge_off[it])];
+            const int rel = S.it_rel[it];
+            if (!(rel == r && S.it_v[it] == rm_src && tt == rm_dst)) {
+              const int child = S.it_child[it];
+              const uint32_t c = S.it_c[it];
+              const int fl = S.it_flags[it];
+              if (fl & 1) emit_contrib(S, sl, p.pcap, tt, child, c);
+              if (fl & 2) {
+                if (!hash_add(S, (child - root) * E + tt, c)) emit_frontier(S, sl, nxt, p.fcap, child, tt, c);
+              }
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // compact the hash into the next frontier and clear it
+    for (int s = tid; s < HCAP; s += BS) {
+      const int k = S.u.a.key[s];
+      if (k != EMPTY) {
+        emit_frontier(S, sl, nxt, p.fcap, root + k / E, k % E, S.u.a.val[s]);
+        S.u.a.key[s] = EMPTY;
+        S.u.a.val[s] = 0u;
+      }
+    }
+    __syncthreads();
+    n_prev = min((int64_t)S.nd, p.fcap);
+    __syncthreads();
+    if (tid == 0) S.nd = 0;
+    cur = nxt;
+    __syncthreads();
+  }
+}
+
+template <int AGG>
+__global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
+  __shared__ Smem S;
+  const int tid = threadIdx.x;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  const Slot sl = make_slot(p.ws, blockIdx.x, p.fcap, p.pcap);
+  for (int s = tid; s < HCAP; s += BS) {
+    S.u.a.key[s] = EMPTY;
+    S.u.a.val[s] = 0u;
+  }
+  __syncthreads();
+#pragma unroll 1
+  while (true) {
+    if (tid == 0) S.q = (int)atomicAdd(&hdr[1], 1u);
+    __syncthreads();
+    const int q = S.q;
+    if (q >= p.nq) break;
+    const int h = (int)p.all_h[q];
+    const int r = (int)p.all_r[q];
+    const int root = p.rl.head_root[r];
+    if (root < 0) {
+      if (tid == 0) {
+        if (p.n_cand) p.n_cand[q] = 0;
+        if (p.digest) p.digest[q] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    int rm_src = -1, rm_dst = -1;
+    if (p.etr) {
+      const int64_t e = p.etr[q];
+      if (e >= 0) {
+        const int base = p.g.edge_base[r];
+        rm_src = p.g.edge_src[base + e];
+        rm_dst = p.g.edge_dst[base + e];
+      }
+    }
+    if (tid == 0) {
+      S.np = 0;
+      S.nd = 0;
+      S.ovf = 0;
+      S.sumlog = 0ull;
+      S.dig = 0ull;
+    }
+    if (tid < 128) {
+      // relation half of score_model.layers.0 folded into a per-query bias
+      float acc = p.s0_b[tid];
+      for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[tid * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+      S.relb[tid] = acc;
+    }
+    __syncthreads();
+    ground_query(p, S, sl, q, h, r, root, rm_src, rm_dst);
+    __syncthreads();
+    const int P = S.np;
+    if (S.ovf || P > p.pcap) {
+      // leave the LDS hash clean for the next query
+      for (int s = tid; s < HCAP; s += BS) {
+        S.u.a.key[s] = EMPTY;
+        S.u.a.val[s] = 0u;
+      }
+      if (tid == 0) {
+        atomicOr(&hdr[0], 1u);
+        if (p.n_cand) p.n_cand[q] = -1;
+      }
+      __syncthreads();
+      continue;
+    }
+    const int np = max(1, (P + 2047) / 2048);
+    float mean_scale = 0.f;
+    if constexpr (AGG == RNNL_AGG_PNA) {
+      // sweep 1: per-query mean of log(degree) over candidates (layers.py:109-116)
+      if (tid == 0) S.sumlog = 0ull;
+      const int nc1 = run_passes<AGG>(p, S, sl, q, P, np, true, 0.f);
+      const double sum = (double)(long long)S.sumlog / 4294967296.0;
+      mean_scale = (float)((float)sum / fmaxf((float)nc1, 1e-6f));
+    }
+    if (tid == 0) S.dig = 0ull;
+    const int ncand = run_passes<AGG>(p, S, sl, q, P, np, false, mean_scale);
+    if (tid == 0) {
+      if (p.n_cand) p.n_cand[q] = ncand;
+      if (p.digest) p.digest[q] = S.dig;
+    }
+    // restore the phase-A hash (phase B reused its LDS)
+    for (int s = tid; s < HCAP; s += BS) {
+      S.u.a.key[s] = EMPTY;
+      S.u.a.val[s] = 0u;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- node weights
+__global__ void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, int ld, int agg,
+                                    unsigned char *__restrict__ out) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = (int)(gid >> 4), d = (int)(gid & 15);
+  if (n >= rl.n_nodes) return;
+  float s1 = 0.f, s2 = 0.f, mn = __builtin_huge_valf(), mx = -__builtin_huge_valf();
+  for (int k = rl.node_rule_ptr[n]; k < rl.node_rule_ptr[n + 1]; ++k) {
+    const float x = emb[(int64_t)rl.node_rules[k] * ld + d];
+    s1 += x;
+    s2 += x * x;
+    mn = fminf(mn, x);
+    mx = fmaxf(mx, x);
+  }
+  const double sc = (double)(1 << kFixShift);
+  if (agg == RNNL_AGG_SUM) {
+    long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStrideSum);
+    rec[d] = llrint((double)s1 * sc);
+  } else {
+    long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStridePna);
+    rec[d] = llrint((double)s1 * sc);
+    rec[16 + d] = llrint((double)s2 * sc);
+    float *fr = reinterpret_cast<float *>(rec + 32);
+    fr[d] = mn;
+    fr[16 + d] = mx;
+  }
+}
+
+}  // namespace rnnl
+
+using namespace rnnl;
+
+extern "C" {
+
+int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, void *node_w, void *stream) {
+  if (!r || !emb || !node_w || (agg != RNNL_AGG_SUM && agg != RNNL_AGG_PNA) || ld < 16) {
+    set_error("rnnl_node_weights: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const int64_t n = (int64_t)r->d.n_nodes * 16;
+  if (n == 0) return RNNL_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, (hipStream_t)stream,
+                     r->d, emb, ld, agg, static_cast<unsigned char *>(node_w));
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+static int nslots_for(int32_t nq) { return (int)std::min<int64_t>(nq, (int64_t)NUM_CU * WG_PER_CU); }
+
+int rnnl_forward_workspace_size(rnnl_graph g, rnnl_rules r, int32_t nq, int32_t scale, size_t *bytes) {
+  if (!g || !r || !bytes || nq < 0 || scale < 1) {
+    set_error("rnnl_forward_workspace_size: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const int64_t fcap = FCAP_BASE * scale, pcap = PCAP_BASE * scale;
+  *bytes = (size_t)(HDR_BYTES + (int64_t)std::max(1, nslots_for(nq)) * slot_bytes(fcap, pcap));
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
+                               const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
+                               int32_t *n_cand, uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale,
+                               void *stream) {
+  if (!g || !r || !pp || !all_h || !all_r || !score || !ws || nq < 0 || scale < 1 || !pp->node_w ||
+      (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA)) {
+    set_error("rnnl_predictorplus_forward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  size_t need = 0;
+  rnnl_forward_workspace_size(g, r, nq, scale, &need);
+  if (ws_bytes < need) {
+    set_error("rnnl_predictorplus_forward: workspace too small");
+    return RNNL_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  KParams p;
+  p.g = g->d;
+  p.rl = r->d;
+  p.agg = pp->aggregator;
+  p.feature = pp->feature;
+  p.node_w = static_cast<const unsigned char *>(pp->node_w);
+  p.add_w = pp->add_w;
+  p.add_b = pp->add_b;
+  p.ln_w = pp->ln_w;
+  p.ln_b = pp->ln_b;
+  p.s0_w = pp->s0_w;
+  p.s0_b = pp->s0_b;
+  p.s1_w = pp->s1_w;
+  p.s1_b = pp->s1_b;
+  p.rel_emb = pp->rel_emb;
+  p.all_h = all_h;
+  p.all_r = all_r;
+  p.etr = etr;
+  p.nq = nq;
+  p.score = score;
+  p.mask = mask;
+  p.n_cand = n_cand;
+  p.digest = digest;
+  p.ws = static_cast<unsigned char *>(ws);
+  p.fcap = FCAP_BASE * scale;
+  p.pcap = PCAP_BASE * scale;
+  p.nslots = nslots_for(nq);
+  if (pp->aggregator == RNNL_AGG_SUM)
+    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+  else
+    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_forward_status(void *ws, void *stream) {
+  unsigned int st = 0;
+  RNNL_HIP_CHECK(hipMemcpyAsync(&st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (st) {
+    set_error("rnnl_predictorplus_forward: workspace capacity exceeded");
+    return RNNL_ERR_OVERFLOW;
+  }
+  return RNNL_OK;
+}
+
+}  // extern "C"

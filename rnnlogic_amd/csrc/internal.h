@@ -1,0 +1,73 @@
+// Internal structures shared by the host builders (graph.cpp) and the HIP
+// kernels.  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/rnnlogic_hip.h"
+
+namespace rnnl {
+
+// Vertex-major CSR of the train graph: edges (v --rel--> t) for fixed (v, rel)
+// are col[off[v*R+rel] .. off[v*R+rel+1]), in train-file order.
+struct GraphDev {
+  int32_t E = 0, R = 0;
+  int64_t n_edges = 0;
+  const int32_t *off = nullptr;        // E*R + 1
+  const int32_t *col = nullptr;        // n_edges
+  const int32_t *edge_base = nullptr;  // R + 1: start of relation r's edge table
+  const int32_t *edge_src = nullptr;   // relation-major, relation-local file order
+  const int32_t *edge_dst = nullptr;
+};
+
+// Rule bodies as one prefix trie per head relation.  Node ids are global;
+// the nodes of one head are contiguous, numbered breadth-first, so the
+// children of a node are contiguous too.  Node 0 of a head is its root
+// (empty prefix, relation -1).
+struct RulesDev {
+  int32_t n_rules = 0, n_nodes = 0, max_depth = 0, n_heads = 0;
+  const int32_t *head_root = nullptr;   // R: root node id, -1 if the head has no rule
+  const int32_t *head_depth = nullptr;  // R: deepest body length of the head
+  const int32_t *head_nodes = nullptr;  // R: number of trie nodes of the head
+  const int32_t *node_rel = nullptr;    // relation of the edge into the node
+  const int32_t *node_child = nullptr;  // first child id
+  const int32_t *node_nchild = nullptr;
+  const int32_t *node_nrules = nullptr;    // rules whose body ends exactly here
+  const int32_t *node_rule_ptr = nullptr;  // n_nodes + 1
+  const int32_t *node_rules = nullptr;     // member rule ids, ascending
+  const uint64_t *node_fp = nullptr;       // sum of mix64(rule id) of members (digest only)
+};
+
+// Node-weight records (bytes per node); see rnnl_node_weights.
+constexpr int kHidden = 16;
+constexpr int kStrideSum = 128;  // int64 fix(sum x)[16]
+constexpr int kStridePna = 384;  // int64 fix(sum x)[16] | int64 fix(sum x^2)[16] | f32 min[16] | f32 max[16]
+constexpr int kFixShift = 28;    // fix(v) = round(v * 2^28)
+
+void set_error(const std::string &msg);
+
+}  // namespace rnnl
+
+struct rnnl_graph_s {
+  rnnl::GraphDev d;
+  int device = 0;
+  void *mem[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+};
+
+struct rnnl_rules_s {
+  rnnl::RulesDev d;
+  int device = 0;
+  int32_t R = 0, E = 0;
+  void *mem[11] = {};
+};
+
+#define RNNL_HIP_CHECK(expr)                                                              \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      rnnl::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                 \
+      return RNNL_ERR_HIP;                                                                \
+    }                                                                                     \
+  } while (0)

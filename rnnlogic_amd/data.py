@@ -1,0 +1,278 @@
+"""Knowledge graph + datasets, API-compatible with the reference's src/data.py.
+
+Names, attributes, batch composition and the order of `random` calls follow
+the reference exactly (file:line cited per symbol) so that run_predictorplus
+/ run_rnnlogic style drivers see identical batches.  What differs is where
+the graph lives: `KnowledgeGraph.device_graph(device)` uploads a vertex-major
+CSR once per GPU (rnnl_graph_create) and the PredictorPlus forward grounds
+rules there with the HIP kernel instead of the dense one-hot propagation of
+the reference (data.py:136-173).
+"""
+import os
+import random
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+from . import _native
+
+
+def _read_dict(path):
+    e2i, i2e = {}, {}
+    with open(path) as fi:
+        for line in fi:
+            i, name = line.strip().split("\t")
+            e2i[name] = int(i)
+            i2e[int(i)] = name
+    return e2i, i2e
+
+
+def _read_triples(path, e2i, r2i):
+    out = []
+    with open(path) as fi:
+        for line in fi:
+            h, r, t = line.strip().split("\t")
+            out.append((e2i[h], r2i[r], e2i[t]))
+    return out
+
+
+class KnowledgeGraph(object):
+    """Reference src/data.py:9-173."""
+
+    def __init__(self, data_path):
+        self.data_path = data_path
+        self.entity2id, self.id2entity = _read_dict(os.path.join(data_path, "entities.dict"))
+        self.relation2id, self.id2relation = _read_dict(os.path.join(data_path, "relations.dict"))
+        self.entity_size = len(self.entity2id)
+        self.relation_size = len(self.relation2id)
+
+        self.train_facts = _read_triples(os.path.join(data_path, "train.txt"), self.entity2id, self.relation2id)
+        self.valid_facts = _read_triples(os.path.join(data_path, "valid.txt"), self.entity2id, self.relation2id)
+        self.test_facts = _read_triples(os.path.join(data_path, "test.txt"), self.entity2id, self.relation2id)
+
+        E = self.entity_size
+        self.hr2o, self.hr2oo, self.hr2ooo = dict(), dict(), dict()
+        self.relation2ht2index = [dict() for _ in range(self.relation_size)]
+        for h, r, t in self.train_facts:  # data.py:43-71
+            k = self.encode_hr(h, r)
+            self.hr2o.setdefault(k, []).append(t)
+            self.hr2oo.setdefault(k, []).append(t)
+            self.hr2ooo.setdefault(k, []).append(t)
+            ht = self.encode_ht(h, t)
+            assert ht not in self.relation2ht2index[r]
+            self.relation2ht2index[r][ht] = len(self.relation2ht2index[r])
+        for h, r, t in self.valid_facts:  # data.py:73-87
+            k = self.encode_hr(h, r)
+            self.hr2oo.setdefault(k, []).append(t)
+            self.hr2ooo.setdefault(k, []).append(t)
+        for h, r, t in self.test_facts:  # data.py:89-99
+            self.hr2ooo.setdefault(self.encode_hr(h, r), []).append(t)
+
+        tr = np.asarray(self.train_facts, dtype=np.int64).reshape(-1, 3)
+        self._train = tr
+        # relation2adjacency[r] = [LongTensor(2, E_r) rows (tail, head), ones] (data.py:101-104)
+        self.relation2adjacency = []
+        self.relation2outdegree = []
+        for r in range(self.relation_size):
+            sel = tr[tr[:, 1] == r]
+            index = torch.from_numpy(np.stack([sel[:, 2], sel[:, 0]]).copy())
+            self.relation2adjacency.append([index, torch.ones(index.size(1))])
+            self.relation2outdegree.append(torch.from_numpy(np.bincount(sel[:, 2], minlength=E).astype(np.int64)))
+        self._device_graphs = {}
+        print("Data loading | DONE!")
+
+    # data.py:110-122
+    def encode_hr(self, h, r):
+        return r * self.entity_size + h
+
+    def decode_hr(self, index):
+        return index % self.entity_size, index // self.entity_size
+
+    def encode_ht(self, h, t):
+        return t * self.entity_size + h
+
+    def decode_ht(self, index):
+        return index % self.entity_size, index // self.entity_size
+
+    # ------------------------------------------------------------ device side
+    def device_graph(self, device):
+        """rnnl_graph handle (vertex-major CSR) on `device`, created once."""
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("the HIP graph lives on a GPU; got device %s" % device)
+        key = device.index if device.index is not None else torch.cuda.current_device()
+        if key not in self._device_graphs:
+            import ctypes
+            hrt = np.ascontiguousarray(self._train, dtype=np.int32)
+            h = ctypes.c_void_p()
+            with torch.cuda.device(key):
+                _native.call("rnnl_graph_create", hrt.ctypes.data_as(ctypes.c_void_p), len(hrt), self.entity_size,
+                             self.relation_size, ctypes.byref(h))
+            self._device_graphs[key] = _DeviceHandle(h, "rnnl_graph_destroy")
+        return self._device_graphs[key].ptr
+
+    # ------------------------------------------------------------ reference API
+    def grounding(self, h, r, rule, edges_to_remove):
+        """Path counts (B, |E|) int64 of `rule` from each h (data.py:136-147).
+
+        Auxiliary API (the PredictorPlus hot path grounds all rules of a batch
+        in one HIP launch instead); kept for callers such as Predictor."""
+        with torch.no_grad():
+            x = torch.nn.functional.one_hot(h, self.entity_size).transpose(0, 1).unsqueeze(-1)
+            for r_body in rule:
+                x = self.propagate(x, r_body, edges_to_remove if r_body == r else None)
+        return x.squeeze(-1).transpose(0, 1)
+
+    def propagate(self, x, relation, edges_to_remove=None):
+        """data.py:149-173 with the scatter-sum done by index_add_."""
+        device = x.device
+        node_in = self.relation2adjacency[relation][0][1].to(device)
+        node_out = self.relation2adjacency[relation][0][0].to(device)
+        message = x[node_in]
+        E, B, D = message.size()
+        if edges_to_remove is not None:
+            message = message.view(-1, D).clone()
+            message[edges_to_remove * B + torch.arange(B, device=device)] = 0
+            message = message.view(E, B, D)
+        out = torch.zeros((x.size(0), B, D), dtype=x.dtype, device=device)
+        return out.index_add_(0, node_out, message)
+
+
+class _DeviceHandle(object):
+    """Owns a native handle; destroyed with the Python object."""
+
+    def __init__(self, ptr, destroy):
+        self.ptr = ptr
+        self._destroy = destroy
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                getattr(_native.lib(), self._destroy)(self.ptr)
+        except Exception:
+            pass
+
+
+class TrainDataset(Dataset):
+    """Reference src/data.py:175-219."""
+
+    def __init__(self, graph, batch_size):
+        self.graph = graph
+        self.batch_size = batch_size
+        self.r2instances = [[] for _ in range(self.graph.relation_size)]
+        for h, r, t in self.graph.train_facts:
+            self.r2instances[r].append((h, r, t))
+        self.make_batches()
+
+    def make_batches(self):
+        for r in range(self.graph.relation_size):
+            random.shuffle(self.r2instances[r])
+        self.batches = list()
+        for r, instances in enumerate(self.r2instances):
+            for k in range(0, len(instances), self.batch_size):
+                self.batches.append(instances[k:min(k + self.batch_size, len(instances))])
+        random.shuffle(self.batches)
+
+    def __len__(self):
+        return len(self.batches)
+
+    def __getitem__(self, idx):
+        data = self.batches[idx]
+        all_h = torch.LongTensor([_[0] for _ in data])
+        all_r = torch.LongTensor([_[1] for _ in data])
+        all_t = torch.LongTensor([_[2] for _ in data])
+        target = torch.zeros(len(data), self.graph.entity_size)
+        edges_to_remove = []
+        for k, (h, r, t) in enumerate(data):
+            target[k][torch.LongTensor(self.graph.hr2o[self.graph.encode_hr(h, r)])] = 1
+            edges_to_remove.append(self.graph.relation2ht2index[r][self.graph.encode_ht(h, t)])
+        return all_h, all_r, all_t, target, torch.LongTensor(edges_to_remove)
+
+
+class _EvalDataset(Dataset):
+    facts_attr = None
+    filter_attr = None
+
+    def __init__(self, graph, batch_size):
+        self.graph = graph
+        self.batch_size = batch_size
+        r2instances = [[] for _ in range(self.graph.relation_size)]
+        for h, r, t in getattr(self.graph, self.facts_attr):
+            r2instances[r].append((h, r, t))
+        self.batches = list()
+        for r, instances in enumerate(r2instances):
+            random.shuffle(instances)
+            for k in range(0, len(instances), self.batch_size):
+                self.batches.append(instances[k:min(k + self.batch_size, len(instances))])
+
+    def __len__(self):
+        return len(self.batches)
+
+    def __getitem__(self, idx):
+        data = self.batches[idx]
+        all_h = torch.LongTensor([_[0] for _ in data])
+        all_r = torch.LongTensor([_[1] for _ in data])
+        all_t = torch.LongTensor([_[2] for _ in data])
+        mask = torch.ones(len(data), self.graph.entity_size).bool()
+        filt = getattr(self.graph, self.filter_attr)
+        for k, (h, r, t) in enumerate(data):
+            mask[k][torch.LongTensor(filt[self.graph.encode_hr(h, r)])] = 0
+        return all_h, all_r, all_t, mask
+
+
+class ValidDataset(_EvalDataset):
+    """Reference src/data.py:221-256 (filter: train+valid answers)."""
+    facts_attr, filter_attr = "valid_facts", "hr2oo"
+
+
+class TestDataset(_EvalDataset):
+    """Reference src/data.py:258-293 (filter: train+valid+test answers)."""
+    facts_attr, filter_attr = "test_facts", "hr2ooo"
+
+
+class RuleDataset(Dataset):
+    """Rule sequences for the LSTM generator (reference src/data.py:295-342).
+
+    Item k is ([head, body..., END], PAD, weight + 1e-5) with END = |R| and
+    PAD = |R| + 1; a rule file holds "head body... H" lines, H scaled by 1000.
+    Generator side: kept for the EM driver, not on the accelerated path."""
+
+    def __init__(self, num_relations, input):
+        self.num_relations = num_relations
+        self.ending_idx = num_relations
+        self.padding_idx = num_relations + 1
+        if isinstance(input, str):
+            with open(input, "r") as fi:
+                toks = [line.split() for line in fi]
+            rules = [[int(x) for x in t[:-1]] + [float(t[-1]) * 1000] for t in toks]
+        elif isinstance(input, list):
+            rules = input
+        else:
+            raise ValueError
+        self.rules = [[list(x[:-1]) + [self.ending_idx], self.padding_idx, x[-1] + 1e-5] for x in rules]
+
+    def __len__(self):
+        return len(self.rules)
+
+    def __getitem__(self, idx):
+        return self.rules[idx]
+
+    @staticmethod
+    def collate_fn(data):
+        seqs = [item[0] for item in data]
+        pads = torch.tensor([int(item[-2]) for item in data], dtype=torch.long)
+        L = max(len(s) for s in seqs) - 1
+        inputs = pads.unsqueeze(1).repeat(1, L)
+        target = pads.unsqueeze(1).repeat(1, L)
+        for k, s in enumerate(seqs):
+            inputs[k, :len(s) - 1] = torch.tensor(s[:-1], dtype=torch.long)
+            target[k, :len(s) - 1] = torch.tensor(s[1:], dtype=torch.long)
+        weight = torch.tensor([float(item[-1]) for item in data])
+        return inputs, target, target != pads.unsqueeze(1), weight
+
+
+def Iterator(dataloader):
+    """Endless iteration over a DataLoader (reference src/data.py:344-347)."""
+    while True:
+        yield from dataloader

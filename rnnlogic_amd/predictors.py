@@ -1,0 +1,341 @@
+"""Reasoning predictors, API-compatible with the reference's src/predictors.py.
+
+PredictorPlus keeps the reference's constructor, set_rules, encode_rules and
+forward signatures and its exact module tree (so state_dict keys/shapes match
+and a seeded construction consumes the RNG identically).  Its forward runs on
+the HIP path:
+
+    rule embeddings (emb table or LSTM encoder, torch)         predictors.py:201-208, 246-249
+      -> per-trie-node aggregates          rnnl_node_weights (HIP)
+    base score  bias row / RotatE / -inf   rnnl_fill_rows / rnnl_rotate_score (HIP)
+    grounding + aggregation + MLP          rnnl_predictorplus_forward (HIP, one launch)
+
+There is no CPU fallback: on a CPU tensor forward() raises.
+"""
+import ctypes
+import logging
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _native
+from .data import _DeviceHandle
+from .embedding import RotatE
+from .layers import MLP, FuncToNode, FuncToNodeSum
+
+
+def _read_rules(input):
+    """Rule list/file -> [(head, [body...])] (predictors.py:27-41, 166-182)."""
+    rules = []
+    if isinstance(input, list):
+        for rule in input:
+            rules.append((rule[0], list(rule[1:])))
+    elif isinstance(input, str):
+        with open(input, "r") as fi:
+            for line in fi:
+                rule = [int(_) for _ in line.strip().split()]
+                rules.append((rule[0], rule[1:]))
+    else:
+        raise ValueError
+    return rules
+
+
+class _NativeRules(object):
+    """Per-device rnnl_rules handle (prefix tries of the rule bodies)."""
+
+    def __init__(self, graph, rules, device):
+        import numpy as np
+        flat, ptr = [], [0]
+        for head, body in rules:
+            flat.append(head)
+            flat.extend(body)
+            ptr.append(len(flat))
+        tok = np.ascontiguousarray(flat, dtype=np.int32)
+        ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _native.call("rnnl_rules_create", graph.device_graph(device), tok.ctypes.data_as(ctypes.c_void_p),
+                         ptr.ctypes.data_as(ctypes.c_void_p), len(rules), ctypes.byref(h))
+        self.handle = _DeviceHandle(h, "rnnl_rules_destroy")
+        info = (ctypes.c_int32 * 5)()
+        _native.call("rnnl_rules_info", h, info)
+        self.n_rules, self.n_nodes, self.max_depth = info[0], info[1], info[2]
+        self.record_bytes = (info[3], info[4])
+
+    @property
+    def ptr(self):
+        return self.handle.ptr
+
+
+class Predictor(torch.nn.Module):
+    """Rule-weight predictor of the EM loop (reference src/predictors.py:17-119).
+
+    score = sum_rho count_rho * w_rho (+ bias).  Grounds through
+    KnowledgeGraph.grounding (torch ops on the batch's device)."""
+
+    def __init__(self, graph, entity_feature="bias"):
+        super(Predictor, self).__init__()
+        self.graph = graph
+        self.num_entities = graph.entity_size
+        self.num_relations = graph.relation_size
+        self.entity_feature = entity_feature
+        if entity_feature == "bias":
+            self.bias = torch.nn.parameter.Parameter(torch.zeros(self.num_entities))
+
+    def set_rules(self, input):
+        self.rules = _read_rules(input)
+        logging.info("Predictor: read {} rules from {}.".format(len(self.rules),
+                                                               "list" if isinstance(input, list) else "file"))
+        self.num_rules = len(self.rules)
+        self.relation2rules = [[] for _ in range(self.num_relations)]
+        for index, rule in enumerate(self.rules):
+            self.relation2rules[rule[0]].append([index, rule])
+        self.rule_weights = torch.nn.parameter.Parameter(torch.zeros(self.num_rules))
+
+    def _counts(self, all_h, all_r, edges_to_remove):
+        query_r = all_r[0].item()
+        assert (all_r != query_r).sum() == 0
+        for index, (r_head, r_body) in self.relation2rules[query_r]:
+            assert r_head == query_r
+            yield index, self.graph.grounding(all_h, r_head, r_body, edges_to_remove)
+
+    def forward(self, all_h, all_r, edges_to_remove):
+        device = all_r.device
+        score = torch.zeros(all_r.size(0), self.num_entities, device=device)
+        mask = torch.zeros(all_r.size(0), self.num_entities, device=device)
+        for index, x in self._counts(all_h, all_r, edges_to_remove):
+            score = score + x * self.rule_weights[index]
+            mask += x
+        if mask.sum().item() == 0:
+            if self.entity_feature == "bias":
+                return mask + self.bias.unsqueeze(0), (1 - mask).bool()
+            return mask - float("-inf"), mask.bool()
+        if self.entity_feature == "bias":
+            return score + self.bias.unsqueeze(0), torch.ones_like(mask).bool()
+        mask = mask != 0
+        return score.masked_fill(~mask, float("-inf")), mask
+
+    def compute_H(self, all_h, all_r, all_t, edges_to_remove):
+        """Per-rule H scores (predictors.py:82-119)."""
+        device = all_r.device
+        rule_score, rule_index = [], []
+        mask = torch.zeros(all_r.size(0), self.num_entities, device=device)
+        for index, x in self._counts(all_h, all_r, edges_to_remove):
+            rule_score.append(x * self.rule_weights[index])
+            rule_index.append(index)
+            mask += x
+        if len(rule_score) == 0:
+            return None, None
+        rule_index = torch.tensor(rule_index, dtype=torch.long, device=device)
+        pos = torch.nn.functional.one_hot(all_t, self.num_entities).bool().to(device)
+        neg = mask != 0
+        H = []
+        for s in rule_score:
+            ps = (s * pos).sum(1) / torch.clamp(pos.sum(1), min=1)
+            ns = (s * neg).sum(1) / torch.clamp(neg.sum(1), min=1)
+            H.append((ps - ns).unsqueeze(-1))
+        return torch.softmax(torch.cat(H, dim=-1), dim=-1).sum(0), rule_index
+
+
+class PredictorPlus(torch.nn.Module):
+    """Reference src/predictors.py:121-271, forward on the HIP path."""
+
+    def __init__(self, graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="bias", aggregator="sum",
+                 embedding_path=None):
+        super(PredictorPlus, self).__init__()
+        self.graph = graph
+        self.type = type
+        self.num_layers = num_layers
+        self.hidden_dim = hidden_dim
+        self.entity_feature = entity_feature
+        self.aggregator = aggregator
+        self.embedding_path = embedding_path
+        self.num_entities = graph.entity_size
+        self.num_relations = graph.relation_size
+        self.padding_index = graph.relation_size
+        if hidden_dim != 16:
+            raise NotImplementedError("the HIP kernels are specialised for hidden_dim == 16 (reference default)")
+
+        # module creation order == reference (identical RNG consumption under set_seed)
+        self.vocab_emb = torch.nn.Embedding(self.num_relations + 1, self.hidden_dim, padding_idx=self.num_relations)
+        if self.type == "lstm":
+            self.rnn = torch.nn.LSTM(self.hidden_dim, self.hidden_dim, self.num_layers, batch_first=True)
+        elif self.type == "gru":
+            self.rnn = torch.nn.GRU(self.hidden_dim, self.hidden_dim, self.num_layers, batch_first=True)
+        elif self.type == "rnn":
+            self.rnn = torch.nn.RNN(self.hidden_dim, self.hidden_dim, self.num_layers, batch_first=True)
+        elif self.type == "emb":
+            self.rule_emb = None
+        else:
+            raise NotImplementedError
+        if aggregator == "sum":
+            self.rule_to_entity = FuncToNodeSum(self.hidden_dim)
+        elif aggregator == "pna":
+            self.rule_to_entity = FuncToNode(self.hidden_dim)
+        else:
+            raise NotImplementedError
+        self.relation_emb = torch.nn.Embedding(self.num_relations, self.hidden_dim)
+        self.score_model = MLP(self.hidden_dim * 2, [128, 1])
+        if entity_feature == "bias":
+            self.bias = torch.nn.parameter.Parameter(torch.zeros(self.num_entities))
+        elif entity_feature == "RotatE":
+            self.RotatE = RotatE(embedding_path)
+        self._native_rules = {}
+        self._node_cache = {}
+        self._ws = {}
+        self.capacity_scale = 1
+
+    # ------------------------------------------------------------------ rules
+    def set_rules(self, input):
+        self.rules = _read_rules(input)
+        logging.info("Predictor+: read {} rules from {}.".format(len(self.rules),
+                                                                "list" if isinstance(input, list) else "file"))
+        self.num_rules = len(self.rules)
+        self.max_length = max([len(rule[1]) for rule in self.rules])
+        self.relation2rules = [[] for _ in range(self.num_relations)]
+        for index, rule in enumerate(self.rules):
+            self.relation2rules[rule[0]].append([index, rule])
+        self.rule_features = torch.tensor(
+            [[h] + b + [self.padding_index] * (self.max_length - len(b)) for h, b in self.rules], dtype=torch.long)
+        if self.type == "emb":
+            self.rule_emb = nn.parameter.Parameter(torch.zeros(self.num_rules, self.hidden_dim))
+            nn.init.kaiming_uniform_(self.rule_emb, a=math.sqrt(5), mode="fan_in")
+        self._native_rules = {}
+        self._node_cache = {}
+
+    def encode_rules(self, rule_features):
+        """LSTM/GRU/RNN output at each rule's last token (predictors.py:201-208)."""
+        rule_masks = rule_features != self.num_relations
+        output, _ = self.rnn(self.vocab_emb(rule_features))
+        idx = (rule_masks.sum(-1) - 1).long()
+        return output.gather(1, idx.view(-1, 1, 1).expand(-1, 1, self.hidden_dim)).squeeze(1)
+
+    # ------------------------------------------------------------------ native plumbing
+    def _device_index(self, device):
+        return device.index if device.index is not None else torch.cuda.current_device()
+
+    def native_rules(self, device):
+        key = self._device_index(device)
+        if key not in self._native_rules:
+            self._native_rules[key] = _NativeRules(self.graph, self.rules, key)
+        return self._native_rules[key]
+
+    def _embedding_sources(self):
+        if self.type == "emb":
+            return [self.rule_emb]
+        return [self.vocab_emb.weight] + list(self.rnn.parameters())
+
+    def all_rule_embeddings(self):
+        """(num_rules, 16) embeddings of every rule, in rule-id order."""
+        if self.type == "emb":
+            return self.rule_emb
+        return self.encode_rules(self.rule_features.to(self.vocab_emb.weight.device))
+
+    def node_weights(self, device):
+        """Per-trie-node aggregates of the rule embeddings (HIP), cached until a
+        source parameter changes (optimizer steps bump `_version`)."""
+        nr = self.native_rules(device)
+        key = (self._device_index(device), self.aggregator,
+               tuple((p.data_ptr(), p._version) for p in self._embedding_sources()))
+        hit = self._node_cache.get(device)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        with torch.no_grad():
+            emb = self.all_rule_embeddings().detach().float().contiguous()
+        agg = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
+        nbytes = nr.record_bytes[agg] * max(nr.n_nodes, 1)
+        w = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg, w.data_ptr(),
+                     torch.cuda.current_stream(device).cuda_stream)
+        self._node_cache[device] = (key, w, emb)
+        return w
+
+    def _workspace(self, device, nq, scale):
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        need = ctypes.c_size_t()
+        _native.call("rnnl_forward_workspace_size", g, nr.ptr, nq, scale, ctypes.byref(need))
+        ws = self._ws.get(device)
+        if ws is None or ws.numel() < need.value:
+            ws = torch.empty(need.value, dtype=torch.uint8, device=device)
+            self._ws[device] = ws
+        return ws
+
+    def _params(self, device, node_w):
+        rte, sm = self.rule_to_entity, self.score_model
+        p = _native.PredictorParams()
+        p.aggregator = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
+        p.feature = _native.FEATURE_ADD if self.entity_feature in ("bias", "RotatE") else _native.FEATURE_NONE
+        p.node_w = node_w.data_ptr()
+        tensors = [rte.add_model.layers[0].weight, rte.add_model.layers[0].bias, rte.layer_norm.weight,
+                   rte.layer_norm.bias, sm.layers[0].weight, sm.layers[0].bias, sm.layers[1].weight,
+                   sm.layers[1].bias, self.relation_emb.weight]
+        keep = [t.detach().float().contiguous() for t in tensors]
+        (p.add_w, p.add_b, p.ln_w, p.ln_b, p.s0_w, p.s0_b, p.s1_w, p.s1_b,
+         p.rel_emb) = [t.data_ptr() for t in keep]
+        return p, keep
+
+    def base_score(self, all_h, all_r, out):
+        """Entity-feature part of the score (predictors.py:260-269)."""
+        stream = torch.cuda.current_stream(out.device).cuda_stream
+        nq = all_h.numel()
+        if self.entity_feature == "bias":
+            b = self.bias.detach().float().contiguous()
+            _native.call("rnnl_fill_rows", b.data_ptr(), nq, self.num_entities, out.data_ptr(), stream)
+        elif self.entity_feature == "RotatE":
+            self.RotatE.score_into(all_h, all_r, out, accumulate=False)
+        else:
+            _native.call("rnnl_fill_value", float("-inf"), out.numel(), out.data_ptr(), stream)
+
+    def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False, digest=None):
+        """Forward for any rows (one or many reference batches, mixed relations).
+
+        Returns (score (n, |E|) f32, mask (n, |E|) bool[, n_cand (n,) int32])."""
+        device = all_h.device
+        if device.type != "cuda":
+            raise RuntimeError("PredictorPlus runs on the HIP path: move inputs and model to a GPU")
+        all_h = all_h.to(torch.int64).contiguous()
+        all_r = all_r.to(torch.int64).contiguous()
+        etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
+        nq = all_h.numel()
+        g = self.graph.device_graph(device)
+        nr = self.native_rules(device)
+        node_w = self.node_weights(device)
+        params, keep = self._params(device, node_w)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
+        none_mode = params.feature == _native.FEATURE_NONE
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        while True:
+            self.base_score(all_h, all_r, score)
+            mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
+            scale = self.capacity_scale
+            ws = self._workspace(device, nq, scale)
+            _native.call("rnnl_predictorplus_forward", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
+                         all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
+                         mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(),
+                         digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
+                         stream)
+            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
+            if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
+                self.capacity_scale *= 2
+                logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
+                continue
+            _native.check(rc)
+            break
+        del keep
+        if none_mode:
+            mask = mask8.bool()
+        else:
+            mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
+        return (score, mask, n_cand) if return_ncand else (score, mask)
+
+    def forward(self, all_h, all_r, edges_to_remove):
+        """predictors.py:210-271: one single-relation batch -> (score, mask)."""
+        query_r = all_r[0].item()
+        assert (all_r != query_r).sum() == 0
+        score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
+        if self.entity_feature not in ("bias", "RotatE") and int(n_cand.sum().item()) == 0:
+            # reference early return `mask - float('-inf')` (predictors.py:236-237): +inf, mask all False
+            score.fill_(float("inf"))
+        return score, mask
