@@ -20,12 +20,15 @@ import os
 import numpy as np
 
 ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
-BUILD = os.path.join(ROOT, "_build")
+# generated datasets (synthetic train graphs, RotatE tables) live outside the repo
+BUILD = os.environ.get("RNNL_DATA_BUILD", "/tmp/rnnlogic_amd_data")
 
 # Forward-triple counts of the real train splits (inverses are added on top).
 PACKED = {
-    "FB15k-237": dict(npz="fb15k237.npz", n_forward=272115, rotate_dim=1000, rotate_gamma=9.0),
-    "wn18rr": dict(npz="wn18rr.npz", n_forward=86835, rotate_dim=500, rotate_gamma=6.0),
+    "FB15k-237": dict(npz="fb15k237.npz", n_forward=272115, rotate_dim=1000, rotate_gamma=9.0,
+                      sha256="bbe41f4a41d09309ca48ca0a3b971289c346215f8e0b2a2d5405962adeaec62c"),
+    "wn18rr": dict(npz="wn18rr.npz", n_forward=86835, rotate_dim=500, rotate_gamma=6.0,
+                   sha256="ade9fcb41fe32293d6b960968633b99b3c1196e45a703e51b1af33e285554e07"),
 }
 SHIPPED = ("umls", "kinship")
 
@@ -109,7 +112,8 @@ def materialize(name, root=None, with_rotate=False):
     """Return a directory in the reference's format for dataset `name`.
 
     Shipped datasets return their in-repo directory.  Packed ones are written
-    once under data/_build/<name>/ (names are synthetic: e<id>, r<id>).
+    once under $RNNL_DATA_BUILD/<name>/ (default /tmp/rnnlogic_amd_data; names
+    are synthetic: e<id>, r<id>).
     """
     if name in SHIPPED:
         return os.path.join(ROOT, name)
@@ -117,40 +121,54 @@ def materialize(name, root=None, with_rotate=False):
         raise KeyError(name)
     spec = PACKED[name]
     out = os.path.join(root or BUILD, name)
-    stamp = os.path.join(out, "manifest.json")
-    if not os.path.exists(stamp):
-        os.makedirs(out, exist_ok=True)
+    if not os.path.exists(os.path.join(out, "manifest.json")):
+        # build in a private directory, then rename: concurrent ranks never see a partial dataset
+        tmp = "%s.tmp.%d" % (out, os.getpid())
+        os.makedirs(tmp, exist_ok=True)
         z = np.load(os.path.join(ROOT, spec["npz"]), allow_pickle=False)
         n_e, n_r = int(z["n_entities"]), int(z["n_relations"])
-        with open(os.path.join(out, "entities.dict"), "w") as f:
+        with open(os.path.join(tmp, "entities.dict"), "w") as f:
             f.write("".join("%d\te%d\n" % (i, i) for i in range(n_e)))
-        with open(os.path.join(out, "relations.dict"), "w") as f:
+        with open(os.path.join(tmp, "relations.dict"), "w") as f:
             f.write("".join("%d\tr%d\n" % (i, i) for i in range(n_r)))
         train = synthesize_train(n_e, n_r, z["valid"], z["test"], spec["n_forward"])
-        _write_triples(os.path.join(out, "train.txt"), train)
-        _write_triples(os.path.join(out, "valid.txt"), z["valid"])
-        _write_triples(os.path.join(out, "test.txt"), z["test"])
+        _write_triples(os.path.join(tmp, "train.txt"), train)
+        _write_triples(os.path.join(tmp, "valid.txt"), z["valid"])
+        _write_triples(os.path.join(tmp, "test.txt"), z["test"])
         flat, ptr = z["rules_flat"], z["rules_ptr"]
-        with open(os.path.join(out, "rnnlogic_rules.txt"), "w") as f:
+        with open(os.path.join(tmp, "rnnlogic_rules.txt"), "w") as f:
             f.write("".join(" ".join(map(str, flat[ptr[i]:ptr[i + 1]].tolist())) + "\n"
                             for i in range(len(ptr) - 1)))
-        man = {"train_sha256": _sha256(os.path.join(out, "train.txt")), "n_train": int(len(train)),
-               "seed": 0}
-        with open(stamp + ".tmp", "w") as f:
-            json.dump(man, f)
-        os.replace(stamp + ".tmp", stamp)
+        digest = _sha256(os.path.join(tmp, "train.txt"))
+        if digest != spec["sha256"]:
+            raise RuntimeError("synthetic %s train graph differs from the one the golden fixtures were made "
+                               "with (sha256 %s != %s)" % (name, digest, spec["sha256"]))
+        with open(os.path.join(tmp, "manifest.json"), "w") as f:
+            json.dump({"train_sha256": digest, "n_train": int(len(train)), "seed": 0}, f)
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        try:
+            os.rename(tmp, out)
+        except OSError:  # another process won the race
+            import shutil
+            shutil.rmtree(tmp, ignore_errors=True)
     if with_rotate:
         rdir = os.path.join(out, "RotatE_%d" % spec["rotate_dim"])
         if not os.path.exists(os.path.join(rdir, "config.json")):
-            os.makedirs(rdir, exist_ok=True)
+            tmp = "%s.tmp.%d" % (rdir, os.getpid())
+            os.makedirs(tmp, exist_ok=True)
             z = np.load(os.path.join(ROOT, spec["npz"]), allow_pickle=False)
             n_e, n_r = int(z["n_entities"]), int(z["n_relations"])
             eemb, remb = synthesize_rotate(n_e, n_r // 2, spec["rotate_dim"], spec["rotate_gamma"])
-            np.save(os.path.join(rdir, "entity_embedding.npy"), eemb)
-            np.save(os.path.join(rdir, "relation_embedding.npy"), remb)
-            with open(os.path.join(rdir, "config.json"), "w") as f:
+            np.save(os.path.join(tmp, "entity_embedding.npy"), eemb)
+            np.save(os.path.join(tmp, "relation_embedding.npy"), remb)
+            with open(os.path.join(tmp, "config.json"), "w") as f:
                 json.dump({"hidden_dim": spec["rotate_dim"], "gamma": spec["rotate_gamma"],
                            "nentity": n_e, "nrelation": n_r // 2, "synthetic": True}, f)
+            try:
+                os.rename(tmp, rdir)
+            except OSError:
+                import shutil
+                shutil.rmtree(tmp, ignore_errors=True)
     return out
 
 
