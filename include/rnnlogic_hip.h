@@ -123,6 +123,10 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */
 int rnnl_forward_status(void *workspace, void *stream);
+/* Diagnostic: when non-NULL, later forward launches add per-phase cycle
+ * counters into dev_counters (6 x uint64: prologue, grounding, candidates,
+ * queries, contributions, candidates). */
+int rnnl_debug_profile(void *dev_counters);
 
 /* --------------------------------------------------------- entity feature --
  * Base-score fills (reference src/predictors.py:260-269). */

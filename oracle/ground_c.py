@@ -120,7 +120,15 @@ class RefMiner:
         self.lib = ctypes.CDLL(REF_LIB)
         self.lib.ref_kg_load.restype = _P
         self.lib.ref_out_test_timed.restype = ctypes.c_double
-        self.kg = self.lib.ref_kg_load(data_path.encode())
+        import sys
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            self.kg = self.lib.ref_kg_load(data_path.encode())
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
 
     def rule_destination(self, e, body, rm=(-1, -1, -1), cap=1 << 20):
         b = np.asarray(body, dtype=np.int32)
@@ -137,8 +145,17 @@ class RefMiner:
             flat += [hd, len(body)] + list(body)
         f = np.asarray(flat, dtype=np.int32)
         n = ctypes.c_longlong(0)
-        sec = self.lib.ref_out_test_timed(_P(self.kg), _ptr(f), len(rules), int(threads), int(sample),
-                                          ctypes.byref(n))
+        # the miner prints progress on stdout: send it to stderr for the call
+        import sys
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            sec = self.lib.ref_out_test_timed(_P(self.kg), _ptr(f), len(rules), int(threads), int(sample),
+                                              ctypes.byref(n))
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         return sec, n.value
 
     def close(self):

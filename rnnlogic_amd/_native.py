@@ -35,6 +35,7 @@ SIGNATURES = [
     ("rnnl_predictorplus_forward", ctypes.c_int,
      [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
+    ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
     ("rnnl_rotate_transpose", ctypes.c_int, [_P, _I32, _I32, _P, _P]),

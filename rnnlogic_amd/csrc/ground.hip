@@ -56,7 +56,11 @@ struct KParams {
   unsigned char *ws;
   int64_t fcap, pcap;
   int32_t nslots;
+  unsigned long long *prof;  // diagnostic phase cycle counters (nullable)
 };
+
+// Diagnostic: phase cycle counters of the next launches (rnnl_debug_profile).
+static unsigned long long *g_prof = nullptr;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ULL;
@@ -594,12 +598,15 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
     S.u.a.val[s] = 0u;
   }
   __syncthreads();
+  unsigned long long pr[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t_q = 0, t_a = 0;
 #pragma unroll 1
   while (true) {
     if (tid == 0) S.q = (int)atomicAdd(&hdr[1], 1u);
     __syncthreads();
     const int q = S.q;
     if (q >= p.nq) break;
+    if (p.prof && tid == 0) t_q = __builtin_amdgcn_s_memtime();
     const int h = (int)p.all_h[q];
     const int r = (int)p.all_r[q];
     const int root = p.rl.head_root[r];
@@ -634,8 +641,15 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
       S.relb[tid] = acc;
     }
     __syncthreads();
+    if (p.prof && tid == 0) t_a = __builtin_amdgcn_s_memtime();
     ground_query(p, S, sl, q, h, r, root, rm_src, rm_dst);
     __syncthreads();
+    if (p.prof && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      pr[1] += t - t_a;
+      pr[0] += t_a - t_q;
+      t_a = t;
+    }
     const int P = S.np;
     if (S.ovf || P > p.pcap) {
       // leave the LDS hash clean for the next query
@@ -664,6 +678,12 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
     if (tid == 0) {
       if (p.n_cand) p.n_cand[q] = ncand;
       if (p.digest) p.digest[q] = S.dig;
+      if (p.prof) {
+        pr[2] += __builtin_amdgcn_s_memtime() - t_a;
+        pr[3] += 1;
+        pr[4] += P;
+        pr[5] += ncand;
+      }
     }
     // restore the phase-A hash (phase B reused its LDS)
     for (int s = tid; s < HCAP; s += BS) {
@@ -672,6 +692,8 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
     }
     __syncthreads();
   }
+  if (p.prof && tid == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[k], pr[k]);
 }
 
 // ---------------------------------------------------------------- node weights
@@ -779,11 +801,17 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   p.fcap = FCAP_BASE * scale;
   p.pcap = PCAP_BASE * scale;
   p.nslots = nslots_for(nq);
+  p.prof = g_prof;
   if (pp->aggregator == RNNL_AGG_SUM)
     hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
   else
     hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
   RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_debug_profile(void *dev_counters) {
+  g_prof = static_cast<unsigned long long *>(dev_counters);
   return RNNL_OK;
 }
 

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(RB) void rotate_kernel(const float *__restrict__ ee
         for (int k = 0; k < QB; ++k) {
           const float x = s_re[dd][k] - a;
           const float y = s_im[dd][k] - b;
-          part[k] += sqrtf(fmaf(x, x, y * y));
+          part[k] += __builtin_amdgcn_sqrtf(fmaf(x, x, y * y));  // v_sqrt_f32 (1 ulp)
         }
       }
 #pragma unroll

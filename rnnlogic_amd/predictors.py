@@ -287,10 +287,16 @@ class PredictorPlus(torch.nn.Module):
         else:
             _native.call("rnnl_fill_value", float("-inf"), out.numel(), out.data_ptr(), stream)
 
-    def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False, digest=None):
+    def invalidate_cache(self):
+        """Drop cached per-node rule aggregates (recomputed on the next forward)."""
+        self._node_cache = {}
+
+    def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False, digest=None, events=None):
         """Forward for any rows (one or many reference batches, mixed relations).
 
-        Returns (score (n, |E|) f32, mask (n, |E|) bool[, n_cand (n,) int32])."""
+        Returns (score (n, |E|) f32, mask (n, |E|) bool[, n_cand (n,) int32]).
+        `events`, if a dict, receives torch.cuda.Events bracketing the node
+        aggregate, base-score and grounding kernels (all on the current stream)."""
         device = all_h.device
         if device.type != "cuda":
             raise RuntimeError("PredictorPlus runs on the HIP path: move inputs and model to a GPU")
@@ -300,6 +306,9 @@ class PredictorPlus(torch.nn.Module):
         nq = all_h.numel()
         g = self.graph.device_graph(device)
         nr = self.native_rules(device)
+        rec = (lambda k: events.setdefault(k, torch.cuda.Event(enable_timing=True)).record()) \
+            if events is not None else (lambda k: None)
+        rec("start")
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -307,15 +316,18 @@ class PredictorPlus(torch.nn.Module):
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
         while True:
-            self.base_score(all_h, all_r, score)
             mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
             scale = self.capacity_scale
             ws = self._workspace(device, nq, scale)
+            rec("base")
+            self.base_score(all_h, all_r, score)
+            rec("ground")
             _native.call("rnnl_predictorplus_forward", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
                          all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
                          mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(),
                          digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
                          stream)
+            rec("end")
             rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
