@@ -33,6 +33,7 @@ extern "C" {
 #define RNNL_ERR_HIP 2       /* HIP runtime error */
 #define RNNL_ERR_OVERFLOW 3  /* workspace capacity exceeded: retry with a larger workspace */
 #define RNNL_ERR_NOMEM 4
+#define RNNL_ERR_INTERNAL 5  /* kernel self-check failed (message names the query) */
 
 #define RNNL_AGG_SUM 0       /* FuncToNodeSum   (reference src/layers.py:53-77)  */
 #define RNNL_AGG_PNA 1       /* FuncToNode, pna (reference src/layers.py:79-126) */
@@ -124,8 +125,8 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
  * Synchronises `stream`. */
 int rnnl_forward_status(void *workspace, void *stream);
 /* Diagnostic: when non-NULL, later forward launches add per-phase cycle
- * counters into dev_counters (6 x uint64: prologue, grounding, candidates,
- * queries, contributions, candidates). */
+ * counters into dev_counters (12 x uint64: prologue, grounding, candidates,
+ * queries, contributions, candidates, then candidate sub-phases). */
 int rnnl_debug_profile(void *dev_counters);
 
 /* --------------------------------------------------------- entity feature --

@@ -11,7 +11,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
 
-RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM = 0, 1, 2, 3, 4
+RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL = 0, 1, 2, 3, 4, 5
 AGG_SUM, AGG_PNA = 0, 1
 FEATURE_ADD, FEATURE_NONE = 0, 1
 

@@ -30,16 +30,29 @@ namespace rnnl {
 constexpr int BS = 256;      // threads per workgroup
 constexpr int NW = BS / 64;  // waves
 constexpr int HCAP = 4096;   // phase A hash slots ((node, entity) -> count)
-constexpr int HC = 2048;     // phase B hash slots (entity -> candidate slot)
-constexpr int MAXC = 1024;   // candidates per phase-B pass
+constexpr int WBITS = 11;    // phase B entity window: WIN = 2048 entities
+constexpr int WIN = 1 << WBITS;
+constexpr int MAXWIN = 256;  // windows per graph (|E| <= 524288)
 constexpr int WG_PER_CU = 3;
 constexpr int NUM_CU = 256;
 constexpr int EMPTY = -1;
-constexpr int HDR_BYTES = 256;  // workspace header: [0] status, [1] dequeue counter
+// Workspace header: [0] status, [1] dequeue counter, then the packed MLP
+// weights (read through a __restrict__ pointer so that hipcc keeps them in the
+// scalar path: uniform s_load into SGPR operands of the per-candidate FMAs).
+constexpr int W_ADDW = 0;                 // add_model weight (16 x 16 | 16 x 192)
+constexpr int W_ADDB = W_ADDW + 16 * 192; // add_model bias (16)
+constexpr int W_LNW = W_ADDB + 16;        // layer_norm weight (16)
+constexpr int W_LNB = W_LNW + 16;         // layer_norm bias (16)
+constexpr int W_S0X = W_LNB + 16;         // score_model.layers.0.weight[:, :16] (128 x 16)
+constexpr int W_S1W = W_S0X + 128 * 16;   // score_model.layers.1.weight (128)
+constexpr int W_S1B = W_S1W + 128;        // score_model.layers.1.bias (1)
+constexpr int W_FLOATS = 5376;            // padded
+constexpr int HDR_BYTES = 256 + W_FLOATS * 4;
 
 // Per-slot scratch geometry (entries); scaled by capacity_scale.
 constexpr int64_t FCAP_BASE = 1 << 16;
 constexpr int64_t PCAP_BASE = 1 << 16;
+static_assert(FCAP_BASE >= PCAP_BASE, "phase B sorts contributions into the frontier buffer");
 
 struct KParams {
   GraphDev g;
@@ -147,6 +160,17 @@ __device__ __forceinline__ int upper_idx(const int *a, int n, int k) {
   return lo;
 }
 
+// Workgroup barrier for data handed between waves through GLOBAL scratch:
+// __syncthreads() alone lowers to s_barrier without waiting for this wave's
+// outstanding stores, so a store could still be in flight when another wave
+// of the workgroup loads the address.  Drain the stores, barrier, and drop
+// this CU's L1 lines (stale copies from the previous query in the slot).
+__device__ __forceinline__ void wg_sync_global() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");
+}
+
 struct __align__(16) Smem {
   union {
     struct {
@@ -154,11 +178,10 @@ struct __align__(16) Smem {
       uint32_t val[HCAP];
     } a;
     struct {
-      int key[HC];
-      int slot[HC];
-      int st[MAXC];
-      uint32_t cnt[MAXC];
-      int off[MAXC];
+      int map[WIN];  // entity offset -> candidate slot
+      int cnt[WIN];
+      int off[WIN];
+      int st[WIN];   // slot -> entity
     } b;
   } u;
   int ent_v[BS], ent_fch[BS], item_off[BS];
@@ -167,9 +190,12 @@ struct __align__(16) Smem {
   uint32_t it_c[BS];
   float relb[128];
   int ws[NW + 1];
-  int q, nd, np, ovf, fail, nc, sp;
+  int q, nd, np, ovf, fail, nc, sp, err;
+  int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
+  unsigned long long t0;
   int stk_lo[32], stk_hi[32];
   unsigned long long sumlog, dig;
+  unsigned long long tp[8];  // diagnostic sub-phase cycles (thread 0)
 };
 
 __device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pcap, int t, int node, uint32_t c) {
@@ -210,16 +236,10 @@ __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
   return false;
 }
 
-__device__ __forceinline__ int cand_find(const Smem &S, int t) {
-  uint32_t h = hash32((uint32_t)t) >> (32 - 11);
-  while (S.u.b.key[h] != t) h = (h + 1) & (HC - 1);
-  return h;
-}
-
 // ---------------------------------------------------------------- per candidate
 template <int AGG>
-__device__ void score_candidate(const KParams &p, Smem &S, const Slot &sl, int q, int t, int beg, int cnt,
-                                float mean_scale) {
+__device__ void score_candidate(const KParams &p, const float *__restrict__ W, Smem &S, const Slot &sl, int q,
+                                int t, int beg, int cnt, float mean_scale) {
   constexpr int STRIDE = AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna;
   long long a1[16];
   long long a2[AGG == RNNL_AGG_PNA ? 16 : 1];
@@ -271,8 +291,8 @@ __device__ void score_candidate(const KParams &p, Smem &S, const Slot &sl, int q
     for (int o = 0; o < 16; ++o) {
       float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc = fmaf(f[i], p.add_w[o * 16 + i], acc);
-      x1[o] = acc + p.add_b[o];
+      for (int i = 0; i < 16; ++i) acc = fmaf(f[i], W[W_ADDW + o * 16 + i], acc);
+      x1[o] = acc + W[W_ADDB + o];
     }
   } else {
     // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123)
@@ -298,9 +318,9 @@ __device__ void score_candidate(const KParams &p, Smem &S, const Slot &sl, int q
       float acc = 0.f;
       for (int f = 0; f < 64; ++f) {
 #pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) acc = fmaf(feat[f] * sc[s3], p.add_w[o * 192 + f * 3 + s3], acc);
+        for (int s3 = 0; s3 < 3; ++s3) acc = fmaf(feat[f] * sc[s3], W[W_ADDW + o * 192 + f * 3 + s3], acc);
       }
-      x1[o] = acc + p.add_b[o];
+      x1[o] = acc + W[W_ADDB + o];
     }
   }
   // LayerNorm(16) + ReLU (layers.py:74-75 / 124-125)
@@ -317,18 +337,18 @@ __device__ void score_candidate(const KParams &p, Smem &S, const Slot &sl, int q
   var = var / 16.0f;
   const float rstd = 1.0f / sqrtf(var + 1e-5f);
 #pragma unroll
-  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * p.ln_w[d] + p.ln_b[d], 0.f);
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * W[W_LNW + d] + W[W_LNB + d], 0.f);
   // score_model: Linear(32,128) [relation half folded into relb], ReLU, Linear(128,1)
   float out = 0.f;
 #pragma unroll 4
   for (int o = 0; o < 128; ++o) {
     float acc = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], p.s0_w[o * 32 + i], acc);
+    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], W[W_S0X + o * 16 + i], acc);
     acc = fmaxf(acc + S.relb[o], 0.f);
-    out = fmaf(acc, p.s1_w[o], out);
+    out = fmaf(acc, W[W_S1W + o], out);
   }
-  out += p.s1_b[0];
+  out += W[W_S1B];
   const int64_t idx = (int64_t)q * p.g.E + t;
   if (p.feature == RNNL_FEATURE_NONE)
     p.score[idx] = out;
@@ -337,163 +357,164 @@ __device__ void score_candidate(const KParams &p, Smem &S, const Slot &sl, int q
   if (p.mask) p.mask[idx] = 1;
 }
 
+// Watchdog: true (uniformly, after the caller's barrier) once the current
+// query has run longer than kWatchdogTicks of the 100 MHz real-time clock;
+// thread 0 then flags S.err.  Guarantees every wave reaches the kernel exit.
+constexpr unsigned long long kWatchdogTicks = 200000000ull;  // 2 s
+__device__ __forceinline__ bool watchdog(Smem &S) {
+  if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - S.t0 > kWatchdogTicks) S.err |= 4;
+  __syncthreads();
+  return S.err != 0;
+}
+
 // ---------------------------------------------------------------- phase B
-// Buckets the query's leaf contributions per candidate entity and scores
-// every candidate.  When `degree_only` (PNA sweep 1), only accumulates
-// sum(log degree) over the candidates.  Returns false on hash overflow
-// (caller doubles the pass count).
-template <int AGG>
-__device__ bool candidates_pass(const KParams &p, Smem &S, const Slot &sl, int q, int P, int t_lo, int t_hi,
-                                bool degree_only, float mean_scale) {
+// The query's leaf contributions (entity t, node, count) are counting-sorted
+// by entity window (t >> WBITS) into the free frontier buffer; each window is
+// then handled with a direct-mapped LDS table over its WIN entities: mark,
+// block-scan the marks into candidate slots (ascending t), count per slot,
+// scan, scatter (node, count) into per-candidate buckets, score.  Reads of
+// the contribution list are O(P) in total; no table can overflow.
+#define PSTAMP(k)                                                     \
+  do {                                                                \
+    if (p.prof && tid == 0) {                                         \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();     \
+      S.tp[k] += _t - S.tp[7];                                        \
+      S.tp[7] = _t;                                                   \
+    }                                                                 \
+  } while (0)
+
+// Exclusive scan of WIN ints in place (PER consecutive per thread); returns the total.
+__device__ __forceinline__ int scan_win(int *a, int *s_ws) {
+  constexpr int PER = WIN / BS;
   const int tid = threadIdx.x;
-  for (int i = tid; i < HC; i += BS) S.u.b.key[i] = EMPTY;
-  for (int i = tid; i < MAXC; i += BS) S.u.b.cnt[i] = 0;
-  if (tid == 0) {
-    S.nc = 0;
-    S.fail = 0;
-  }
-  __syncthreads();
-  // B1: insert entity keys
-  for (int i = tid; i < P; i += BS) {
-    const int t = sl.ct[i];
-    if (t < t_lo || t >= t_hi) continue;
-    uint32_t h = hash32((uint32_t)t) >> (32 - 11);
-    int probe = 0;
-    for (; probe < HC; ++probe) {
-      const int k = atomicCAS(&S.u.b.key[h], EMPTY, t);
-      if (k == EMPTY || k == t) break;
-      h = (h + 1) & (HC - 1);
-    }
-    if (probe == HC) S.fail = 1;
-  }
-  __syncthreads();
-  if (S.fail) return false;
-  // B2: slot ids
-  for (int h = tid; h < HC; h += BS) {
-    const int k = S.u.b.key[h];
-    if (k != EMPTY) {
-      const int s = atomicAdd(&S.nc, 1);
-      if (s < MAXC) {
-        S.u.b.slot[h] = s;
-        S.u.b.st[s] = k;
-      } else {
-        S.fail = 1;
-      }
-    }
-  }
-  __syncthreads();
-  if (S.fail) return false;
-  const int nc = S.nc;
-  // B3: bucket sizes
-  for (int i = tid; i < P; i += BS) {
-    const int t = sl.ct[i];
-    if (t < t_lo || t >= t_hi) continue;
-    atomicAdd(&S.u.b.cnt[S.u.b.slot[cand_find(S, t)]], 1u);
-  }
-  __syncthreads();
-  // B4: exclusive scan of cnt[0..nc) (MAXC / BS = 4 per thread, contiguous)
-  {
-    constexpr int PER = MAXC / BS;
-    int loc[PER];
-    int sum = 0;
+  int loc[PER];
+  int sum = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int idx = tid * PER + j;
-      loc[j] = idx < nc ? (int)S.u.b.cnt[idx] : 0;
-      sum += loc[j];
-    }
-    int total;
-    int base = block_scan(sum, S.ws, total);
+  for (int j = 0; j < PER; ++j) {
+    loc[j] = a[tid * PER + j];
+    sum += loc[j];
+  }
+  int total;
+  int base = block_scan(sum, s_ws, total);
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int idx = tid * PER + j;
-      S.u.b.off[idx] = base;
-      base += loc[j];
+  for (int j = 0; j < PER; ++j) {
+    a[tid * PER + j] = base;
+    base += loc[j];
+  }
+  __syncthreads();
+  return total;
+}
+
+// One entity window [lo, lo + WIN) whose contributions are wt/wn/wc[beg, end).
+// degree_only (PNA sweep 1): accumulate sum log(degree) instead of scoring.
+template <int AGG>
+__device__ int window_pass(const KParams &p, const float *__restrict__ W, Smem &S, const Slot &sl, int q, int lo,
+                           int beg, int end, bool degree_only, float mean_scale) {
+  const int tid = threadIdx.x;
+  const int32_t *wt = sl.fn[0], *wn = sl.fv[0];
+  const uint32_t *wc = sl.fc[0];
+  if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
+  for (int i = tid; i < WIN; i += BS) S.u.b.map[i] = 0;
+  __syncthreads();
+  // M2: mark present entities
+  for (int i = beg + tid; i < end; i += BS) S.u.b.map[wt[i] - lo] = 1;
+  __syncthreads();
+  PSTAMP(0);
+  // M3: slots in ascending entity order
+  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = S.u.b.map[i];
+  __syncthreads();
+  const int nc = scan_win(S.u.b.cnt, S.ws);
+  for (int i = tid; i < WIN; i += BS) {
+    if (S.u.b.map[i]) {
+      const int slot = S.u.b.cnt[i];
+      S.u.b.map[i] = slot;
+      S.u.b.st[slot] = lo + i;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
+  __syncthreads();
+  PSTAMP(1);
+  if (degree_only) {
+    // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
+    for (int i = beg + tid; i < end; i += BS)
+      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[wt[i] - lo]]),
+                wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
+    __syncthreads();
+    for (int s2 = tid; s2 < nc; s2 += BS) {
+      const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
+      atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
     }
     __syncthreads();
+    return nc;
   }
-  if (degree_only) {
-    // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate.
-    // B5': accumulate degree per slot directly (no bucket scatter needed).
-    for (int i = tid; i < MAXC; i += BS) S.u.b.cnt[i] = 0;
+  // M4: bucket sizes
+  for (int i = beg + tid; i < end; i += BS) atomicAdd(&S.u.b.cnt[S.u.b.map[wt[i] - lo]], 1);
+  __syncthreads();
+  PSTAMP(2);
+  // M5: bucket offsets (relative to beg)
+  for (int i = tid; i < WIN; i += BS) S.u.b.off[i] = S.u.b.cnt[i];
+  __syncthreads();
+  scan_win(S.u.b.off, S.ws);
+  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
+  __syncthreads();
+  PSTAMP(3);
+  // M6: scatter (node, count) into buckets
+  for (int i = beg + tid; i < end; i += BS) {
+    const int s2 = S.u.b.map[wt[i] - lo];
+    const int pos = beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
+    sl.bn[pos] = wn[i];
+    sl.bc[pos] = wc[i];
+  }
+  wg_sync_global();
+  PSTAMP(4);
+  // M7: one lane per candidate
+  for (int s2 = tid; s2 < nc; s2 += BS)
+    score_candidate<AGG>(p, W, S, sl, q, S.u.b.st[s2], beg + S.u.b.off[s2], S.u.b.cnt[s2], mean_scale);
+  __syncthreads();
+  PSTAMP(5);
+  return nc;
+}
+
+// Counting sort of the contributions by entity window into fn/fv/fc[0]
+// (free during phase B), then window_pass over every non-empty window.
+template <int AGG>
+__device__ int candidates_phase(const KParams &p, const float *__restrict__ W, Smem &S, const Slot &sl, int q,
+                                int P, bool degree_only, float mean_scale, bool sorted) {
+  const int tid = threadIdx.x;
+  const int nwin = (p.g.E + WIN - 1) >> WBITS;
+  if (!sorted) {
+    for (int i = tid; i < nwin; i += BS) S.whist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < P; i += BS) atomicAdd(&S.whist[sl.ct[i] >> WBITS], 1);
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int w = 0; w < nwin; ++w) {
+        const int c = S.whist[w];
+        S.wbeg[w] = acc;
+        S.wfill[w] = acc;
+        acc += c;
+      }
+      S.wbeg[nwin] = acc;
+    }
     __syncthreads();
     for (int i = tid; i < P; i += BS) {
       const int t = sl.ct[i];
-      if (t < t_lo || t >= t_hi) continue;
-      const int s = S.u.b.slot[cand_find(S, t)];
-      atomicAdd(&S.u.b.cnt[s], sl.cc[i] * (uint32_t)p.rl.node_nrules[sl.cn[i]]);
+      const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
+      sl.fn[0][pos] = t;
+      sl.fv[0][pos] = sl.cn[i];
+      sl.fc[0][pos] = sl.cc[i];
     }
-    __syncthreads();
-    for (int s = tid; s < nc; s += BS) {
-      const float degf = (float)((double)S.u.b.cnt[s] + 1.0);
-      const double fx = (double)logf(degf) * 4294967296.0;  // 2^32 fixed point
-      atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint(fx));
-    }
-    __syncthreads();
-    return true;
+    wg_sync_global();
   }
-  // B5: scatter (node, count) into buckets
-  for (int i = tid; i < MAXC; i += BS) S.u.b.cnt[i] = 0;
-  __syncthreads();
-  for (int i = tid; i < P; i += BS) {
-    const int t = sl.ct[i];
-    if (t < t_lo || t >= t_hi) continue;
-    const int s = S.u.b.slot[cand_find(S, t)];
-    const int pos = S.u.b.off[s] + (int)atomicAdd(&S.u.b.cnt[s], 1u);
-    sl.bn[pos] = sl.cn[i];
-    sl.bc[pos] = sl.cc[i];
+  int ncand = 0;
+  for (int w = 0; w < nwin; ++w) {
+    const int beg = S.wbeg[w], end = S.wbeg[w + 1];
+    if (beg == end) continue;
+    ncand += window_pass<AGG>(p, W, S, sl, q, w << WBITS, beg, end, degree_only, mean_scale);
   }
-  __syncthreads();
-  // B6: one lane per candidate
-  for (int s = tid; s < nc; s += BS)
-    score_candidate<AGG>(p, S, sl, q, S.u.b.st[s], S.u.b.off[s], (int)S.u.b.cnt[s], mean_scale);
-  __syncthreads();
-  return true;
-}
-
-// Runs candidates_pass over entity ranges [0, E) split into np pieces; a
-// range whose candidates overflow the LDS tables (detected before anything is
-// written) is split in two and redone.  Returns the number of candidates.
-template <int AGG>
-__device__ int run_passes(const KParams &p, Smem &S, const Slot &sl, int q, int P, int np, bool degree_only,
-                          float mean_scale) {
-  const int tid = threadIdx.x;
-  if (tid == 0) S.sp = 0;
-  int next = 0, cnt = 0;
-#pragma unroll 1
-  while (true) {
-    __syncthreads();
-    const int sp = S.sp;
-    int lo, hi;
-    if (sp > 0) {
-      lo = S.stk_lo[sp - 1];
-      hi = S.stk_hi[sp - 1];
-    } else if (next < np) {
-      lo = (int)((int64_t)next * p.g.E / np);
-      hi = (int)((int64_t)(next + 1) * p.g.E / np);
-      ++next;
-    } else {
-      break;
-    }
-    __syncthreads();
-    if (tid == 0 && sp > 0) S.sp = sp - 1;
-    const bool ok = candidates_pass<AGG>(p, S, sl, q, P, lo, hi, degree_only, mean_scale);
-    if (ok) {
-      cnt += S.nc;
-    } else if (tid == 0) {
-      const int mid = lo + (hi - lo) / 2;
-      if (S.sp + 2 <= 32 && hi - lo > 1) {
-        S.stk_lo[S.sp] = mid;
-        S.stk_hi[S.sp] = hi;
-        S.stk_lo[S.sp + 1] = lo;
-        S.stk_hi[S.sp + 1] = mid;
-        S.sp += 2;
-      } else {
-        S.ovf = 1;
-      }
-    }
-  }
-  return cnt;
+  return ncand;
 }
 
 // ---------------------------------------------------------------- phase A
@@ -508,11 +529,12 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, i
     sl.fc[0][0] = 1u;
     if (p.rl.node_nrules[root] > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
   }
-  __syncthreads();
+  wg_sync_global();
   int cur = 0, n_prev = 1;
   for (int d = 1; d <= depth; ++d) {
     const int nxt = cur ^ 1;
     for (int cb = 0; cb < n_prev; cb += BS) {
+      if (watchdog(S)) break;
       const int ne = min(BS, n_prev - cb);
       int nch = 0;
       if (tid < ne) {
@@ -578,7 +600,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, i
         S.u.a.val[s] = 0u;
       }
     }
-    __syncthreads();
+    wg_sync_global();
     n_prev = min((int64_t)S.nd, p.fcap);
     __syncthreads();
     if (tid == 0) S.nd = 0;
@@ -588,7 +610,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, i
 }
 
 template <int AGG>
-__global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
+__global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const float *__restrict__ W) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
@@ -599,6 +621,7 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
   }
   __syncthreads();
   unsigned long long pr[6] = {0, 0, 0, 0, 0, 0};
+  if (tid < 8) S.tp[tid] = 0ull;
   unsigned long long t_q = 0, t_a = 0;
 #pragma unroll 1
   while (true) {
@@ -628,6 +651,8 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
       }
     }
     if (tid == 0) {
+      S.t0 = __builtin_amdgcn_s_memrealtime();
+      S.err = 0;
       S.np = 0;
       S.nd = 0;
       S.ovf = 0;
@@ -643,7 +668,7 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
     __syncthreads();
     if (p.prof && tid == 0) t_a = __builtin_amdgcn_s_memtime();
     ground_query(p, S, sl, q, h, r, root, rm_src, rm_dst);
-    __syncthreads();
+    wg_sync_global();
     if (p.prof && tid == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       pr[1] += t - t_a;
@@ -651,32 +676,44 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
       t_a = t;
     }
     const int P = S.np;
-    if (S.ovf || P > p.pcap) {
+    if (S.ovf || P > p.pcap || S.err) {
       // leave the LDS hash clean for the next query
       for (int s = tid; s < HCAP; s += BS) {
         S.u.a.key[s] = EMPTY;
         S.u.a.val[s] = 0u;
       }
       if (tid == 0) {
-        atomicOr(&hdr[0], 1u);
-        if (p.n_cand) p.n_cand[q] = -1;
+        atomicOr(&hdr[0], S.err ? 2u : 1u);
+        if (S.err) {
+          atomicOr(&hdr[2], (unsigned)S.err);
+          atomicExch(&hdr[3], (unsigned)q);
+        }
+        if (p.n_cand) p.n_cand[q] = S.err ? -2 : -1;
       }
       __syncthreads();
       continue;
     }
-    const int np = max(1, (P + 2047) / 2048);
     float mean_scale = 0.f;
+    bool sorted = false;
     if constexpr (AGG == RNNL_AGG_PNA) {
       // sweep 1: per-query mean of log(degree) over candidates (layers.py:109-116)
       if (tid == 0) S.sumlog = 0ull;
-      const int nc1 = run_passes<AGG>(p, S, sl, q, P, np, true, 0.f);
+      const int nc1 = candidates_phase<AGG>(p, W, S, sl, q, P, true, 0.f, false);
+      sorted = true;
       const double sum = (double)(long long)S.sumlog / 4294967296.0;
       mean_scale = (float)((float)sum / fmaxf((float)nc1, 1e-6f));
     }
     if (tid == 0) S.dig = 0ull;
-    const int ncand = run_passes<AGG>(p, S, sl, q, P, np, false, mean_scale);
+    __syncthreads();
+    const int ncand = candidates_phase<AGG>(p, W, S, sl, q, P, false, mean_scale, sorted);
+    if (tid == 0 && S.err) {
+      // diagnostics: hdr[2] |= error bits, hdr[3] = last failing query
+      atomicOr(&hdr[2], (unsigned)S.err);
+      atomicExch(&hdr[3], (unsigned)q);
+      atomicOr(&hdr[0], 2u);
+    }
     if (tid == 0) {
-      if (p.n_cand) p.n_cand[q] = ncand;
+      if (p.n_cand) p.n_cand[q] = S.err ? -2 : ncand;
       if (p.digest) p.digest[q] = S.dig;
       if (p.prof) {
         pr[2] += __builtin_amdgcn_s_memtime() - t_a;
@@ -692,8 +729,35 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p) {
     }
     __syncthreads();
   }
-  if (p.prof && tid == 0)
+  if (p.prof && tid == 0) {
     for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[k], pr[k]);
+    for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
+  }
+}
+
+// Packs the MLP weights into the workspace header (layout W_* above).
+__global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
+  const int kin = p.agg == RNNL_AGG_SUM ? 16 : 192;
+  for (int i = threadIdx.x; i < W_FLOATS; i += blockDim.x) {
+    float v = 0.f;
+    if (i < W_ADDB) {
+      if (i < 16 * kin) v = p.add_w[i];
+    } else if (i < W_LNW) {
+      v = p.add_b[i - W_ADDB];
+    } else if (i < W_LNB) {
+      v = p.ln_w[i - W_LNW];
+    } else if (i < W_S0X) {
+      v = p.ln_b[i - W_LNB];
+    } else if (i < W_S1W) {
+      const int k = i - W_S0X;
+      v = p.s0_w[(k / 16) * 32 + (k % 16)];
+    } else if (i < W_S1B) {
+      v = p.s1_w[i - W_S1W];
+    } else if (i == W_S1B) {
+      v = p.s1_b[0];
+    }
+    W[i] = v;
+  }
 }
 
 // ---------------------------------------------------------------- node weights
@@ -765,6 +829,10 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
     set_error("rnnl_predictorplus_forward: bad arguments");
     return RNNL_ERR_INVALID;
   }
+  if ((int64_t)g->d.E > (int64_t)MAXWIN * WIN) {
+    set_error("rnnl_predictorplus_forward: more entities than the kernel's window table supports");
+    return RNNL_ERR_INVALID;
+  }
   size_t need = 0;
   rnnl_forward_workspace_size(g, r, nq, scale, &need);
   if (ws_bytes < need) {
@@ -772,7 +840,7 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
     return RNNL_ERR_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_BYTES, st));
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, 256, st));
   if (nq == 0) return RNNL_OK;
   KParams p;
   p.g = g->d;
@@ -802,10 +870,12 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   p.pcap = PCAP_BASE * scale;
   p.nslots = nslots_for(nq);
   p.prof = g_prof;
+  float *W = reinterpret_cast<float *>(p.ws + 256);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
   if (pp->aggregator == RNNL_AGG_SUM)
-    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p, (const float *)W);
   else
-    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
+    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p, (const float *)W);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
@@ -816,10 +886,15 @@ int rnnl_debug_profile(void *dev_counters) {
 }
 
 int rnnl_forward_status(void *ws, void *stream) {
-  unsigned int st = 0;
-  RNNL_HIP_CHECK(hipMemcpyAsync(&st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  unsigned int st[4] = {0, 0, 0, 0};
+  RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
   RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-  if (st) {
+  if (st[0] & 2u) {
+    set_error("rnnl_predictorplus_forward: internal error bits 0x" + std::to_string(st[2]) +
+              " (1: candidate lookup miss, 2: bucket overflow, 4: watchdog) at query " + std::to_string(st[3]));
+    return RNNL_ERR_INTERNAL;
+  }
+  if (st[0] & 1u) {
     set_error("rnnl_predictorplus_forward: workspace capacity exceeded");
     return RNNL_ERR_OVERFLOW;
   }

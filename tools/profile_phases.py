@@ -16,6 +16,8 @@ from rnnlogic_amd import _native  # noqa: E402
 
 
 def main():
+    import faulthandler
+    faulthandler.dump_traceback_later(int(os.environ.get("HANG_DUMP_S", "60")), exit=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--feature", default="bias")
     ap.add_argument("--rows", type=int, default=0)
@@ -29,7 +31,7 @@ def main():
     r = torch.from_numpy(rows[:, 1]).to(dev)
     with torch.no_grad():
         model.forward_rows(h, r, None)
-        prof = torch.zeros(6, dtype=torch.int64, device=dev)
+        prof = torch.zeros(12, dtype=torch.int64, device=dev)
         _native.call("rnnl_debug_profile", prof.data_ptr())
         ev = {}
         model.forward_rows(h, r, None, events=ev)
@@ -39,6 +41,8 @@ def main():
     nq = max(p[3], 1)
     print("queries %d  contributions/q %.1f  candidates/q %.1f" % (p[3], p[4] / nq, p[5] / nq))
     for name, v in zip(["prologue", "grounding(A)", "candidates(B)"], p[:3]):
+        print("  %-14s %10.0f cycles/query" % (name, v / nq))
+    for name, v in zip(["B mark", "B slots", "B count", "B scan", "B scatter", "B score"], p[6:12]):
         print("  %-14s %10.0f cycles/query" % (name, v / nq))
     print("events ms: nodes %.3f base %.3f ground %.3f" % (ev["start"].elapsed_time(ev["base"]),
           ev["base"].elapsed_time(ev["ground"]), ev["ground"].elapsed_time(ev["end"])))
