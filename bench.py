@@ -122,7 +122,9 @@ def main():
     if world > 1:
         dist.barrier()
 
-    graph, test_set, model, rows = build_workload(args.feature)
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+        graph, test_set, model, rows = build_workload(args.feature)
     model = model.to(dev).eval()
     h = torch.from_numpy(rows[:, 0]).to(dev)
     r = torch.from_numpy(rows[:, 1]).to(dev)

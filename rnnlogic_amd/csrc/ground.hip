@@ -1,27 +1,32 @@
-// Fused PredictorPlus forward for gfx950 (MI355X).
+// PredictorPlus forward for gfx950 (MI355X): two kernels per launch.
 //
-// One persistent workgroup (256 lanes = 4 waves) owns one query at a time,
-// dequeued from a device counter, and runs the whole reference forward for
-// that row of the batch:
-//
+// K1 ground_kernel — one persistent workgroup (256 lanes) per query at a
+// time, dequeued from a device counter:
 //   grounding / propagate (ref src/data.py:136-173, torch_scatter scatter-sum)
 //       -> level-synchronous walk of the head relation's rule-prefix trie over
 //          the vertex-major CSR; every (trie node, entity) path count lives in
 //          an LDS hash (integer, exact); the query's own edge is skipped on
 //          hops of the query relation (data.py:164-169).
 //   candidate set + rule_count stack (ref src/predictors.py:221-244)
-//       -> leaf contributions (entity, node, count) bucketed per candidate
-//          entity through an LDS hash.
+//       -> leaf contributions (entity, node, count) are counting-sorted by
+//          entity window and bucketed per candidate through a direct-mapped
+//          LDS table into a global pool: per query a contiguous run of
+//          candidate records (entity, bucket) and (node, count) entries —
+//          the COO of the reference's stacked rule_count matrix.
+// K2 score_kernel — one workgroup per query (grid-stride), one lane per
+// candidate:
 //   rule_to_entity (ref src/layers.py:53-126) + score_model (layers.py:9-51)
-//       -> one lane per candidate: node sums in exact fixed point, then
-//          Linear/LayerNorm/ReLU and the 32->128->1 MLP in fp32 registers;
-//          the result is added into the pre-filled base score (bias/RotatE)
-//          or written (entity_feature none).
-//
-// Memory: the graph (CSR ~ E*R*4 B + edges*4 B) and the node tables are
-// read-only and L2/MALL resident; per-slot scratch in HBM holds the frontier
-// lists, contributions and buckets of the query in flight.
+//       -> node sums in exact fixed point (order-independent, deterministic),
+//          Linear/LayerNorm/ReLU, then the 32->128->1 MLP with the weights in
+//          LDS and the relation half folded into a per-query bias; the result
+//          is added into the pre-filled base score (bias/RotatE) or written
+//          (entity_feature none).
+// Splitting the MLP out of K1 keeps K1's registers low (it is latency-bound:
+// dependent CSR reads and barriers) and gives K2 a simple, fully occupied
+// streaming shape.
 #include <hip/hip_runtime.h>
+
+#include <string>
 
 #include "internal.h"
 
@@ -29,16 +34,19 @@ namespace rnnl {
 
 constexpr int BS = 256;      // threads per workgroup
 constexpr int NW = BS / 64;  // waves
-constexpr int HCAP = 4096;   // phase A hash slots ((node, entity) -> count)
-constexpr int WBITS = 11;    // phase B entity window: WIN = 2048 entities
+constexpr int HCAP = 4096;   // phase-A hash slots ((node, entity) -> count)
+constexpr int WBITS = 11;    // phase-B entity window: WIN = 2048 entities
 constexpr int WIN = 1 << WBITS;
 constexpr int MAXWIN = 256;  // windows per graph (|E| <= 524288)
 constexpr int WG_PER_CU = 3;
 constexpr int NUM_CU = 256;
 constexpr int EMPTY = -1;
-// Workspace header: [0] status, [1] dequeue counter, then the packed MLP
-// weights (read through a __restrict__ pointer so that hipcc keeps them in the
-// scalar path: uniform s_load into SGPR operands of the per-candidate FMAs).
+
+// Workspace header words (uint32), then a 64-bit pool counter at byte 64.
+enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5 };
+constexpr int HDR_WORDS_BYTES = 256;
+
+// Packed MLP weights (written by pack_weights_kernel behind the header).
 constexpr int W_ADDW = 0;                 // add_model weight (16 x 16 | 16 x 192)
 constexpr int W_ADDB = W_ADDW + 16 * 192; // add_model bias (16)
 constexpr int W_LNW = W_ADDB + 16;        // layer_norm weight (16)
@@ -47,12 +55,21 @@ constexpr int W_S0X = W_LNB + 16;         // score_model.layers.0.weight[:, :16]
 constexpr int W_S1W = W_S0X + 128 * 16;   // score_model.layers.1.weight (128)
 constexpr int W_S1B = W_S1W + 128;        // score_model.layers.1.bias (1)
 constexpr int W_FLOATS = 5376;            // padded
-constexpr int HDR_BYTES = 256 + W_FLOATS * 4;
+constexpr int HDR_BYTES = HDR_WORDS_BYTES + W_FLOATS * 4;
 
-// Per-slot scratch geometry (entries); scaled by capacity_scale.
-constexpr int64_t FCAP_BASE = 1 << 16;
-constexpr int64_t PCAP_BASE = 1 << 16;
+// LDS copy of the weights used by K2: [add_w 16*KIN | add_b | ln_w | ln_b | s0x 128x16 | s1w 128 | s1b]
+template <int AGG>
+struct WL {
+  static constexpr int KIN = AGG == RNNL_AGG_SUM ? 16 : 192;
+  static constexpr int ADDW = 0, ADDB = 16 * KIN, LNW = ADDB + 16, LNB = LNW + 16, S0X = LNB + 16,
+                       S1W = S0X + 128 * 16, S1B = S1W + 128, N = S1B + 4;
+};
+
+// Per-slot scratch (entries), scaled by capacity_scale.
+constexpr int64_t FCAP_BASE = 1 << 16;  // frontier list (and window-sorted contributions)
+constexpr int64_t PCAP_BASE = 1 << 16;  // contributions of one query
 static_assert(FCAP_BASE >= PCAP_BASE, "phase B sorts contributions into the frontier buffer");
+constexpr int64_t POOL_PER_QUERY = 8192;  // global bucket pool entries per query (x scale)
 
 struct KParams {
   GraphDev g;
@@ -67,12 +84,20 @@ struct KParams {
   int32_t *n_cand;
   uint64_t *digest;
   unsigned char *ws;
-  int64_t fcap, pcap;
+  // workspace carve-up
+  int64_t fcap, pcap, pool_cap;
   int32_t nslots;
+  unsigned char *slots;
+  int64_t *q_base;   // per query: first pool index of its run
+  float *q_scale;    // per query: PNA mean log-degree
+  int32_t *c_t;      // per pool index: candidate entity (first n_cand entries of a run)
+  int32_t *c_beg;    //                 candidate bucket start (pool index)
+  int32_t *c_cnt;    //                 candidate bucket length
+  int32_t *b_node;   // bucket entries: trie node
+  uint32_t *b_cnt;   //                 path count
   unsigned long long *prof;  // diagnostic phase cycle counters (nullable)
 };
 
-// Diagnostic: phase cycle counters of the next launches (rnnl_debug_profile).
 static unsigned long long *g_prof = nullptr;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -89,16 +114,12 @@ struct Slot {
   uint32_t *fc[2];
   int32_t *ct, *cn;
   uint32_t *cc;
-  int32_t *bn;
-  uint32_t *bc;
 };
 
-__host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) {
-  return 2 * fcap * 12 + pcap * 12 + pcap * 8;
-}
+__host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) { return 2 * fcap * 12 + pcap * 12; }
 
-__device__ inline Slot make_slot(unsigned char *ws, int slot, int64_t fcap, int64_t pcap) {
-  unsigned char *b = ws + HDR_BYTES + (int64_t)slot * slot_bytes(fcap, pcap);
+__device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, int64_t pcap) {
+  unsigned char *b = base + (int64_t)slot * slot_bytes(fcap, pcap);
   Slot s;
   for (int k = 0; k < 2; ++k) {
     s.fn[k] = reinterpret_cast<int32_t *>(b);
@@ -113,11 +134,42 @@ __device__ inline Slot make_slot(unsigned char *ws, int slot, int64_t fcap, int6
   s.cn = reinterpret_cast<int32_t *>(b);
   b += pcap * 4;
   s.cc = reinterpret_cast<uint32_t *>(b);
-  b += pcap * 4;
-  s.bn = reinterpret_cast<int32_t *>(b);
-  b += pcap * 4;
-  s.bc = reinterpret_cast<uint32_t *>(b);
   return s;
+}
+
+// Workspace layout, shared by host sizing and the launch.
+struct Layout {
+  int64_t nslots, fcap, pcap, pool_cap;
+  int64_t off_qbase, off_qscale, off_ct, off_cbeg, off_ccnt, off_bnode, off_bcnt, off_slots, total;
+};
+
+static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+static Layout make_layout(int64_t nq, int64_t scale) {
+  Layout L;
+  L.nslots = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)NUM_CU * WG_PER_CU));
+  L.fcap = FCAP_BASE * scale;
+  L.pcap = PCAP_BASE * scale;
+  L.pool_cap = std::max<int64_t>(POOL_PER_QUERY * scale * std::max<int64_t>(nq, 1), L.pcap);
+  int64_t o = HDR_BYTES;
+  L.off_qbase = o = align256(o);
+  o += 8 * std::max<int64_t>(nq, 1);
+  L.off_qscale = o = align256(o);
+  o += 4 * std::max<int64_t>(nq, 1);
+  L.off_ct = o = align256(o);
+  o += 4 * L.pool_cap;
+  L.off_cbeg = o = align256(o);
+  o += 4 * L.pool_cap;
+  L.off_ccnt = o = align256(o);
+  o += 4 * L.pool_cap;
+  L.off_bnode = o = align256(o);
+  o += 4 * L.pool_cap;
+  L.off_bcnt = o = align256(o);
+  o += 4 * L.pool_cap;
+  L.off_slots = o = align256(o);
+  o += L.nslots * slot_bytes(L.fcap, L.pcap);
+  L.total = o;
+  return L;
 }
 
 // Exclusive block scan of one int per thread; `total` gets the block sum.
@@ -186,15 +238,14 @@ struct __align__(16) Smem {
   } u;
   int ent_v[BS], ent_fch[BS], item_off[BS];
   uint32_t ent_c[BS];
-  int it_child[BS], it_beg[BS], it_v[BS], it_rel[BS], it_flags[BS], edge_off[BS];
+  int it_child[BS], it_beg[BS], it_flags[BS], edge_off[BS];
   uint32_t it_c[BS];
-  float relb[128];
   int ws[NW + 1];
-  int q, nd, np, ovf, fail, nc, sp, err;
-  int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
+  int q, nd, np, ovf, err;
+  long long qbase;
   unsigned long long t0;
-  int stk_lo[32], stk_hi[32];
-  unsigned long long sumlog, dig;
+  int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
+  unsigned long long sumlog;
   unsigned long long tp[8];  // diagnostic sub-phase cycles (thread 0)
 };
 
@@ -236,130 +287,9 @@ __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
   return false;
 }
 
-// ---------------------------------------------------------------- per candidate
-template <int AGG>
-__device__ void score_candidate(const KParams &p, const float *__restrict__ W, Smem &S, const Slot &sl, int q,
-                                int t, int beg, int cnt, float mean_scale) {
-  constexpr int STRIDE = AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna;
-  long long a1[16];
-  long long a2[AGG == RNNL_AGG_PNA ? 16 : 1];
-  float mn[AGG == RNNL_AGG_PNA ? 16 : 1], mx[AGG == RNNL_AGG_PNA ? 16 : 1];
-#pragma unroll
-  for (int d = 0; d < 16; ++d) a1[d] = 0;
-  if constexpr (AGG == RNNL_AGG_PNA) {
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a2[d] = 0;
-      mn[d] = __builtin_huge_valf();
-      mx[d] = -__builtin_huge_valf();
-    }
-  }
-  long long deg = 0;
-  uint64_t fp = 0;
-  for (int e = beg; e < beg + cnt; ++e) {
-    const int n = sl.bn[e];
-    const long long c = sl.bc[e];
-    const long long *rec = reinterpret_cast<const long long *>(p.node_w + (int64_t)n * STRIDE);
-#pragma unroll
-    for (int d = 0; d < 16; ++d) a1[d] += c * rec[d];
-    const int k = p.rl.node_nrules[n];
-    deg += c * k;
-    if (p.digest) fp += (uint64_t)c * p.rl.node_fp[n];
-    if constexpr (AGG == RNNL_AGG_PNA) {
-#pragma unroll
-      for (int d = 0; d < 16; ++d) a2[d] += c * rec[16 + d];
-      const float *fr = reinterpret_cast<const float *>(rec + 32);
-#pragma unroll
-      for (int d = 0; d < 16; ++d) {
-        mn[d] = fminf(mn[d], fr[d]);
-        mx[d] = fmaxf(mx[d], fr[16 + d]);
-      }
-    }
-  }
-  if (p.digest) {
-    const uint64_t dg = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
-    atomicAdd(&S.dig, (unsigned long long)dg);
-  }
-  constexpr float inv_fix = 1.0f / (float)(1 << kFixShift);
-  float x1[16];
-  if constexpr (AGG == RNNL_AGG_SUM) {
-    // FuncToNodeSum: Linear(16,16) on the rule-weighted sum (layers.py:68-74)
-    float f[16];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) f[d] = (float)((double)a1[d] * (double)inv_fix);
-#pragma unroll
-    for (int o = 0; o < 16; ++o) {
-      float acc = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc = fmaf(f[i], W[W_ADDW + o * 16 + i], acc);
-      x1[o] = acc + W[W_ADDB + o];
-    }
-  } else {
-    // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123)
-    const float degf = (float)(deg + 1);
-    const float dcl = fmaxf(degf, 1e-6f);
-    float feat[64];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      const float s = (float)((double)a1[d] * (double)inv_fix);
-      const float sq = (float)((double)a2[d] * (double)inv_fix);
-      const float mean = s / dcl;
-      const float sqm = sq / dcl;
-      feat[d] = mean;
-      feat[16 + d] = mn[d];
-      feat[32 + d] = mx[d];
-      feat[48 + d] = sqrtf(fmaxf(sqm - mean * mean, 1e-6f));
-    }
-    float scale = logf(degf);
-    scale = scale / fmaxf(mean_scale, 1e-6f);
-    const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
-#pragma unroll
-    for (int o = 0; o < 16; ++o) {
-      float acc = 0.f;
-      for (int f = 0; f < 64; ++f) {
-#pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) acc = fmaf(feat[f] * sc[s3], W[W_ADDW + o * 192 + f * 3 + s3], acc);
-      }
-      x1[o] = acc + W[W_ADDB + o];
-    }
-  }
-  // LayerNorm(16) + ReLU (layers.py:74-75 / 124-125)
-  float mu = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; ++d) mu += x1[d];
-  mu = mu / 16.0f;
-  float var = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    const float z = x1[d] - mu;
-    var = fmaf(z, z, var);
-  }
-  var = var / 16.0f;
-  const float rstd = 1.0f / sqrtf(var + 1e-5f);
-#pragma unroll
-  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * W[W_LNW + d] + W[W_LNB + d], 0.f);
-  // score_model: Linear(32,128) [relation half folded into relb], ReLU, Linear(128,1)
-  float out = 0.f;
-#pragma unroll 4
-  for (int o = 0; o < 128; ++o) {
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], W[W_S0X + o * 16 + i], acc);
-    acc = fmaxf(acc + S.relb[o], 0.f);
-    out = fmaf(acc, W[W_S1W + o], out);
-  }
-  out += W[W_S1B];
-  const int64_t idx = (int64_t)q * p.g.E + t;
-  if (p.feature == RNNL_FEATURE_NONE)
-    p.score[idx] = out;
-  else
-    p.score[idx] = out + p.score[idx];
-  if (p.mask) p.mask[idx] = 1;
-}
-
-// Watchdog: true (uniformly, after the caller's barrier) once the current
-// query has run longer than kWatchdogTicks of the 100 MHz real-time clock;
-// thread 0 then flags S.err.  Guarantees every wave reaches the kernel exit.
+// Watchdog: true (uniformly, after the barrier) once the current query has
+// run longer than kWatchdogTicks of the 100 MHz real-time clock; thread 0
+// then flags S.err.  Guarantees every wave reaches the kernel exit.
 constexpr unsigned long long kWatchdogTicks = 200000000ull;  // 2 s
 __device__ __forceinline__ bool watchdog(Smem &S) {
   if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - S.t0 > kWatchdogTicks) S.err |= 4;
@@ -367,13 +297,6 @@ __device__ __forceinline__ bool watchdog(Smem &S) {
   return S.err != 0;
 }
 
-// ---------------------------------------------------------------- phase B
-// The query's leaf contributions (entity t, node, count) are counting-sorted
-// by entity window (t >> WBITS) into the free frontier buffer; each window is
-// then handled with a direct-mapped LDS table over its WIN entities: mark,
-// block-scan the marks into candidate slots (ascending t), count per slot,
-// scan, scatter (node, count) into per-candidate buckets, score.  Reads of
-// the contribution list are O(P) in total; no table can overflow.
 #define PSTAMP(k)                                                     \
   do {                                                                \
     if (p.prof && tid == 0) {                                         \
@@ -383,142 +306,8 @@ __device__ __forceinline__ bool watchdog(Smem &S) {
     }                                                                 \
   } while (0)
 
-// Exclusive scan of WIN ints in place (PER consecutive per thread); returns the total.
-__device__ __forceinline__ int scan_win(int *a, int *s_ws) {
-  constexpr int PER = WIN / BS;
-  const int tid = threadIdx.x;
-  int loc[PER];
-  int sum = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    loc[j] = a[tid * PER + j];
-    sum += loc[j];
-  }
-  int total;
-  int base = block_scan(sum, s_ws, total);
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    a[tid * PER + j] = base;
-    base += loc[j];
-  }
-  __syncthreads();
-  return total;
-}
-
-// One entity window [lo, lo + WIN) whose contributions are wt/wn/wc[beg, end).
-// degree_only (PNA sweep 1): accumulate sum log(degree) instead of scoring.
-template <int AGG>
-__device__ int window_pass(const KParams &p, const float *__restrict__ W, Smem &S, const Slot &sl, int q, int lo,
-                           int beg, int end, bool degree_only, float mean_scale) {
-  const int tid = threadIdx.x;
-  const int32_t *wt = sl.fn[0], *wn = sl.fv[0];
-  const uint32_t *wc = sl.fc[0];
-  if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
-  for (int i = tid; i < WIN; i += BS) S.u.b.map[i] = 0;
-  __syncthreads();
-  // M2: mark present entities
-  for (int i = beg + tid; i < end; i += BS) S.u.b.map[wt[i] - lo] = 1;
-  __syncthreads();
-  PSTAMP(0);
-  // M3: slots in ascending entity order
-  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = S.u.b.map[i];
-  __syncthreads();
-  const int nc = scan_win(S.u.b.cnt, S.ws);
-  for (int i = tid; i < WIN; i += BS) {
-    if (S.u.b.map[i]) {
-      const int slot = S.u.b.cnt[i];
-      S.u.b.map[i] = slot;
-      S.u.b.st[slot] = lo + i;
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
-  __syncthreads();
-  PSTAMP(1);
-  if (degree_only) {
-    // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
-    for (int i = beg + tid; i < end; i += BS)
-      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[wt[i] - lo]]),
-                wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
-    __syncthreads();
-    for (int s2 = tid; s2 < nc; s2 += BS) {
-      const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
-      atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
-    }
-    __syncthreads();
-    return nc;
-  }
-  // M4: bucket sizes
-  for (int i = beg + tid; i < end; i += BS) atomicAdd(&S.u.b.cnt[S.u.b.map[wt[i] - lo]], 1);
-  __syncthreads();
-  PSTAMP(2);
-  // M5: bucket offsets (relative to beg)
-  for (int i = tid; i < WIN; i += BS) S.u.b.off[i] = S.u.b.cnt[i];
-  __syncthreads();
-  scan_win(S.u.b.off, S.ws);
-  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
-  __syncthreads();
-  PSTAMP(3);
-  // M6: scatter (node, count) into buckets
-  for (int i = beg + tid; i < end; i += BS) {
-    const int s2 = S.u.b.map[wt[i] - lo];
-    const int pos = beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
-    sl.bn[pos] = wn[i];
-    sl.bc[pos] = wc[i];
-  }
-  wg_sync_global();
-  PSTAMP(4);
-  // M7: one lane per candidate
-  for (int s2 = tid; s2 < nc; s2 += BS)
-    score_candidate<AGG>(p, W, S, sl, q, S.u.b.st[s2], beg + S.u.b.off[s2], S.u.b.cnt[s2], mean_scale);
-  __syncthreads();
-  PSTAMP(5);
-  return nc;
-}
-
-// Counting sort of the contributions by entity window into fn/fv/fc[0]
-// (free during phase B), then window_pass over every non-empty window.
-template <int AGG>
-__device__ int candidates_phase(const KParams &p, const float *__restrict__ W, Smem &S, const Slot &sl, int q,
-                                int P, bool degree_only, float mean_scale, bool sorted) {
-  const int tid = threadIdx.x;
-  const int nwin = (p.g.E + WIN - 1) >> WBITS;
-  if (!sorted) {
-    for (int i = tid; i < nwin; i += BS) S.whist[i] = 0;
-    __syncthreads();
-    for (int i = tid; i < P; i += BS) atomicAdd(&S.whist[sl.ct[i] >> WBITS], 1);
-    __syncthreads();
-    if (tid == 0) {
-      int acc = 0;
-      for (int w = 0; w < nwin; ++w) {
-        const int c = S.whist[w];
-        S.wbeg[w] = acc;
-        S.wfill[w] = acc;
-        acc += c;
-      }
-      S.wbeg[nwin] = acc;
-    }
-    __syncthreads();
-    for (int i = tid; i < P; i += BS) {
-      const int t = sl.ct[i];
-      const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
-      sl.fn[0][pos] = t;
-      sl.fv[0][pos] = sl.cn[i];
-      sl.fc[0][pos] = sl.cc[i];
-    }
-    wg_sync_global();
-  }
-  int ncand = 0;
-  for (int w = 0; w < nwin; ++w) {
-    const int beg = S.wbeg[w], end = S.wbeg[w + 1];
-    if (beg == end) continue;
-    ncand += window_pass<AGG>(p, W, S, sl, q, w << WBITS, beg, end, degree_only, mean_scale);
-  }
-  return ncand;
-}
-
 // ---------------------------------------------------------------- phase A
-__device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, int h, int r, int root, int rm_src,
+__device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, int r, int root, int rm_src,
                              int rm_dst) {
   const int tid = threadIdx.x;
   const int E = p.g.E, R = p.g.R;
@@ -561,10 +350,11 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, i
           deg = p.g.off[o + 1] - beg;
           S.it_child[tid] = child;
           S.it_beg[tid] = beg;
-          S.it_v[tid] = v;
-          S.it_rel[tid] = rel;
           S.it_c[tid] = S.ent_c[ent];
-          S.it_flags[tid] = (p.rl.node_nrules[child] > 0 ? 1 : 0) | (p.rl.node_nchild[child] > 0 ? 2 : 0);
+          // bit 0: leaf (rules end here), bit 1: inner (has children),
+          // bit 2: this hop may traverse the query's own edge (data.py:143-146)
+          S.it_flags[tid] = (p.rl.node_nrules[child] > 0 ? 1 : 0) | (p.rl.node_nchild[child] > 0 ? 2 : 0) |
+                            (rel == r && v == rm_src ? 4 : 0);
         }
         int NE;
         const int eoff = block_scan(deg, S.ws, NE);
@@ -576,11 +366,10 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, i
           if (j < NE) {
             const int it = upper_idx(S.edge_off, nit, j);
             const int tt = p.g.col[S.it_beg[it] + (j - S.edge_off[it])];
-            const int rel = S.it_rel[it];
-            if (!(rel == r && S.it_v[it] == rm_src && tt == rm_dst)) {
+            const int fl = S.it_flags[it];
+            if (!((fl & 4) && tt == rm_dst)) {
               const int child = S.it_child[it];
               const uint32_t c = S.it_c[it];
-              const int fl = S.it_flags[it];
               if (fl & 1) emit_contrib(S, sl, p.pcap, tt, child, c);
               if (fl & 2) {
                 if (!hash_add(S, (child - root) * E + tt, c)) emit_frontier(S, sl, nxt, p.fcap, child, tt, c);
@@ -609,23 +398,163 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int q, i
   }
 }
 
+// ---------------------------------------------------------------- phase B
+// Exclusive scan of WIN ints in place (PER consecutive per thread); returns the total.
+__device__ __forceinline__ int scan_win(int *a, int *s_ws) {
+  constexpr int PER = WIN / BS;
+  const int tid = threadIdx.x;
+  int loc[PER];
+  int sum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    loc[j] = a[tid * PER + j];
+    sum += loc[j];
+  }
+  int total;
+  int base = block_scan(sum, s_ws, total);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    a[tid * PER + j] = base;
+    base += loc[j];
+  }
+  __syncthreads();
+  return total;
+}
+
+// One entity window [lo, lo + WIN) whose contributions are wt/wn/wc[beg, end):
+// candidate records for it are written at pool indices cbase + [0, nc) and
+// its buckets at pool indices qbase + beg + [0, end - beg).  degree_only (PNA
+// sweep 1) accumulates sum log(degree) instead.  Returns nc.
+__device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, int beg, int end, int64_t cbase,
+                           bool degree_only) {
+  const int tid = threadIdx.x;
+  const int32_t *wt = sl.fn[0], *wn = sl.fv[0];
+  const uint32_t *wc = sl.fc[0];
+  if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
+  for (int i = tid; i < WIN; i += BS) S.u.b.map[i] = 0;
+  __syncthreads();
+  for (int i = beg + tid; i < end; i += BS) S.u.b.map[wt[i] - lo] = 1;  // mark present entities
+  __syncthreads();
+  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = S.u.b.map[i];
+  __syncthreads();
+  const int nc = scan_win(S.u.b.cnt, S.ws);  // slots in ascending entity order
+  for (int i = tid; i < WIN; i += BS) {
+    if (S.u.b.map[i]) {
+      const int slot = S.u.b.cnt[i];
+      S.u.b.map[i] = slot;
+      S.u.b.st[slot] = lo + i;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
+  __syncthreads();
+  PSTAMP(0);
+  if (degree_only) {
+    // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
+    for (int i = beg + tid; i < end; i += BS)
+      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[wt[i] - lo]]),
+                wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
+    __syncthreads();
+    for (int s2 = tid; s2 < nc; s2 += BS) {
+      const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
+      atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
+    }
+    __syncthreads();
+    return nc;
+  }
+  for (int i = beg + tid; i < end; i += BS) atomicAdd(&S.u.b.cnt[S.u.b.map[wt[i] - lo]], 1);  // bucket sizes
+  __syncthreads();
+  for (int i = tid; i < WIN; i += BS) S.u.b.off[i] = S.u.b.cnt[i];
+  __syncthreads();
+  scan_win(S.u.b.off, S.ws);
+  // candidate records
+  const int64_t qb = S.qbase;
+  for (int s2 = tid; s2 < nc; s2 += BS) {
+    p.c_t[cbase + s2] = S.u.b.st[s2];
+    p.c_beg[cbase + s2] = (int32_t)(qb + beg + S.u.b.off[s2]);
+    p.c_cnt[cbase + s2] = S.u.b.cnt[s2];
+  }
+  __syncthreads();
+  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
+  __syncthreads();
+  PSTAMP(1);
+  for (int i = beg + tid; i < end; i += BS) {  // scatter (node, count) into the buckets
+    const int s2 = S.u.b.map[wt[i] - lo];
+    const int64_t pos = qb + beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
+    p.b_node[pos] = wn[i];
+    p.b_cnt[pos] = wc[i];
+  }
+  __syncthreads();
+  PSTAMP(2);
+  return nc;
+}
+
+// Counting sort of the contributions by entity window into fn/fv/fc[0]
+// (free during phase B), then window_pass over every non-empty window.
+__device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P, bool degree_only, bool sorted) {
+  const int tid = threadIdx.x;
+  const int nwin = (p.g.E + WIN - 1) >> WBITS;
+  if (!sorted) {
+    for (int i = tid; i < nwin; i += BS) S.whist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < P; i += BS) atomicAdd(&S.whist[sl.ct[i] >> WBITS], 1);
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int w = 0; w < nwin; ++w) {
+        const int c = S.whist[w];
+        S.wbeg[w] = acc;
+        S.wfill[w] = acc;
+        acc += c;
+      }
+      S.wbeg[nwin] = acc;
+    }
+    __syncthreads();
+    for (int i = tid; i < P; i += BS) {
+      const int t = sl.ct[i];
+      const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
+      sl.fn[0][pos] = t;
+      sl.fv[0][pos] = sl.cn[i];
+      sl.fc[0][pos] = sl.cc[i];
+    }
+    wg_sync_global();
+  }
+  int ncand = 0;
+  for (int w = 0; w < nwin; ++w) {
+    const int beg = S.wbeg[w], end = S.wbeg[w + 1];
+    if (beg == end) continue;
+    ncand += window_pass(p, S, sl, w << WBITS, beg, end, S.qbase + ncand, degree_only);
+  }
+  return ncand;
+}
+
+__device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, Smem &S, int q) {
+  atomicOr(&hdr[H_STATUS], S.err ? 2u : 1u);
+  if (S.err) {
+    atomicOr(&hdr[H_ERRBITS], (unsigned)S.err);
+    atomicExch(&hdr[H_ERRQ], (unsigned)q);
+  }
+  if (p.n_cand) p.n_cand[q] = S.err ? -2 : -1;
+}
+
 template <int AGG>
-__global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const float *__restrict__ W) {
+__global__ __launch_bounds__(BS) void ground_kernel(KParams p) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
-  const Slot sl = make_slot(p.ws, blockIdx.x, p.fcap, p.pcap);
+  unsigned long long *pool_ctr = reinterpret_cast<unsigned long long *>(p.ws + 64);
+  const Slot sl = make_slot(p.slots, blockIdx.x, p.fcap, p.pcap);
   for (int s = tid; s < HCAP; s += BS) {
     S.u.a.key[s] = EMPTY;
     S.u.a.val[s] = 0u;
   }
-  __syncthreads();
   unsigned long long pr[6] = {0, 0, 0, 0, 0, 0};
   if (tid < 8) S.tp[tid] = 0ull;
   unsigned long long t_q = 0, t_a = 0;
+  __syncthreads();
 #pragma unroll 1
   while (true) {
-    if (tid == 0) S.q = (int)atomicAdd(&hdr[1], 1u);
+    if (tid == 0) S.q = (int)atomicAdd(&hdr[H_DEQUEUE], 1u);
     __syncthreads();
     const int q = S.q;
     if (q >= p.nq) break;
@@ -635,8 +564,8 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const floa
     const int root = p.rl.head_root[r];
     if (root < 0) {
       if (tid == 0) {
-        if (p.n_cand) p.n_cand[q] = 0;
-        if (p.digest) p.digest[q] = 0;
+        p.n_cand[q] = 0;
+        p.q_base[q] = 0;
       }
       __syncthreads();
       continue;
@@ -657,17 +586,10 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const floa
       S.nd = 0;
       S.ovf = 0;
       S.sumlog = 0ull;
-      S.dig = 0ull;
-    }
-    if (tid < 128) {
-      // relation half of score_model.layers.0 folded into a per-query bias
-      float acc = p.s0_b[tid];
-      for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[tid * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
-      S.relb[tid] = acc;
     }
     __syncthreads();
     if (p.prof && tid == 0) t_a = __builtin_amdgcn_s_memtime();
-    ground_query(p, S, sl, q, h, r, root, rm_src, rm_dst);
+    ground_query(p, S, sl, h, r, root, rm_src, rm_dst);
     wg_sync_global();
     if (p.prof && tid == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -676,45 +598,36 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const floa
       t_a = t;
     }
     const int P = S.np;
+    if (tid == 0 && !S.ovf && !S.err && P <= p.pcap) {
+      // reserve the query's pool run: P bucket entries and <= P candidate records
+      const unsigned long long b = atomicAdd(pool_ctr, (unsigned long long)P);
+      if (b + P > (unsigned long long)p.pool_cap) S.ovf = 1;
+      S.qbase = (long long)b;
+    }
+    __syncthreads();
     if (S.ovf || P > p.pcap || S.err) {
-      // leave the LDS hash clean for the next query
-      for (int s = tid; s < HCAP; s += BS) {
+      for (int s = tid; s < HCAP; s += BS) {  // leave the LDS hash clean for the next query
         S.u.a.key[s] = EMPTY;
         S.u.a.val[s] = 0u;
       }
-      if (tid == 0) {
-        atomicOr(&hdr[0], S.err ? 2u : 1u);
-        if (S.err) {
-          atomicOr(&hdr[2], (unsigned)S.err);
-          atomicExch(&hdr[3], (unsigned)q);
-        }
-        if (p.n_cand) p.n_cand[q] = S.err ? -2 : -1;
-      }
+      if (tid == 0) flag_error(p, hdr, S, q);
       __syncthreads();
       continue;
     }
-    float mean_scale = 0.f;
     bool sorted = false;
     if constexpr (AGG == RNNL_AGG_PNA) {
       // sweep 1: per-query mean of log(degree) over candidates (layers.py:109-116)
-      if (tid == 0) S.sumlog = 0ull;
-      const int nc1 = candidates_phase<AGG>(p, W, S, sl, q, P, true, 0.f, false);
+      const int nc1 = candidates_phase(p, S, sl, P, true, false);
       sorted = true;
-      const double sum = (double)(long long)S.sumlog / 4294967296.0;
-      mean_scale = (float)((float)sum / fmaxf((float)nc1, 1e-6f));
+      if (tid == 0) {
+        const double sum = (double)(long long)S.sumlog / 4294967296.0;
+        p.q_scale[q] = (float)((float)sum / fmaxf((float)nc1, 1e-6f));
+      }
     }
-    if (tid == 0) S.dig = 0ull;
-    __syncthreads();
-    const int ncand = candidates_phase<AGG>(p, W, S, sl, q, P, false, mean_scale, sorted);
-    if (tid == 0 && S.err) {
-      // diagnostics: hdr[2] |= error bits, hdr[3] = last failing query
-      atomicOr(&hdr[2], (unsigned)S.err);
-      atomicExch(&hdr[3], (unsigned)q);
-      atomicOr(&hdr[0], 2u);
-    }
+    const int ncand = candidates_phase(p, S, sl, P, false, sorted);
     if (tid == 0) {
-      if (p.n_cand) p.n_cand[q] = S.err ? -2 : ncand;
-      if (p.digest) p.digest[q] = S.dig;
+      p.n_cand[q] = ncand;
+      p.q_base[q] = S.qbase;
       if (p.prof) {
         pr[2] += __builtin_amdgcn_s_memtime() - t_a;
         pr[3] += 1;
@@ -722,8 +635,7 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const floa
         pr[5] += ncand;
       }
     }
-    // restore the phase-A hash (phase B reused its LDS)
-    for (int s = tid; s < HCAP; s += BS) {
+    for (int s = tid; s < HCAP; s += BS) {  // restore the phase-A hash (phase B reused its LDS)
       S.u.a.key[s] = EMPTY;
       S.u.a.val[s] = 0u;
     }
@@ -731,11 +643,189 @@ __global__ __launch_bounds__(BS) void predictorplus_kernel(KParams p, const floa
   }
   if (p.prof && tid == 0) {
     for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[k], pr[k]);
-    for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
+    for (int k = 0; k < 3; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
   }
 }
 
-// Packs the MLP weights into the workspace header (layout W_* above).
+// ---------------------------------------------------------------- K2: scoring
+template <int AGG>
+__device__ __forceinline__ float score_one(const KParams &p, const float *__restrict__ wl, const float *relb,
+                                           int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
+  using L = WL<AGG>;
+  constexpr int STRIDE = AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna;
+  long long a1[16];
+  long long a2[AGG == RNNL_AGG_PNA ? 16 : 1];
+  float mn[AGG == RNNL_AGG_PNA ? 16 : 1], mx[AGG == RNNL_AGG_PNA ? 16 : 1];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) a1[d] = 0;
+  if constexpr (AGG == RNNL_AGG_PNA) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a2[d] = 0;
+      mn[d] = __builtin_huge_valf();
+      mx[d] = -__builtin_huge_valf();
+    }
+  }
+  long long deg = 0;
+  uint64_t fp = 0;
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int n = p.b_node[e];
+    const long long c = p.b_cnt[e];
+    const long long *rec = reinterpret_cast<const long long *>(p.node_w + (int64_t)n * STRIDE);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) a1[d] += c * rec[d];
+    deg += c * p.rl.node_nrules[n];
+    if (dig_out) fp += (uint64_t)c * p.rl.node_fp[n];
+    if constexpr (AGG == RNNL_AGG_PNA) {
+#pragma unroll
+      for (int d = 0; d < 16; ++d) a2[d] += c * rec[16 + d];
+      const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        mn[d] = fminf(mn[d], fr[d]);
+        mx[d] = fmaxf(mx[d], fr[16 + d]);
+      }
+    }
+  }
+  if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+  constexpr double inv_fix = 1.0 / (double)(1 << kFixShift);
+  float x1[16];
+  if constexpr (AGG == RNNL_AGG_SUM) {
+    // FuncToNodeSum: Linear(16,16) on the rule-weighted sum (layers.py:68-74)
+    float f[16];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) f[d] = (float)((double)a1[d] * inv_fix);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc = fmaf(f[i], wl[L::ADDW + o * 16 + i], acc);
+      x1[o] = acc + wl[L::ADDB + o];
+    }
+  } else {
+    // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123)
+    const float degf = (float)(deg + 1);
+    const float dcl = fmaxf(degf, 1e-6f);
+    float feat[64];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      const float s = (float)((double)a1[d] * inv_fix);
+      const float sq = (float)((double)a2[d] * inv_fix);
+      const float mean = s / dcl;
+      const float sqm = sq / dcl;
+      feat[d] = mean;
+      feat[16 + d] = mn[d];
+      feat[32 + d] = mx[d];
+      feat[48 + d] = sqrtf(fmaxf(sqm - mean * mean, 1e-6f));
+    }
+    const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
+    const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
+#pragma unroll 1
+    for (int o = 0; o < 16; ++o) {
+      float acc = 0.f;
+#pragma unroll
+      for (int f = 0; f < 64; ++f) {
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) acc = fmaf(feat[f] * sc[s3], wl[L::ADDW + o * 192 + f * 3 + s3], acc);
+      }
+      x1[o] = acc + wl[L::ADDB + o];
+    }
+  }
+  // LayerNorm(16) + ReLU (layers.py:74-75 / 124-125)
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+  // score_model: Linear(32,128) [relation half folded into relb], ReLU, Linear(128,1)
+  float out = 0.f;
+#pragma unroll 2
+  for (int o = 0; o < 128; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], wl[L::S0X + o * 16 + i], acc);
+    acc = fmaxf(acc + relb[o], 0.f);
+    out = fmaf(acc, wl[L::S1W + o], out);
+  }
+  return out + wl[L::S1B];
+}
+
+template <int AGG>
+__global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__restrict__ W) {
+  using L = WL<AGG>;
+  __shared__ __attribute__((aligned(16))) float s_w[L::N];
+  __shared__ float s_relb[128];
+  __shared__ int s_q;
+  __shared__ unsigned long long s_dig;
+  const int tid = threadIdx.x;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  for (int i = tid; i < L::N; i += BS) {
+    float v = 0.f;
+    if (i < L::ADDB) v = W[W_ADDW + i];
+    else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
+    else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
+    else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
+    else if (i < L::S1W) v = W[W_S0X + i - L::S0X];
+    else if (i < L::S1B) v = W[W_S1W + i - L::S1W];
+    else if (i == L::S1B) v = W[W_S1B];
+    s_w[i] = v;
+  }
+#pragma unroll 1
+  while (true) {
+    __syncthreads();
+    if (tid == 0) {
+      s_q = (int)atomicAdd(&hdr[H_DEQUEUE2], 1u);
+      s_dig = 0ull;
+    }
+    __syncthreads();
+    const int q = s_q;
+    if (q >= p.nq) break;
+    const int nc = p.n_cand[q];
+    if (nc <= 0) {
+      if (tid == 0 && p.digest && nc == 0) p.digest[q] = 0;
+      continue;
+    }
+    const int r = (int)p.all_r[q];
+    if (tid < 128) {
+      // relation half of score_model.layers.0 folded into a per-query bias
+      float acc = p.s0_b[tid];
+      for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[tid * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+      s_relb[tid] = acc;
+    }
+    __syncthreads();
+    const int64_t qb = p.q_base[q];
+    const float ms = AGG == RNNL_AGG_PNA ? p.q_scale[q] : 0.f;
+    for (int s = tid; s < nc; s += BS) {
+      const int t = p.c_t[qb + s];
+      uint64_t dg = 0;
+      // keep the loop-invariant LDS weight reads inside the loop (hoisted,
+      // they would pin ~200 VGPRs and starve occupancy)
+      asm volatile("" ::: "memory");
+      const float out = score_one<AGG>(p, s_w, s_relb, p.c_beg[qb + s], p.c_cnt[qb + s], ms,
+                                       p.digest ? &dg : nullptr, t);
+      if (p.digest) atomicAdd(&s_dig, (unsigned long long)dg);
+      const int64_t idx = (int64_t)q * p.g.E + t;
+      if (p.feature == RNNL_FEATURE_NONE)
+        p.score[idx] = out;
+      else
+        p.score[idx] = out + p.score[idx];
+      if (p.mask) p.mask[idx] = 1;
+    }
+    __syncthreads();
+    if (tid == 0 && p.digest) p.digest[q] = s_dig;
+  }
+}
+
+// Packs the MLP weights behind the workspace header (layout W_* above).
 __global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
   const int kin = p.agg == RNNL_AGG_SUM ? 16 : 192;
   for (int i = threadIdx.x; i < W_FLOATS; i += blockDim.x) {
@@ -808,15 +898,12 @@ int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, v
   return RNNL_OK;
 }
 
-static int nslots_for(int32_t nq) { return (int)std::min<int64_t>(nq, (int64_t)NUM_CU * WG_PER_CU); }
-
 int rnnl_forward_workspace_size(rnnl_graph g, rnnl_rules r, int32_t nq, int32_t scale, size_t *bytes) {
   if (!g || !r || !bytes || nq < 0 || scale < 1) {
     set_error("rnnl_forward_workspace_size: bad arguments");
     return RNNL_ERR_INVALID;
   }
-  const int64_t fcap = FCAP_BASE * scale, pcap = PCAP_BASE * scale;
-  *bytes = (size_t)(HDR_BYTES + (int64_t)std::max(1, nslots_for(nq)) * slot_bytes(fcap, pcap));
+  *bytes = (size_t)make_layout(nq, scale).total;
   return RNNL_OK;
 }
 
@@ -824,7 +911,7 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
                                const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
                                int32_t *n_cand, uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale,
                                void *stream) {
-  if (!g || !r || !pp || !all_h || !all_r || !score || !ws || nq < 0 || scale < 1 || !pp->node_w ||
+  if (!g || !r || !pp || !all_h || !all_r || !score || !ws || !n_cand || nq < 0 || scale < 1 || !pp->node_w ||
       (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA)) {
     set_error("rnnl_predictorplus_forward: bad arguments");
     return RNNL_ERR_INVALID;
@@ -833,15 +920,19 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
     set_error("rnnl_predictorplus_forward: more entities than the kernel's window table supports");
     return RNNL_ERR_INVALID;
   }
-  size_t need = 0;
-  rnnl_forward_workspace_size(g, r, nq, scale, &need);
-  if (ws_bytes < need) {
+  const Layout Ly = make_layout(nq, scale);
+  if ((int64_t)ws_bytes < Ly.total) {
     set_error("rnnl_predictorplus_forward: workspace too small");
     return RNNL_ERR_INVALID;
   }
+  if (Ly.pool_cap >= INT32_MAX) {
+    set_error("rnnl_predictorplus_forward: too many rows for one launch (pool index exceeds 31 bits)");
+    return RNNL_ERR_INVALID;
+  }
   hipStream_t st = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, 256, st));
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
   if (nq == 0) return RNNL_OK;
+  unsigned char *base = static_cast<unsigned char *>(ws);
   KParams p;
   p.g = g->d;
   p.rl = r->d;
@@ -865,17 +956,30 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   p.mask = mask;
   p.n_cand = n_cand;
   p.digest = digest;
-  p.ws = static_cast<unsigned char *>(ws);
-  p.fcap = FCAP_BASE * scale;
-  p.pcap = PCAP_BASE * scale;
-  p.nslots = nslots_for(nq);
+  p.ws = base;
+  p.fcap = Ly.fcap;
+  p.pcap = Ly.pcap;
+  p.pool_cap = Ly.pool_cap;
+  p.nslots = (int32_t)Ly.nslots;
+  p.slots = base + Ly.off_slots;
+  p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
+  p.q_scale = reinterpret_cast<float *>(base + Ly.off_qscale);
+  p.c_t = reinterpret_cast<int32_t *>(base + Ly.off_ct);
+  p.c_beg = reinterpret_cast<int32_t *>(base + Ly.off_cbeg);
+  p.c_cnt = reinterpret_cast<int32_t *>(base + Ly.off_ccnt);
+  p.b_node = reinterpret_cast<int32_t *>(base + Ly.off_bnode);
+  p.b_cnt = reinterpret_cast<uint32_t *>(base + Ly.off_bcnt);
   p.prof = g_prof;
-  float *W = reinterpret_cast<float *>(p.ws + 256);
+  float *W = reinterpret_cast<float *>(base + HDR_WORDS_BYTES);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
-  if (pp->aggregator == RNNL_AGG_SUM)
-    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p, (const float *)W);
-  else
-    hipLaunchKernelGGL(predictorplus_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p, (const float *)W);
+  const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
+  if (pp->aggregator == RNNL_AGG_SUM) {
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+    hipLaunchKernelGGL(score_kernel<RNNL_AGG_SUM>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
+  } else {
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
+    hipLaunchKernelGGL(score_kernel<RNNL_AGG_PNA>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
+  }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
@@ -886,15 +990,15 @@ int rnnl_debug_profile(void *dev_counters) {
 }
 
 int rnnl_forward_status(void *ws, void *stream) {
-  unsigned int st[4] = {0, 0, 0, 0};
+  unsigned int st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
   RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-  if (st[0] & 2u) {
-    set_error("rnnl_predictorplus_forward: internal error bits 0x" + std::to_string(st[2]) +
-              " (1: candidate lookup miss, 2: bucket overflow, 4: watchdog) at query " + std::to_string(st[3]));
+  if (st[H_STATUS] & 2u) {
+    set_error("rnnl_predictorplus_forward: internal error bits 0x" + std::to_string(st[H_ERRBITS]) +
+              " (4: watchdog) at query " + std::to_string(st[H_ERRQ]));
     return RNNL_ERR_INTERNAL;
   }
-  if (st[0] & 1u) {
+  if (st[H_STATUS] & 1u) {
     set_error("rnnl_predictorplus_forward: workspace capacity exceeded");
     return RNNL_ERR_OVERFLOW;
   }
