@@ -14,6 +14,8 @@
 // table traffic is |E| * 8D bytes per 32 queries (L2/MALL resident).
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include "internal.h"
 
 namespace rnnl {
@@ -84,6 +86,117 @@ __global__ __launch_bounds__(RB) void rotate_kernel(const float *__restrict__ ee
       score[idx] = accumulate ? score[idx] + v : v;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA formulation.  For one dimension d the squared distance of every
+// (query q, entity e) pair is a K = 4 contraction:
+//   s = (hr_re - a)^2 + (hr_im - b)^2
+//     = [-2 hr_re, -2 hr_im, |hr|^2, 1] . [a, b, 1, a^2 + b^2]
+// so one v_mfma_f32_16x16x4_f32 yields s for a 16 x 16 tile (exact fp32
+// fmaf chain), and the VALU is left with sqrt(|s|) + accumulate per term
+// (|s| absorbs a rounding-negative s at a near-zero distance; abs is a free
+// source modifier).  Block = 64 queries x 256 entities, wave = 64 x 64
+// (16 tiles, 64 accumulator VGPRs); A fragments (per query) come from LDS,
+// B fragments (per entity) from the transposed table, one dword per lane.
+constexpr int MQ = 64;   // queries per block
+constexpr int ME = 256;  // entities per block (64 per wave)
+constexpr int MDC = 32;  // dims per LDS chunk
+constexpr int MQP = MQ + 16;  // padded row (bank spread of the 4 k-groups)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void rotate_mfma_kernel(const float *__restrict__ eemb,
+                                                          const float *__restrict__ eemb_t,
+                                                          const float *__restrict__ remb, int D, float gamma,
+                                                          const int64_t *__restrict__ all_h,
+                                                          const int64_t *__restrict__ all_r, int nq, int E,
+                                                          float *__restrict__ score, int accumulate) {
+  __shared__ __attribute__((aligned(16))) float sA[MDC][4][MQP];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int k = lane >> 4, i16 = lane & 15;
+  const int q0 = blockIdx.y * MQ;
+  const int e_base = blockIdx.x * ME + wave * 64;
+  const float div = (float)(((double)gamma + 2.0) / (double)D / 3.141592653589793238462643383279);
+  // entity of this lane in each of the 4 entity groups; loads are clamped in-range
+  int ecol[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) ecol[g] = min(e_base + g * 16 + i16, E - 1);
+  const int plane = (k & 1) ? D : 0;  // k = 0, 2: real plane; k = 1, 3: imaginary plane
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int qg = 0; qg < 4; ++qg)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[qg][g] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int d0 = 0; d0 < D; d0 += MDC) {
+    const int nd = min(MDC, D - d0);
+    __syncthreads();
+    // A fragments for MQ queries x nd dims: [-2 re, -2 im, |hr|^2, 1] of h o r
+    for (int idx = tid; idx < MQ * MDC; idx += 256) {
+      const int qq = idx / MDC, dd = idx % MDC;
+      float re = 0.f, im = 0.f;
+      if (q0 + qq < nq && dd < nd) {
+        const int64_t h = all_h[q0 + qq], r = all_r[q0 + qq];
+        const int d = d0 + dd;
+        const float ph = remb[r * D + d] / div;
+        const float cr = cosf(ph), sr = sinf(ph);
+        const float rh = eemb[h * 2 * D + d], ih = eemb[h * 2 * D + D + d];
+        re = rh * cr - ih * sr;
+        im = rh * sr + ih * cr;
+      }
+      sA[dd][0][qq] = -2.f * re;
+      sA[dd][1][qq] = -2.f * im;
+      sA[dd][2][qq] = fmaf(re, re, im * im);
+      sA[dd][3][qq] = (dd < nd) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    float v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = eemb_t[(int64_t)(plane + d0) * E + ecol[g]];
+    for (int dd = 0; dd < nd; ++dd) {
+      // prefetch the next dimension's table values
+      float vn[4];
+      const int dn = min(dd + 1, nd - 1);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) vn[g] = eemb_t[(int64_t)(plane + d0 + dn) * E + ecol[g]];
+      float b[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float o = __shfl_xor(v[g], 16, 64);  // k = 3 lanes: real part from their k = 2 partner
+        b[g] = k == 0 || k == 1 ? v[g] : (k == 2 ? 1.f : fmaf(o, o, v[g] * v[g]));
+      }
+      float a[4];
+#pragma unroll
+      for (int qg = 0; qg < 4; ++qg) a[qg] = sA[dd][k][qg * 16 + i16];
+#pragma unroll
+      for (int qg = 0; qg < 4; ++qg) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 s = __builtin_amdgcn_mfma_f32_16x16x4f32(a[qg], b[g], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[qg][g][j] += __builtin_amdgcn_sqrtf(__builtin_fabsf(s[j]));
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v[g] = vn[g];
+    }
+  }
+  // D layout: lane holds entity column i16 of group g, query rows 4k + j of group qg
+#pragma unroll
+  for (int qg = 0; qg < 4; ++qg)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = q0 + qg * 16 + k * 4 + j;
+        const int e = e_base + g * 16 + i16;
+        if (q < nq && e < E) {
+          const int64_t idx = (int64_t)q * E + e;
+          const float val = gamma - acc[qg][g][j];
+          score[idx] = accumulate ? score[idx] + val : val;
+        }
+      }
 }
 
 __global__ void transpose_kernel(const float *__restrict__ in, int rows, int cols, float *__restrict__ out) {
@@ -162,8 +275,13 @@ int rnnl_rotate_score(const float *eemb, const float *eemb_t, const float *remb,
     return RNNL_ERR_INVALID;
   }
   if (nq == 0) return RNNL_OK;
-  hipLaunchKernelGGL(rotate_kernel, dim3((E + RB - 1) / RB, (nq + QB - 1) / QB), dim3(RB), 0,
-                     (hipStream_t)stream, eemb, eemb_t, remb, D, gamma, all_h, all_r, nq, E, score, accumulate);
+  static const bool valu = getenv("RNNL_ROTATE_VALU") != nullptr;  // diagnostic: VALU-only variant
+  if (valu)
+    hipLaunchKernelGGL(rotate_kernel, dim3((E + RB - 1) / RB, (nq + QB - 1) / QB), dim3(RB), 0,
+                       (hipStream_t)stream, eemb, eemb_t, remb, D, gamma, all_h, all_r, nq, E, score, accumulate);
+  else
+    hipLaunchKernelGGL(rotate_mfma_kernel, dim3((E + ME - 1) / ME, (nq + MQ - 1) / MQ), dim3(256), 0,
+                       (hipStream_t)stream, eemb, eemb_t, remb, D, gamma, all_h, all_r, nq, E, score, accumulate);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
