@@ -176,18 +176,27 @@ def main():
     ground_bytes = 12 * F + 12 * T + 8 * P + 4 * nq * E
     D = model.RotatE.emb_dim if args.feature == "RotatE" else 0
     rotate_flops = 7.0 * nq * E * D
-    rotate_bytes = 8.0 * D * E * ((nq + 31) // 32) + 8.0 * D * nq + 4.0 * nq * E
+    rotate_bytes = 8.0 * D * E * ((nq + 15) // 16) + 8.0 * D * nq + 4.0 * nq * E
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
               "traffic": None, "kernel": "predictorplus_kernel", "ms": round(ground_ms, 3),
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
     if args.feature == "RotatE":
         ach = rotate_flops / (base_ms * 1e-3) / 1e12
+        mode = "direct" if model.RotatE.mode == 0 else "mfma"
+        # VALU issue: cycles per 64 terms on one SIMD at the 2.4 GHz nominal
+        # clock, against the measured floor of the kernel's instruction mix
+        # (tools/micro/valu_rates.hip: sub,sub,mul,fma + pipelined sqrt + add
+        # = 19.1; bf16 MFMA + sqrt + add = 13.1)
+        cyc = base_ms * 1e-3 * 2.4e9 * 1024 / (nq * E * D / 64.0)
+        floor = 19.1 if mode == "direct" else 13.1
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": None, "kernel": "rotate_kernel",
+                "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": None, "kernel": "rotate_%s_kernel" % mode,
                 "ms": round(base_ms, 3), "alg_flops": rotate_flops,
-                "note": "fp32 compute-bound on the VALU (one sqrt per term inside the reduction, not a GEMM); "
-                        "157.3 TF/s is the fp32 peak of both VALU and MFMA; table bytes %.3g per launch"
+                "valu_issue": {"cycles_per_64_terms": round(cyc, 2), "floor": floor, "frac": round(floor / cyc, 3)},
+                "note": "fp32 compute-bound on the VALU issue port (sub, sub, mul, fma, one quarter-rate sqrt and "
+                        "an add per term; the sqrt inside the reduction keeps it off the matrix cores); "
+                        "157.3 TF/s is the fp32 peak shared by VALU and MFMA; entity-table bytes %.3g per launch"
                         % rotate_bytes}
         dominant = roof if base_ms >= ground_ms else ground
     else:

@@ -137,13 +137,35 @@ int rnnl_fill_value(float value, int64_t n, float *score, void *stream);
 /* RotatE entity feature (reference src/embedding.py:28-70):
  * score[q][e] = gamma - sum_d |(h_q o r_q)_d - e_d|, complex entries stored
  * [re(0:D) | im(D:2D)]; relation ids >= n_rel_fwd use the negated half
- * (embedding.py:26).  eemb_t is the entity table transposed to 2D x E
- * (rnnl_rotate_transpose), remb is (n_rel_total x D).  accumulate != 0 adds
- * into score instead of overwriting. */
-int rnnl_rotate_transpose(const float *eemb, int32_t n_entities, int32_t dim2, float *eemb_t, void *stream);
-int rnnl_rotate_score(const float *eemb, const float *eemb_t, const float *remb, int32_t dim, float gamma,
-                      const int64_t *all_h, const int64_t *all_r, int32_t n_queries, int32_t n_entities,
-                      float *score, int32_t accumulate, void *stream);
+ * (embedding.py:26).  Two kernels (mode):
+ *   RNNL_ROTATE_DIRECT (default)  the reference's arithmetic term by term
+ *                                 (differences, squares, sqrt) on the VALU;
+ *   RNNL_ROTATE_MFMA              |hr - t|^2 expanded into a bf16x3 MFMA
+ *                                 contraction: ~1.7x faster, but the
+ *                                 expansion cancels when h o r ~= t (error up
+ *                                 to ~sqrt(2^-24 (|hr|^2+|t|^2)) per dim;
+ *                                 DESIGN.md "RotatE numerics").
+ * Weight-derived device tables, built once per weight version:
+ *   entity table    mode-specific layout (rnnl_rotate_entity_table, from eemb
+ *                   (E x 2 dim)); size from rnnl_rotate_table_sizes;
+ *   relation table  [n_rel_total][dim][2] (cos, sin) of the relation phase
+ *                   (rnnl_rotate_relation_table, from remb (n_rel_total x dim)).
+ * rnnl_rotate_score replaces RotatE.forward (embedding.py:45-70); it needs a
+ * per-call workspace of rnnl_rotate_workspace_size bytes (h o r of every
+ * query in DIRECT mode; 0 for MFMA).  accumulate != 0 adds into score. */
+#define RNNL_ROTATE_DIRECT 0
+#define RNNL_ROTATE_MFMA 1
+int rnnl_rotate_table_sizes(int32_t n_entities, int32_t dim, int32_t n_rel_total, int32_t mode,
+                            size_t *entity_bytes, size_t *relation_bytes);
+int rnnl_rotate_entity_table(const float *eemb, int32_t n_entities, int32_t dim, int32_t mode, void *entity_table,
+                             void *stream);
+int rnnl_rotate_relation_table(const float *remb, int32_t n_rel_total, int32_t dim, float gamma,
+                               float *relation_table, void *stream);
+int rnnl_rotate_workspace_size(int32_t n_queries, int32_t dim, int32_t mode, size_t *bytes);
+int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *relation_table, int32_t dim,
+                      float gamma, const int64_t *all_h, const int64_t *all_r, int32_t n_queries,
+                      int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
+                      size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

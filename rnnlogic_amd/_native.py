@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
 RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL = 0, 1, 2, 3, 4, 5
 AGG_SUM, AGG_PNA = 0, 1
 FEATURE_ADD, FEATURE_NONE = 0, 1
+ROTATE_DIRECT, ROTATE_MFMA = 0, 1
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -38,8 +39,12 @@ SIGNATURES = [
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
-    ("rnnl_rotate_transpose", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
-    ("rnnl_rotate_score", ctypes.c_int, [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _P]),
+    ("rnnl_rotate_table_sizes", ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P]),
+    ("rnnl_rotate_entity_table", ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    ("rnnl_rotate_relation_table", ctypes.c_int, [_P, _I32, _I32, _F32, _P, _P]),
+    ("rnnl_rotate_workspace_size", ctypes.c_int, [_I32, _I32, _I32, _P]),
+    ("rnnl_rotate_score", ctypes.c_int,
+     [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _I32, _P, ctypes.c_size_t, _P]),
 ]
 
 

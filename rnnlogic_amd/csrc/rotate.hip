@@ -5,188 +5,247 @@
 //   (re_r, im_r) = (cos, sin)(remb[r][d] / ((gamma + 2) / D / pi))
 // (reference src/embedding.py:28-70, forward at :64-70).
 //
-// Shape of the work: B queries x |E| entities x D complex dims, every term a
-// sqrt — VALU/transcendental-bound (about 5 FMA-class ops + 1 sqrt per term),
-// not a GEMM (the sqrt sits inside the reduction).  Each lane owns one entity
-// and QB = 32 query rows; the entity table is read transposed (2D x E) so a
-// wave's loads are 256 contiguous bytes, and h o r of the 32 rows sits in LDS
-// (uniform broadcast reads).  One pass over the table serves 32 rows, so the
-// table traffic is |E| * 8D bytes per 32 queries (L2/MALL resident).
+// Shape of the work: B queries x |E| entities x D complex dims, one sqrt per
+// term inside the reduction.  The sqrt is a quarter-rate transcendental
+// (8 issue cycles per wave64 instruction vs 2 for an FMA, measured with
+// tools/micro/valu_rates.hip), so the VALU issue port is the bound: the
+// kernel's job is to leave the VALU nothing but sqrt + accumulate.
+//
+// Weight-derived tables (built once per weight version, see RotatE in
+// rnnlogic_amd/embedding.py):
+//   etab [D][4][Ep]   per dim d and K group kg: the 4 bf16 B-operand slots
+//                     (8 bytes) of every entity for the MFMA contraction
+//                     below, built from the exact 3-part bf16 split of
+//                     a = re, b = im and m = a^2 + b^2; Ep = |E| rounded up to
+//                     256 and zero padded, so 16 lanes read 128 contiguous
+//                     bytes and never need clamping;
+//   rtab [R2][D][2]   (cos, sin) of every relation phase (R2 = 2 |R|, the
+//                     second half negated, embedding.py:26).
 #include <hip/hip_runtime.h>
-
-#include <stdlib.h>
 
 #include "internal.h"
 
 namespace rnnl {
 
-constexpr int RB = 256;  // entities per block (one per lane)
-constexpr int QB = 32;   // query rows per block
-constexpr int DC = 64;   // dims per LDS chunk
-
-__global__ __launch_bounds__(RB) void rotate_kernel(const float *__restrict__ eemb, const float *__restrict__ eemb_t,
-                                                    const float *__restrict__ remb, int D, float gamma,
-                                                    const int64_t *__restrict__ all_h,
-                                                    const int64_t *__restrict__ all_r, int nq, int E,
-                                                    float *__restrict__ score, int accumulate) {
-  __shared__ float s_re[DC][QB];
-  __shared__ float s_im[DC][QB];
-  const int tid = threadIdx.x;
-  const int e = blockIdx.x * RB + tid;
-  const int q0 = blockIdx.y * QB;
-  const int nrow = min(QB, nq - q0);
-  // torch computes vec / (range / pi) in fp32 with the divisor rounded to fp32
-  const float div = (float)(((double)gamma + 2.0) / (double)D / 3.141592653589793238462643383279);
-  float acc[QB];
-#pragma unroll
-  for (int k = 0; k < QB; ++k) acc[k] = 0.f;
-  for (int d0 = 0; d0 < D; d0 += DC) {
-    const int nd = min(DC, D - d0);
-    __syncthreads();
-    // h o r for QB rows x nd dims (RB lanes cover QB * DC = 2048 terms)
-    for (int i = tid; i < QB * DC; i += RB) {
-      const int k = i / DC, dd = i % DC;
-      float re = 0.f, im = 0.f;
-      if (k < nrow && dd < nd) {
-        const int q = q0 + k;
-        const int64_t h = all_h[q], r = all_r[q];
-        const int d = d0 + dd;
-        const float ph = remb[r * D + d] / div;
-        const float cr = cosf(ph), sr = sinf(ph);
-        const float rh = eemb[h * 2 * D + d], ih = eemb[h * 2 * D + D + d];
-        re = rh * cr - ih * sr;
-        im = rh * sr + ih * cr;
-      }
-      s_re[dd][k] = re;
-      s_im[dd][k] = im;
-    }
-    __syncthreads();
-    if (e < E) {
-      float part[QB];
-#pragma unroll
-      for (int k = 0; k < QB; ++k) part[k] = 0.f;
-      for (int dd = 0; dd < nd; ++dd) {
-        const float a = eemb_t[(int64_t)(d0 + dd) * E + e];
-        const float b = eemb_t[(int64_t)(D + d0 + dd) * E + e];
-#pragma unroll
-        for (int k = 0; k < QB; ++k) {
-          const float x = s_re[dd][k] - a;
-          const float y = s_im[dd][k] - b;
-          part[k] += __builtin_amdgcn_sqrtf(fmaf(x, x, y * y));  // v_sqrt_f32 (1 ulp)
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < QB; ++k) acc[k] += part[k];
-    }
-  }
-  if (e < E) {
-    for (int k = 0; k < nrow; ++k) {
-      const int64_t idx = (int64_t)(q0 + k) * E + e;
-      const float v = gamma - acc[k];
-      score[idx] = accumulate ? score[idx] + v : v;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// MFMA formulation.  For one dimension d the squared distance of every
-// (query q, entity e) pair is a K = 4 contraction:
-//   s = (hr_re - a)^2 + (hr_im - b)^2
-//     = [-2 hr_re, -2 hr_im, |hr|^2, 1] . [a, b, 1, a^2 + b^2]
-// so one v_mfma_f32_16x16x4_f32 yields s for a 16 x 16 tile (exact fp32
-// fmaf chain), and the VALU is left with sqrt(|s|) + accumulate per term
-// (|s| absorbs a rounding-negative s at a near-zero distance; abs is a free
-// source modifier).  Block = 64 queries x 256 entities, wave = 64 x 64
-// (16 tiles, 64 accumulator VGPRs); A fragments (per query) come from LDS,
-// B fragments (per entity) from the transposed table, one dword per lane.
-constexpr int MQ = 64;   // queries per block
-constexpr int ME = 256;  // entities per block (64 per wave)
-constexpr int MDC = 32;  // dims per LDS chunk
-constexpr int MQP = MQ + 16;  // padded row (bank spread of the 4 k-groups)
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void rotate_mfma_kernel(const float *__restrict__ eemb,
-                                                          const float *__restrict__ eemb_t,
-                                                          const float *__restrict__ remb, int D, float gamma,
+__host__ __device__ constexpr int64_t ent_pad(int64_t E) { return (E + 255) / 256 * 256; }
+
+// torch computes vec / (range / pi) in fp32 with the python-float divisor
+// rounded to fp32 (embedding.py:57-58)
+__device__ __forceinline__ float phase_div(float gamma, int D) {
+  return (float)(((double)gamma + 2.0) / (double)D / 3.141592653589793238462643383279);
+}
+
+// (h o r)_d for one query row, rounded as torch evaluates it: two products
+// then one difference/sum, no contraction (embedding.py:60-61)
+__device__ __forceinline__ void rotate_head(const float *hrow, const float2 *rrow, int D, int d, float &re,
+                                            float &im) {
+  const float rh = hrow[d], ih = hrow[D + d];
+  const float2 cs = rrow[d];
+  re = __fsub_rn(__fmul_rn(rh, cs.x), __fmul_rn(ih, cs.y));
+  im = __fadd_rn(__fmul_rn(rh, cs.y), __fmul_rn(ih, cs.x));
+}
+
+// XCD-aware tile order.  Blocks are dealt to the 8 XCDs round-robin by
+// linear id; remap so each XCD walks its own contiguous slab of tiles, swept
+// in super-rows of G query tiles x all entity tiles: the blocks resident on
+// one XCD at a time then cover ~G query tiles x (resident / G) entity tiles,
+// and both the entity table slices and the query rows are re-read from that
+// XCD's L2 instead of MALL/HBM.  Only the speed depends on the placement.
+constexpr int XCDS = 8;
+#ifndef RNNL_TILE_G
+#define RNNL_TILE_G 16
+#endif
+constexpr int TILE_G = RNNL_TILE_G;
+__device__ __forceinline__ bool xcd_tile(int nE, int nQ, int &et, int &qt) {
+  const int64_t n = (int64_t)nE * nQ;
+  const int64_t per = (n + XCDS - 1) / XCDS;
+  const int64_t v = (int64_t)(blockIdx.x % XCDS) * per + blockIdx.x / XCDS;
+  if (v >= n) return false;
+  const int64_t super = v / ((int64_t)TILE_G * nE);
+  const int64_t w = v % ((int64_t)TILE_G * nE);
+  const int g = (int)min<int64_t>(TILE_G, nQ - super * TILE_G);
+  et = (int)(w / g);
+  qt = (int)(super * TILE_G + w % g);
+  return true;
+}
+static unsigned xcd_grid(int64_t nE, int64_t nQ) { return (unsigned)((nE * nQ + XCDS - 1) / XCDS * XCDS); }
+
+// ---------------------------------------------------------------------------
+// MFMA formulation (default).  For one dimension d the squared distance of
+// every (query q, entity e) pair is a short contraction:
+//   s = (hr_re - a)^2 + (hr_im - b)^2 = |hr|^2 + x a + y b + |t|^2,
+//   x = -2 hr_re, y = -2 hr_im, |t|^2 = a^2 + b^2,
+// evaluated by one v_mfma_f32_16x16x16_bf16 per 16 x 16 tile: every fp32
+// operand is split exactly into three bf16 parts (v = v0 + v1 + v2, 8 + 8 + 8
+// mantissa bits), the cross products keep the six part pairs i + j <= 2 (the
+// dropped ones are below 2^-23 |x a|), |t|^2 rides on constant-1 slots and
+// |hr|^2 is the fp32 accumulator input C.  16 K slots:
+//   k  0..3   x0 a0 | x0 a1 | x0 a2 | x1 a0
+//   k  4..7   x1 a1 | x2 a0 | y0 b0 | y0 b1
+//   k  8..11  y0 b2 | y1 b0 | y1 b1 | y2 b0
+//   k 12..15  1 m0  | 1 m1  | 1 m2  | 0
+// The bf16 matrix pipe runs beside the VALU (the f32 MFMA shares the VALU's
+// issue; tools/micro/valu_rates.hip: 13.1 vs 21.3 cycles per 64 terms), so
+// the VALU keeps only sqrt(|s|) + accumulate per term (|s| absorbs a
+// rounding-negative s at a near-zero distance; abs is a free modifier).
+// Rounding: s carries the fp32 cancellation of the expanded form,
+// ~2^-24 (|hr|^2 + |t|^2); DESIGN.md "RotatE numerics".
+//
+// Block = 64 queries x 256 entities (4 waves of 64 x 64: 16 tiles, 64
+// accumulator VGPRs).  A fragments (8 B per lane) and C = |hr|^2 (4 rows per
+// lane) are built per MDC-dim chunk in a double-buffered LDS image; B
+// fragments (8 B per lane) come straight from the entity table, two dims
+// ahead.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#ifndef RNNL_WQ
+#define RNNL_WQ 4
+#endif
+#ifndef RNNL_WE
+#define RNNL_WE 4
+#endif
+#ifndef RNNL_MDC
+#define RNNL_MDC 8
+#endif
+constexpr int WQ = RNNL_WQ;    // 16-query tile rows per wave
+constexpr int WE = RNNL_WE;    // 16-entity tile columns per wave
+constexpr int MQ = 16 * WQ;    // queries per block
+constexpr int ME = 64 * WE;    // entities per block (4 waves side by side; divides 256)
+constexpr int MDC = RNNL_MDC;  // dims per LDS chunk (unrolled; even)
+constexpr int AST = 256 / MQ;  // A side: dims built per pass of the block
+static_assert(MDC % 2 == 0 && MDC % AST == 0, "chunk shape");
+
+__device__ __forceinline__ unsigned short bf16_bits(float v) {
+  return __builtin_bit_cast(unsigned short, (__bf16)v);  // v_cvt_pk_bf16_f32 (RNE)
+}
+__device__ __forceinline__ float bf16_val(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+// v = p0 + p1 + p2 exactly (each residual is exact by Sterbenz)
+__device__ __forceinline__ void split3(float v, unsigned short p[3]) {
+  p[0] = bf16_bits(v);
+  const float r1 = v - bf16_val(p[0]);
+  p[1] = bf16_bits(r1);
+  p[2] = bf16_bits(r1 - bf16_val(p[1]));
+}
+__device__ __forceinline__ uint2 pack4(unsigned short a, unsigned short b, unsigned short c, unsigned short d) {
+  return make_uint2(a | ((unsigned)b << 16), c | ((unsigned)d << 16));
+}
+
+#ifndef RNNL_ROT_MINB
+#define RNNL_ROT_MINB 1
+#endif
+__global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const float *__restrict__ eemb,
+                                                          const uint2 *__restrict__ etab,
+                                                          const float2 *__restrict__ rtab, int D, float gamma,
                                                           const int64_t *__restrict__ all_h,
                                                           const int64_t *__restrict__ all_r, int nq, int E,
                                                           float *__restrict__ score, int accumulate) {
-  __shared__ __attribute__((aligned(16))) float sA[MDC][4][MQP];
+  __shared__ __attribute__((aligned(16))) uint2 sA[2][MDC][4][MQ];
+  __shared__ __attribute__((aligned(16))) float sN[2][MDC][MQ];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int k = lane >> 4, i16 = lane & 15;
-  const int q0 = blockIdx.y * MQ;
-  const int e_base = blockIdx.x * ME + wave * 64;
-  const float div = (float)(((double)gamma + 2.0) / (double)D / 3.141592653589793238462643383279);
-  // entity of this lane in each of the 4 entity groups; loads are clamped in-range
-  int ecol[4];
+  const int64_t Ep = ent_pad(E);
+  int et, qt;
+  if (!xcd_tile((int)(Ep / ME), (nq + MQ - 1) / MQ, et, qt)) return;
+  const int q0 = qt * MQ;
+  const int e_base = et * ME + wave * 16 * WE;
+  const int nchunk = (D + MDC - 1) / MDC;
+
+  // ---- A side: this thread builds query row q0 + tid % MQ, dims tid / MQ + AST i of each chunk
+  const int aq = tid % MQ, adw = tid / MQ;
+  const bool avalid = q0 + aq < nq;
+  const float *hrow = eemb;
+  const float2 *rrow = rtab;
+  if (avalid) {
+    hrow = eemb + all_h[q0 + aq] * 2 * (int64_t)D;
+    rrow = rtab + all_r[q0 + aq] * (int64_t)D;
+  }
+  float pre[MDC / AST], pim[MDC / AST];
+  auto load_chunk = [&](int c) {
 #pragma unroll
-  for (int g = 0; g < 4; ++g) ecol[g] = min(e_base + g * 16 + i16, E - 1);
-  const int plane = (k & 1) ? D : 0;  // k = 0, 2: real plane; k = 1, 3: imaginary plane
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int qg = 0; qg < 4; ++qg)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) acc[qg][g] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int d0 = 0; d0 < D; d0 += MDC) {
-    const int nd = min(MDC, D - d0);
-    __syncthreads();
-    // A fragments for MQ queries x nd dims: [-2 re, -2 im, |hr|^2, 1] of h o r
-    for (int idx = tid; idx < MQ * MDC; idx += 256) {
-      const int qq = idx / MDC, dd = idx % MDC;
-      float re = 0.f, im = 0.f;
-      if (q0 + qq < nq && dd < nd) {
-        const int64_t h = all_h[q0 + qq], r = all_r[q0 + qq];
-        const int d = d0 + dd;
-        const float ph = remb[r * D + d] / div;
-        const float cr = cosf(ph), sr = sinf(ph);
-        const float rh = eemb[h * 2 * D + d], ih = eemb[h * 2 * D + D + d];
-        re = rh * cr - ih * sr;
-        im = rh * sr + ih * cr;
-      }
-      sA[dd][0][qq] = -2.f * re;
-      sA[dd][1][qq] = -2.f * im;
-      sA[dd][2][qq] = fmaf(re, re, im * im);
-      sA[dd][3][qq] = (dd < nd) ? 1.f : 0.f;
+    for (int i = 0; i < MDC / AST; ++i) {
+      const int d = c * MDC + adw + AST * i;
+      pre[i] = pim[i] = 0.f;
+      if (avalid && d < D) rotate_head(hrow, rrow, D, d, pre[i], pim[i]);
     }
-    __syncthreads();
-    float v[4];
+  };
+  auto store_chunk = [&](int c, int buf) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) v[g] = eemb_t[(int64_t)(plane + d0) * E + ecol[g]];
-    for (int dd = 0; dd < nd; ++dd) {
-      // prefetch the next dimension's table values
-      float vn[4];
-      const int dn = min(dd + 1, nd - 1);
+    for (int i = 0; i < MDC / AST; ++i) {
+      const int dd = adw + AST * i;
+      const bool live = avalid && c * MDC + dd < D;
+      unsigned short x[3], y[3];
+      split3(-2.f * pre[i], x);
+      split3(-2.f * pim[i], y);
+      const unsigned short one = live ? 0x3f80 : 0;  // dead rows / dims: A = 0, C = 0, s = 0
+      sA[buf][dd][0][aq] = pack4(x[0], x[0], x[0], x[1]);
+      sA[buf][dd][1][aq] = pack4(x[1], x[2], y[0], y[0]);
+      sA[buf][dd][2][aq] = pack4(y[0], y[1], y[1], y[2]);
+      sA[buf][dd][3][aq] = pack4(one, one, one, 0);
+      sN[buf][dd][aq] = fmaf(pre[i], pre[i], pim[i] * pim[i]);
+    }
+  };
+
+  // ---- B side: lane (k, i16) loads k-group k of entity e_base + 16 g + i16, dim d
+  const uint2 *bp = etab + k * Ep + e_base + i16;
+  const int64_t dstride = 4 * Ep;
+  uint2 vb[2][WE];  // ring: dim d lives in slot d & 1, reloaded with d + 2 once consumed
 #pragma unroll
-      for (int g = 0; g < 4; ++g) vn[g] = eemb_t[(int64_t)(plane + d0 + dn) * E + ecol[g]];
-      float b[4];
+  for (int p = 0; p < 2; ++p)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float o = __shfl_xor(v[g], 16, 64);  // k = 3 lanes: real part from their k = 2 partner
-        b[g] = k == 0 || k == 1 ? v[g] : (k == 2 ? 1.f : fmaf(o, o, v[g] * v[g]));
-      }
-      float a[4];
+    for (int g = 0; g < WE; ++g) vb[p][g] = bp[min(p, D - 1) * dstride + g * 16];
+
+  f32x4 acc[WQ][WE];
 #pragma unroll
-      for (int qg = 0; qg < 4; ++qg) a[qg] = sA[dd][k][qg * 16 + i16];
+  for (int qg = 0; qg < WQ; ++qg)
 #pragma unroll
-      for (int qg = 0; qg < 4; ++qg) {
+    for (int g = 0; g < WE; ++g) acc[qg][g] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load_chunk(0);
+  store_chunk(0, 0);
+  for (int c = 0; c < nchunk; ++c) {
+    __syncthreads();  // chunk c's image is complete; chunk c-1's buffer is free
+    const int buf = c & 1;
+    if (c + 1 < nchunk) load_chunk(c + 1);  // global loads in flight under the compute
+    // dims past D in the last chunk: A and C are zero there, so s = 0 adds sqrt(0)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 s = __builtin_amdgcn_mfma_f32_16x16x4f32(a[qg], b[g], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    for (int dd = 0; dd < MDC; ++dd) {
+      const int slot = dd & 1;  // MDC is even: slot of dim c*MDC + dd
+      s16x4 b[WE];
+#pragma unroll
+      for (int g = 0; g < WE; ++g) b[g] = __builtin_bit_cast(s16x4, vb[slot][g]);
+      const int dn = min(c * MDC + dd + 2, D - 1);
+#pragma unroll
+      for (int g = 0; g < WE; ++g) vb[slot][g] = bp[dn * dstride + g * 16];
+#pragma unroll
+      for (int qg = 0; qg < WQ; ++qg) {
+        const s16x4 a = __builtin_bit_cast(s16x4, sA[buf][dd][k][qg * 16 + i16]);
+        const f32x4 cn = *reinterpret_cast<const f32x4 *>(&sN[buf][dd][qg * 16 + k * 4]);
+#pragma unroll
+        for (int g = 0; g < WE; ++g) {
+          const f32x4 s = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b[g], cn, 0, 0, 0);
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[qg][g][j] += __builtin_amdgcn_sqrtf(__builtin_fabsf(s[j]));
         }
       }
+      // keep the unrolled dims apart: the accumulators are complete here and
+      // the next dim's LDS/global reads stay below (memory clobber), so its
+      // MFMAs cannot be hoisted — hoisting every MFMA of the chunk first
+      // needs MDC x the result registers and spills
 #pragma unroll
-      for (int g = 0; g < 4; ++g) v[g] = vn[g];
+      for (int qg = 0; qg < WQ; ++qg)
+#pragma unroll
+        for (int g = 0; g < WE; ++g) asm volatile("" ::"v"(acc[qg][g]) : "memory");
     }
+    if (c + 1 < nchunk) store_chunk(c + 1, buf ^ 1);
   }
   // D layout: lane holds entity column i16 of group g, query rows 4k + j of group qg
 #pragma unroll
-  for (int qg = 0; qg < 4; ++qg)
+  for (int qg = 0; qg < WQ; ++qg)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < WE; ++g)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = q0 + qg * 16 + k * 4 + j;
@@ -199,18 +258,157 @@ __global__ __launch_bounds__(256) void rotate_mfma_kernel(const float *__restric
       }
 }
 
-__global__ void transpose_kernel(const float *__restrict__ in, int rows, int cols, float *__restrict__ out) {
-  __shared__ float tile[32][33];
-  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+// ---------------------------------------------------------------------------
+// Direct formulation (mode RNNL_ROTATE_DIRECT, the default): the reference's
+// arithmetic term by term — (hr_re - a), (hr_im - b), sqrt of the sum of
+// squares — on the VALU, so no cancellation beyond the reference's own
+// rounding.  Each lane owns one entity; a wave owns DQ = 16 queries whose
+// h o r values for the current dim are wave-uniform and come in as SGPR
+// operands (s_load from the per-call hr workspace, built by rotate_hr_kernel)
+// — per term the VALU issues exactly sub, sub, mul, fma, sqrt, add.
+// Sums are kept per DCH-dim chunk and folded into the row total, which keeps
+// the fp32 summation error of a 1000-term row near the reference's.
+constexpr int RB = 256;   // entities per block (one per lane)
+#ifndef RNNL_DQ
+#define RNNL_DQ 16
+#endif
+constexpr int DQ = RNNL_DQ;  // queries per block (SGPR-resident)
+constexpr int DCH = 32;   // dims per partial sum
+
+// hr[g][d][0..15 | 16..31] = (re | im) of (h o r)_d for queries 16 g + k
+__global__ void rotate_hr_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D,
+                                 const int64_t *__restrict__ all_h, const int64_t *__restrict__ all_r, int nq,
+                                 float *__restrict__ hr) {
+  const int64_t n = (int64_t)((nq + DQ - 1) / DQ) * D * DQ;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % DQ);
+    const int64_t gd = i / DQ;
+    const int d = (int)(gd % D);
+    const int q = (int)(gd / D) * DQ + k;
+    float re = 0.f, im = 0.f;
+    if (q < nq) rotate_head(eemb + all_h[q] * 2 * (int64_t)D, rtab + all_r[q] * (int64_t)D, D, d, re, im);
+    hr[gd * 2 * DQ + k] = re;
+    hr[gd * 2 * DQ + DQ + k] = im;
+  }
+}
+
+__global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restrict__ ptab,
+                                                           const float *__restrict__ hr, int D, float gamma,
+                                                           int nq, int E, float *__restrict__ score,
+                                                           int accumulate) {
+  const int64_t Ep = ent_pad(E);
+  int et, qt;
+  if (!xcd_tile((int)(Ep / RB), (nq + DQ - 1) / DQ, et, qt)) return;
+  const int e = et * RB + threadIdx.x;  // < Ep: the table is padded
+  const int q0 = qt * DQ;
+  const float *hp = hr + (int64_t)qt * D * 2 * DQ;
+  const float *ap = ptab + e;
+  // software pipeline: the sqrt of dim d runs one dim later than its
+  // squared distance (a VALU result feeding v_sqrt directly costs ~6 more
+  // cycles per term; tools/micro/valu_rates.hip "direct pipelined")
+  float acc[DQ], sq[DQ];
+#pragma unroll
+  for (int k = 0; k < DQ; ++k) acc[k] = sq[k] = 0.f;
+  float va = ap[0], vb = ap[Ep];
+  for (int d0 = 0; d0 < D; d0 += DCH) {
+    const int nd = min(DCH, D - d0);
+    float part[DQ];
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) part[k] = 0.f;
+    for (int dd = 0; dd < nd; ++dd) {
+      const int d = d0 + dd;
+      const float a = va, b = vb;
+      const int64_t dn = min(d + 1, D - 1);  // prefetch the next dim's entity values
+      va = ap[dn * 2 * Ep];
+      vb = ap[dn * 2 * Ep + Ep];
+      const float *h = hp + (int64_t)d * 2 * DQ;  // wave-uniform: s_load
+#pragma unroll
+      for (int k = 0; k < DQ; ++k) {
+        part[k] += __builtin_amdgcn_sqrtf(sq[k]);  // dim d - 1 (sqrt(0) = 0 before the first)
+        const float x = h[k] - a;
+        const float y = h[DQ + k] - b;
+        sq[k] = fmaf(x, x, y * y);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) acc[k] += part[k];
+  }
+#pragma unroll
+  for (int k = 0; k < DQ; ++k) acc[k] += __builtin_amdgcn_sqrtf(sq[k]);  // v_sqrt_f32 (1 ulp)
+  if (e < E) {
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) {
+      if (q0 + k < nq) {
+        const int64_t idx = (int64_t)(q0 + k) * E + e;
+        const float v = gamma - acc[k];
+        score[idx] = accumulate ? score[idx] + v : v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Table builders (once per weight version)
+
+// etab[d][kg][e] from eemb[e][2D]: 32 entities x 32 dims per tile through
+// LDS, so both the row reads and the table writes are coalesced.
+__global__ void entity_table_kernel(const float *__restrict__ eemb, int E, int D, uint2 *__restrict__ etab) {
+  __shared__ float ta[32][33], tb[32][33];
+  const int d0 = blockIdx.x * 32, e0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  const int64_t Ep = ent_pad(E);
   for (int j = ty; j < 32; j += 8) {
-    const int r = r0 + j, c = c0 + tx;
-    tile[j][tx] = (r < rows && c < cols) ? in[(int64_t)r * cols + c] : 0.f;
+    const int e = e0 + j, d = d0 + tx;
+    const bool in = e < E && d < D;
+    ta[j][tx] = in ? eemb[(int64_t)e * 2 * D + d] : 0.f;
+    tb[j][tx] = in ? eemb[(int64_t)e * 2 * D + D + d] : 0.f;
   }
   __syncthreads();
   for (int j = ty; j < 32; j += 8) {
-    const int c = c0 + j, r = r0 + tx;
-    if (c < cols && r < rows) out[(int64_t)c * rows + r] = tile[tx][j];
+    const int d = d0 + j, e = e0 + tx;
+    if (d < D && e < Ep) {
+      const float a = ta[tx][j], b = tb[tx][j];
+      unsigned short pa[3], pb[3], pm[3];
+      split3(a, pa);
+      split3(b, pb);
+      split3(fmaf(a, a, b * b), pm);
+      uint2 *col = etab + (int64_t)d * 4 * Ep + e;
+      col[0] = pack4(pa[0], pa[1], pa[2], pa[0]);
+      col[Ep] = pack4(pa[1], pa[0], pb[0], pb[1]);
+      col[2 * Ep] = pack4(pb[2], pb[0], pb[1], pb[0]);
+      col[3 * Ep] = pack4(pm[0], pm[1], pm[2], 0);
+    }
+  }
+}
+
+// ptab[d][0 | 1][e] = re | im of every entity (direct mode), same tiling
+__global__ void plane_table_kernel(const float *__restrict__ eemb, int E, int D, float *__restrict__ ptab) {
+  __shared__ float ta[32][33], tb[32][33];
+  const int d0 = blockIdx.x * 32, e0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t Ep = ent_pad(E);
+  for (int j = ty; j < 32; j += 8) {
+    const int e = e0 + j, d = d0 + tx;
+    const bool in = e < E && d < D;
+    ta[j][tx] = in ? eemb[(int64_t)e * 2 * D + d] : 0.f;
+    tb[j][tx] = in ? eemb[(int64_t)e * 2 * D + D + d] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int d = d0 + j, e = e0 + tx;
+    if (d < D && e < Ep) {
+      ptab[(int64_t)d * 2 * Ep + e] = ta[tx][j];
+      ptab[(int64_t)d * 2 * Ep + Ep + e] = tb[tx][j];
+    }
+  }
+}
+
+__global__ void relation_table_kernel(const float *__restrict__ remb, int64_t n, int D, float gamma,
+                                      float2 *__restrict__ rtab) {
+  const float div = phase_div(gamma, D);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float ph = remb[i] / div;
+    rtab[i] = make_float2(cosf(ph), sinf(ph));
   }
 }
 
@@ -256,32 +454,83 @@ int rnnl_fill_value(float v, int64_t n, float *score, void *stream) {
   return RNNL_OK;
 }
 
-int rnnl_rotate_transpose(const float *eemb, int32_t E, int32_t dim2, float *eemb_t, void *stream) {
-  if (!eemb || !eemb_t || E <= 0 || dim2 <= 0) {
-    set_error("rnnl_rotate_transpose: bad arguments");
+static bool valid_mode(int32_t mode) { return mode == RNNL_ROTATE_DIRECT || mode == RNNL_ROTATE_MFMA; }
+
+int rnnl_rotate_table_sizes(int32_t E, int32_t D, int32_t n_rel_total, int32_t mode, size_t *entity_bytes,
+                            size_t *relation_bytes) {
+  if (E <= 0 || D <= 0 || n_rel_total <= 0 || !valid_mode(mode) || !entity_bytes || !relation_bytes) {
+    set_error("rnnl_rotate_table_sizes: bad arguments");
     return RNNL_ERR_INVALID;
   }
-  hipLaunchKernelGGL(transpose_kernel, dim3((dim2 + 31) / 32, (E + 31) / 32), dim3(256), 0, (hipStream_t)stream,
-                     eemb, E, dim2, eemb_t);
+  *entity_bytes = mode == RNNL_ROTATE_MFMA ? (size_t)4 * D * ent_pad(E) * sizeof(uint2)
+                                           : (size_t)2 * D * ent_pad(E) * sizeof(float);
+  *relation_bytes = (size_t)n_rel_total * D * 2 * sizeof(float);
+  return RNNL_OK;
+}
+
+int rnnl_rotate_entity_table(const float *eemb, int32_t E, int32_t D, int32_t mode, void *etab, void *stream) {
+  if (!eemb || !etab || E <= 0 || D <= 0 || !valid_mode(mode)) {
+    set_error("rnnl_rotate_entity_table: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const dim3 grid((D + 31) / 32, (unsigned)(ent_pad(E) / 32));
+  if (mode == RNNL_ROTATE_MFMA)
+    hipLaunchKernelGGL(entity_table_kernel, grid, dim3(256), 0, (hipStream_t)stream, eemb, E, D, (uint2 *)etab);
+  else
+    hipLaunchKernelGGL(plane_table_kernel, grid, dim3(256), 0, (hipStream_t)stream, eemb, E, D, (float *)etab);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
 
-int rnnl_rotate_score(const float *eemb, const float *eemb_t, const float *remb, int32_t D, float gamma,
+int rnnl_rotate_relation_table(const float *remb, int32_t n_rel_total, int32_t D, float gamma, float *rtab,
+                               void *stream) {
+  if (!remb || !rtab || n_rel_total <= 0 || D <= 0) {
+    set_error("rnnl_rotate_relation_table: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const int64_t n = (int64_t)n_rel_total * D;
+  hipLaunchKernelGGL(relation_table_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, remb, n, D,
+                     gamma, (float2 *)rtab);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_rotate_workspace_size(int32_t nq, int32_t D, int32_t mode, size_t *bytes) {
+  if (nq < 0 || D <= 0 || !valid_mode(mode) || !bytes) {
+    set_error("rnnl_rotate_workspace_size: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = mode == RNNL_ROTATE_DIRECT ? (size_t)((nq + DQ - 1) / DQ) * D * 2 * DQ * sizeof(float) : 0;
+  return RNNL_OK;
+}
+
+int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, int32_t D, float gamma,
                       const int64_t *all_h, const int64_t *all_r, int32_t nq, int32_t E, float *score,
-                      int32_t accumulate, void *stream) {
-  if (!eemb || !eemb_t || !remb || !all_h || !all_r || !score || D <= 0 || E <= 0 || nq < 0) {
+                      int32_t accumulate, int32_t mode, void *workspace, size_t ws_bytes, void *stream) {
+  if (!eemb || !etab || !rtab || !all_h || !all_r || !score || D <= 0 || E <= 0 || nq < 0 || !valid_mode(mode)) {
     set_error("rnnl_rotate_score: bad arguments");
     return RNNL_ERR_INVALID;
   }
   if (nq == 0) return RNNL_OK;
-  static const bool valu = getenv("RNNL_ROTATE_VALU") != nullptr;  // diagnostic: VALU-only variant
-  if (valu)
-    hipLaunchKernelGGL(rotate_kernel, dim3((E + RB - 1) / RB, (nq + QB - 1) / QB), dim3(RB), 0,
-                       (hipStream_t)stream, eemb, eemb_t, remb, D, gamma, all_h, all_r, nq, E, score, accumulate);
-  else
-    hipLaunchKernelGGL(rotate_mfma_kernel, dim3((E + ME - 1) / ME, (nq + MQ - 1) / MQ), dim3(256), 0,
-                       (hipStream_t)stream, eemb, eemb_t, remb, D, gamma, all_h, all_r, nq, E, score, accumulate);
+  if (mode == RNNL_ROTATE_DIRECT) {
+    size_t need = 0;
+    rnnl_rotate_workspace_size(nq, D, mode, &need);
+    if (!workspace || ws_bytes < need) {
+      set_error("rnnl_rotate_score: workspace too small (see rnnl_rotate_workspace_size)");
+      return RNNL_ERR_INVALID;
+    }
+    const int64_t nhr = (int64_t)((nq + DQ - 1) / DQ) * D * DQ;
+    hipLaunchKernelGGL(rotate_hr_kernel, dim3(grid_for(nhr)), dim3(256), 0, (hipStream_t)stream, eemb,
+                       (const float2 *)rtab, D, all_h, all_r, nq, (float *)workspace);
+    RNNL_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(rotate_direct_kernel, dim3(xcd_grid(ent_pad(E) / RB, (nq + DQ - 1) / DQ)), dim3(RB), 0,
+                       (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E, score,
+                       accumulate);
+  } else {
+    hipLaunchKernelGGL(rotate_mfma_kernel, dim3(xcd_grid(ent_pad(E) / ME, (nq + MQ - 1) / MQ)), dim3(256), 0,
+                       (hipStream_t)stream, eemb, (const uint2 *)etab, (const float2 *)rtab, D, gamma, all_h, all_r,
+                       nq, E, score, accumulate);
+  }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -2,10 +2,11 @@
 src/embedding.py (parameters `eemb` (|E|, 2D) and `remb` (2 nrel, D) with the
 negated inverse half, embedding.py:7-26).
 
-forward() on a GPU runs the HIP kernel rnnl_rotate_score (rotate.hip): every
-(query, entity) distance for a block of 32 query rows is computed from one
-pass over the (transposed) entity table.
+forward() on a GPU runs the HIP kernel rnnl_rotate_score (rotate.hip) over
+two weight-derived device tables (entity planes, relation cos/sin) that are
+built once per weight version.
 """
+import ctypes
 import json
 import os
 
@@ -29,17 +30,42 @@ class RotatE(torch.nn.Module):
         self.eemb = torch.nn.parameter.Parameter(torch.tensor(eemb))
         remb = torch.tensor(np.load(os.path.join(path, "relation_embedding.npy"), allow_pickle=False))
         self.remb = torch.nn.parameter.Parameter(torch.cat([remb, -remb], dim=0))
-        self._t_cache = None
+        self._tables = None
+        self._ws = None
+        # DIRECT (default) evaluates the reference's arithmetic term by term;
+        # RNNL_ROTATE_MFMA=1 selects the faster expanded bf16x3 MFMA kernel
+        # (cancellation-prone when h o r ~= t; include/rnnlogic_hip.h)
+        self.mode = _native.ROTATE_MFMA if os.environ.get("RNNL_ROTATE_MFMA") else _native.ROTATE_DIRECT
 
-    def _transposed(self):
-        """(2D, |E|) copy of eemb for coalesced loads, rebuilt when eemb changes."""
-        key = (self.eemb.data_ptr(), self.eemb._version, self.eemb.device)
-        if self._t_cache is None or self._t_cache[0] != key:
-            t = torch.empty((self.eemb.size(1), self.eemb.size(0)), dtype=torch.float32, device=self.eemb.device)
-            _native.call("rnnl_rotate_transpose", self.eemb.data_ptr(), self.eemb.size(0), self.eemb.size(1),
-                         t.data_ptr(), torch.cuda.current_stream(self.eemb.device).cuda_stream)
-            self._t_cache = (key, t)
-        return self._t_cache[1]
+    def _device_tables(self):
+        """Weight-derived tables (rotate.hip header), rebuilt when eemb/remb or
+        the mode change: the mode's entity table and the relation (cos, sin)."""
+        dev = self.eemb.device
+        key = (self.eemb.data_ptr(), self.eemb._version, self.remb.data_ptr(), self.remb._version, dev,
+               int(self.mode))
+        if self._tables is None or self._tables[0] != key:
+            E, D, R2 = self.num_entities, self.emb_dim, self.remb.size(0)
+            eb, rb = ctypes.c_size_t(), ctypes.c_size_t()
+            _native.call("rnnl_rotate_table_sizes", E, D, R2, int(self.mode), ctypes.byref(eb), ctypes.byref(rb))
+            etab = torch.empty(eb.value // 4, dtype=torch.float32, device=dev)
+            rtab = torch.empty(rb.value // 4, dtype=torch.float32, device=dev)
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            eemb = self.eemb.detach().contiguous()
+            remb = self.remb.detach().contiguous()
+            _native.call("rnnl_rotate_entity_table", eemb.data_ptr(), E, D, int(self.mode), etab.data_ptr(), stream)
+            _native.call("rnnl_rotate_relation_table", remb.data_ptr(), R2, D, float(self.gamma), rtab.data_ptr(),
+                         stream)
+            self._tables = (key, etab, rtab)
+        return self._tables[1], self._tables[2]
+
+    def _workspace(self, nq):
+        need = ctypes.c_size_t()
+        _native.call("rnnl_rotate_workspace_size", nq, self.emb_dim, int(self.mode), ctypes.byref(need))
+        if need.value == 0:
+            return None, 0
+        if self._ws is None or self._ws.numel() * 4 < need.value or self._ws.device != self.eemb.device:
+            self._ws = torch.empty((need.value + 3) // 4, dtype=torch.float32, device=self.eemb.device)
+        return self._ws.data_ptr(), need.value
 
     def score_into(self, all_h, all_r, out, accumulate=False):
         """out (B, |E|) (+)= gamma - dist(h o r, e) for every entity (HIP)."""
@@ -48,10 +74,11 @@ class RotatE(torch.nn.Module):
         all_h = all_h.to(self.eemb.device, torch.int64).contiguous()
         all_r = all_r.to(self.eemb.device, torch.int64).contiguous()
         eemb = self.eemb.detach().contiguous()
-        remb = self.remb.detach().contiguous()
-        _native.call("rnnl_rotate_score", eemb.data_ptr(), self._transposed().data_ptr(), remb.data_ptr(),
+        etab, rtab = self._device_tables()
+        ws, ws_bytes = self._workspace(all_h.numel())
+        _native.call("rnnl_rotate_score", eemb.data_ptr(), etab.data_ptr(), rtab.data_ptr(),
                      self.emb_dim, float(self.gamma), all_h.data_ptr(), all_r.data_ptr(), all_h.numel(),
-                     self.num_entities, out.data_ptr(), 1 if accumulate else 0,
+                     self.num_entities, out.data_ptr(), 1 if accumulate else 0, int(self.mode), ws, ws_bytes,
                      torch.cuda.current_stream(self.eemb.device).cuda_stream)
         return out
 

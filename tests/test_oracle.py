@@ -26,7 +26,9 @@ def test_oracle_grounding_counts(case, fixtures):
     fx = fixtures(case)
     g = graph_for(fx)
     rules = ref.Rules(fx.rule_path(), g.relation_size)
-    for k in range(min(fx.ncalls, 6)):
+    # the dense pure-numpy restatement is slow on WN18RR's 40,943 entities:
+    # one batch there (the C oracle covers every batch, test_oracle_c.py)
+    for k in range(min(fx.ncalls, 1 if case.startswith("wn") else 6)):
         c = fx.call(k)
         q = int(c["r"][0])
         got = []
@@ -44,7 +46,7 @@ def test_oracle_forward(case, fixtures):
     g = graph_for(fx)
     rules = ref.Rules(fx.rule_path(), g.relation_size)
     rot = ref.load_rotate(fx.rotate_path()) if fx.rotate_path() else None
-    n = fx.ncalls if case.startswith(("umls", "kinship")) else min(fx.ncalls, 3)
+    n = fx.ncalls if case.startswith(("umls", "kinship")) else min(fx.ncalls, 1 if case.startswith("wn") else 3)
     for k in range(0, n, max(1, n // 12)):
         c = fx.call(k)
         score, mask = ref.predictorplus_forward(fx.sd, fx.cfg["model"], g, rules, c["h"], c["r"], c["etr"], rot)
