@@ -71,6 +71,10 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *rule_tokens, const int64_t *r
 int rnnl_rules_destroy(rnnl_rules r);
 /* host out: {n_rules, n_nodes, max_depth, node record bytes (sum), node record bytes (pna)} */
 int rnnl_rules_info(rnnl_rules r, int32_t *info5);
+/* host out (n_rules): the trie node where each rule's body ends — several
+ * rules share a node when one body is a prefix-equal duplicate; node ids are
+ * those of the grounding COO (rnnl_ground_export_entries). */
+int rnnl_rules_node_of_rule(rnnl_rules r, int32_t *node_of_rule);
 
 /* Per-node aggregate of rule embeddings (device): rule_emb is n_rules x H
  * (row stride `ld` floats), H == 16.  Writes node_w: n_nodes records of
@@ -124,6 +128,25 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */
 int rnnl_forward_status(void *workspace, void *stream);
+/* Grounding only (reference data.py:136-173 for every rule of every row,
+ * predictors.py:221-244): fills the workspace's COO of the stacked rule_count
+ * matrix and n_cand (per row candidate count, -1/-2 on overflow/error; check
+ * rnnl_forward_status).  Used by the differentiable training path, which
+ * exports the COO and evaluates the aggregator/MLP with autograd. */
+int rnnl_ground(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t *all_r,
+                const int64_t *edges_to_remove, int32_t n_queries, int32_t *n_cand, void *workspace,
+                size_t workspace_bytes, int32_t capacity_scale, void *stream);
+/* COO export after rnnl_ground or rnnl_predictorplus_forward (same n_queries /
+ * capacity_scale).  cand_off (n_queries + 1, exclusive prefix of n_cand):
+ * out_t[cand_off[q] + s] = entity of row q's s-th candidate (ascending entity
+ * order = the reference's row-major nonzero), out_nent = its bucket size.
+ * ent_off (n_queries + 1): prefix of the per-row sums of out_nent; the
+ * entries (trie node, path count) of row q's candidates, candidate-major, land
+ * at out_node/out_count[ent_off[q] ..]. */
+int rnnl_ground_export_candidates(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
+                                  const int64_t *cand_off, int32_t *out_t, int32_t *out_nent, void *stream);
+int rnnl_ground_export_entries(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
+                               const int64_t *ent_off, int32_t *out_node, int32_t *out_count, void *stream);
 /* Diagnostic: when non-NULL, later forward launches add per-phase cycle
  * counters into dev_counters (12 x uint64: prologue, grounding, candidates,
  * queries, contributions, candidates, then candidate sub-phases). */

@@ -31,11 +31,15 @@ SIGNATURES = [
     ("rnnl_rules_create", ctypes.c_int, [_P, _P, _P, _I32, _P]),
     ("rnnl_rules_destroy", ctypes.c_int, [_P]),
     ("rnnl_rules_info", ctypes.c_int, [_P, _P]),
+    ("rnnl_rules_node_of_rule", ctypes.c_int, [_P, _P]),
     ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P]),
     ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     ("rnnl_predictorplus_forward", ctypes.c_int,
      [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
+    ("rnnl_ground", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _P]),
+    ("rnnl_ground_export_candidates", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
+    ("rnnl_ground_export_entries", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),

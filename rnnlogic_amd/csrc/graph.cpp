@@ -154,6 +154,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   std::vector<int32_t> head_root(R, -1), head_depth(R, 0), head_nodes(R, 0);
   std::vector<int32_t> node_rel, node_child, node_nchild, node_nrules, node_rule_ptr(1, 0), node_rules;
   std::vector<uint64_t> node_fp;
+  std::vector<int32_t> node_of_rule(n_rules, -1);
   int max_depth = 0;
   for (int r = 0; r < R; ++r) {
     auto &t = tries[r];
@@ -176,6 +177,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
       uint64_t fp = 0;
       for (int rid : nd.rules) {
         node_rules.push_back(rid);
+        node_of_rule[rid] = newid[loc];
         fp += mix64((uint64_t)rid);
       }
       node_fp.push_back(fp);
@@ -208,6 +210,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   rs->d.n_nodes = (int32_t)node_rel.size();
   rs->d.max_depth = max_depth;
   rs->d.n_heads = R;
+  rs->node_of_rule = std::move(node_of_rule);
   int rc = RNNL_OK;
   if ((rc = upload(head_root, &rs->mem[0], &rs->d.head_root)) ||
       (rc = upload(head_depth, &rs->mem[1], &rs->d.head_depth)) ||
@@ -231,6 +234,15 @@ int rnnl_rules_destroy(rnnl_rules r) {
   for (void *p : r->mem)
     if (p) (void)hipFree(p);
   delete r;
+  return RNNL_OK;
+}
+
+int rnnl_rules_node_of_rule(rnnl_rules r, int32_t *node_of_rule) {
+  if (!r || !node_of_rule) {
+    set_error("rnnl_rules_node_of_rule: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  std::copy(r->node_of_rule.begin(), r->node_of_rule.end(), node_of_rule);
   return RNNL_OK;
 }
 

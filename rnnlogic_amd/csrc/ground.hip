@@ -878,6 +878,37 @@ __global__ void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, 
   }
 }
 
+// ---------------------------------------------------------------- COO export
+// The grounding COO of one launch in reference order: per query its
+// candidates in ascending entity order (= row-major nonzero, predictors.py:239)
+// and, per candidate, its (trie node, path count) bucket entries.  A query's
+// bucket entries are contiguous in the pool in candidate order, so the entry
+// export is one copy per query.
+__global__ void export_candidates_kernel(KParams p, const int64_t *__restrict__ cand_off, int32_t *__restrict__ out_t,
+                                         int32_t *__restrict__ out_nent) {
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    const int nc = p.n_cand[q];
+    if (nc <= 0) continue;
+    const int64_t qb = p.q_base[q], o = cand_off[q];
+    for (int s = threadIdx.x; s < nc; s += blockDim.x) {
+      out_t[o + s] = p.c_t[qb + s];
+      out_nent[o + s] = p.c_cnt[qb + s];
+    }
+  }
+}
+
+__global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent_off, int32_t *__restrict__ out_node,
+                                      int32_t *__restrict__ out_count) {
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    if (p.n_cand[q] <= 0) continue;
+    const int64_t qb = p.q_base[q], o = ent_off[q], n = ent_off[q + 1] - o;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      out_node[o + i] = p.b_node[qb + i];
+      out_count[o + i] = (int32_t)p.b_cnt[qb + i];
+    }
+  }
+}
+
 }  // namespace rnnl
 
 using namespace rnnl;
@@ -907,55 +938,37 @@ int rnnl_forward_workspace_size(rnnl_graph g, rnnl_rules r, int32_t nq, int32_t 
   return RNNL_OK;
 }
 
-int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
-                               const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
-                               int32_t *n_cand, uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale,
-                               void *stream) {
-  if (!g || !r || !pp || !all_h || !all_r || !score || !ws || !n_cand || nq < 0 || scale < 1 || !pp->node_w ||
-      (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA)) {
-    set_error("rnnl_predictorplus_forward: bad arguments");
+// Graph/rules/rows/workspace part of the launch parameters, shared by the
+// forward, the ground-only launch and the COO export.
+static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t *all_r,
+                        const int64_t *etr, int32_t nq, int32_t *n_cand, void *ws, size_t ws_bytes, int32_t scale,
+                        KParams &p) {
+  if (!g || !r || !all_h || !all_r || !ws || !n_cand || nq < 0 || scale < 1) {
+    set_error(std::string(who) + ": bad arguments");
     return RNNL_ERR_INVALID;
   }
   if ((int64_t)g->d.E > (int64_t)MAXWIN * WIN) {
-    set_error("rnnl_predictorplus_forward: more entities than the kernel's window table supports");
+    set_error(std::string(who) + ": more entities than the kernel's window table supports");
     return RNNL_ERR_INVALID;
   }
   const Layout Ly = make_layout(nq, scale);
   if ((int64_t)ws_bytes < Ly.total) {
-    set_error("rnnl_predictorplus_forward: workspace too small");
+    set_error(std::string(who) + ": workspace too small");
     return RNNL_ERR_INVALID;
   }
   if (Ly.pool_cap >= INT32_MAX) {
-    set_error("rnnl_predictorplus_forward: too many rows for one launch (pool index exceeds 31 bits)");
+    set_error(std::string(who) + ": too many rows for one launch (pool index exceeds 31 bits)");
     return RNNL_ERR_INVALID;
   }
-  hipStream_t st = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
-  if (nq == 0) return RNNL_OK;
   unsigned char *base = static_cast<unsigned char *>(ws);
-  KParams p;
+  p = KParams{};
   p.g = g->d;
   p.rl = r->d;
-  p.agg = pp->aggregator;
-  p.feature = pp->feature;
-  p.node_w = static_cast<const unsigned char *>(pp->node_w);
-  p.add_w = pp->add_w;
-  p.add_b = pp->add_b;
-  p.ln_w = pp->ln_w;
-  p.ln_b = pp->ln_b;
-  p.s0_w = pp->s0_w;
-  p.s0_b = pp->s0_b;
-  p.s1_w = pp->s1_w;
-  p.s1_b = pp->s1_b;
-  p.rel_emb = pp->rel_emb;
   p.all_h = all_h;
   p.all_r = all_r;
   p.etr = etr;
   p.nq = nq;
-  p.score = score;
-  p.mask = mask;
   p.n_cand = n_cand;
-  p.digest = digest;
   p.ws = base;
   p.fcap = Ly.fcap;
   p.pcap = Ly.pcap;
@@ -970,7 +983,40 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   p.b_node = reinterpret_cast<int32_t *>(base + Ly.off_bnode);
   p.b_cnt = reinterpret_cast<uint32_t *>(base + Ly.off_bcnt);
   p.prof = g_prof;
-  float *W = reinterpret_cast<float *>(base + HDR_WORDS_BYTES);
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
+                               const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
+                               int32_t *n_cand, uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale,
+                               void *stream) {
+  if (!pp || !score || !pp->node_w || (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA)) {
+    set_error("rnnl_predictorplus_forward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p;
+  if (int rc = setup_params("rnnl_predictorplus_forward", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
+                            p))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  p.agg = pp->aggregator;
+  p.feature = pp->feature;
+  p.node_w = static_cast<const unsigned char *>(pp->node_w);
+  p.add_w = pp->add_w;
+  p.add_b = pp->add_b;
+  p.ln_w = pp->ln_w;
+  p.ln_b = pp->ln_b;
+  p.s0_w = pp->s0_w;
+  p.s0_b = pp->s0_b;
+  p.s1_w = pp->s1_w;
+  p.s1_b = pp->s1_b;
+  p.rel_emb = pp->rel_emb;
+  p.score = score;
+  p.mask = mask;
+  p.digest = digest;
+  float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
   const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
   if (pp->aggregator == RNNL_AGG_SUM) {
@@ -980,6 +1026,62 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
     hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
     hipLaunchKernelGGL(score_kernel<RNNL_AGG_PNA>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
   }
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_ground(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t *all_r, const int64_t *etr,
+                int32_t nq, int32_t *n_cand, void *ws, size_t ws_bytes, int32_t scale, void *stream) {
+  KParams p;
+  if (int rc = setup_params("rnnl_ground", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale, p)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  p.agg = RNNL_AGG_SUM;
+  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+// Only the workspace carve-up is needed to read the pool back.
+static KParams export_params(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand) {
+  const Layout Ly = make_layout(nq, scale);
+  unsigned char *base = static_cast<unsigned char *>(ws);
+  KParams p{};
+  p.nq = nq;
+  p.n_cand = const_cast<int32_t *>(n_cand);
+  p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
+  p.c_t = reinterpret_cast<int32_t *>(base + Ly.off_ct);
+  p.c_cnt = reinterpret_cast<int32_t *>(base + Ly.off_ccnt);
+  p.b_node = reinterpret_cast<int32_t *>(base + Ly.off_bnode);
+  p.b_cnt = reinterpret_cast<uint32_t *>(base + Ly.off_bcnt);
+  return p;
+}
+
+int rnnl_ground_export_candidates(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand,
+                                  const int64_t *cand_off, int32_t *out_t, int32_t *out_nent, void *stream) {
+  if (!ws || nq < 0 || scale < 1 || !n_cand || !cand_off || !out_t || !out_nent) {
+    set_error("rnnl_ground_export_candidates: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  const KParams p = export_params(ws, nq, scale, n_cand);
+  hipLaunchKernelGGL(export_candidates_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, p, cand_off, out_t, out_nent);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_ground_export_entries(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand, const int64_t *ent_off,
+                               int32_t *out_node, int32_t *out_count, void *stream) {
+  if (!ws || nq < 0 || scale < 1 || !n_cand || !ent_off || !out_node || !out_count) {
+    set_error("rnnl_ground_export_entries: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  const KParams p = export_params(ws, nq, scale, n_cand);
+  hipLaunchKernelGGL(export_entries_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, p, ent_off, out_node, out_count);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/rnnlogic_hip.h"
 
@@ -61,6 +62,7 @@ struct rnnl_rules_s {
   int device = 0;
   int32_t R = 0, E = 0;
   void *mem[11] = {};
+  std::vector<int32_t> node_of_rule;  // host: trie node where each rule's body ends
 };
 
 #define RNNL_HIP_CHECK(expr)                                                              \

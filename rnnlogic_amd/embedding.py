@@ -82,7 +82,26 @@ class RotatE(torch.nn.Module):
                      torch.cuda.current_stream(self.eemb.device).cuda_stream)
         return out
 
+    def forward_torch(self, all_h, all_r):
+        """Differentiable (B, |E|) scores as torch ops (training path): the
+        reference's arithmetic (embedding.py:28-70) without expanding h and r
+        to (B * |E|) rows — h o r is formed once per row."""
+        pi = 3.141592653589793238462643383279
+        D = self.emb_dim
+        h = self.eemb.index_select(0, all_h)
+        phase = self.remb.index_select(0, all_r) / (self.range / pi)
+        re_r, im_r = torch.cos(phase), torch.sin(phase)
+        re_h, im_h = h[:, :D], h[:, D:]
+        re_hr = re_h * re_r - im_h * im_r
+        im_hr = re_h * im_r + im_h * re_r
+        re_t, im_t = self.eemb[:, :D], self.eemb[:, D:]
+        diff = torch.stack([re_hr.unsqueeze(1) - re_t.unsqueeze(0), im_hr.unsqueeze(1) - im_t.unsqueeze(0)], dim=0)
+        return self.gamma - diff.norm(dim=0).sum(dim=-1)
+
     def forward(self, all_h, all_r):
-        """(B, |E|) = gamma - sum_d |h o r - e| (embedding.py:64-70)."""
+        """(B, |E|) = gamma - sum_d |h o r - e| (embedding.py:64-70): the HIP
+        kernel, or forward_torch when autograd needs the graph (training)."""
+        if torch.is_grad_enabled() and (self.eemb.requires_grad or self.remb.requires_grad):
+            return self.forward_torch(all_h.to(self.eemb.device), all_r.to(self.eemb.device))
         out = torch.empty((all_h.numel(), self.num_entities), dtype=torch.float32, device=self.eemb.device)
         return self.score_into(all_h, all_r, out)

@@ -54,7 +54,10 @@ class FuncToNodeSum(nn.Module):
 
     def forward(self, A_fn, x_f, b_n):
         # (R_q, C)^T @ (R_q, H) == sum over rules of count * embedding
-        features = A_fn.t().matmul(x_f)
+        return self.finish(A_fn.t().matmul(x_f))
+
+    def finish(self, features):
+        """relu(LN(Linear(features))) on the count-weighted sums (C, H)."""
         return torch.relu(self.layer_norm(self.add_model(features)))
 
 
@@ -71,21 +74,28 @@ class FuncToNode(nn.Module):
         self.eps = 1e-6
 
     def forward(self, A_fn, x_f, b_n):
-        eps = self.eps
-        n_batch = int(b_n.max().item()) + 1
         At = A_fn.t()                                  # (C, R_q)
-        deg = At.sum(1, keepdim=True) + 1              # (C, 1)
-        mean = At.matmul(x_f) / deg.clamp(min=eps)
-        sq_mean = At.matmul(x_f * x_f) / deg.clamp(min=eps)
+        deg = At.sum(1) + 1                            # (C,)
         active = (At != 0).unsqueeze(-1)               # (C, R_q, 1)
         xb = x_f.unsqueeze(0)
         mn = torch.where(active, xb, torch.full_like(xb, float("inf"))).min(1)[0]
         mx = torch.where(active, xb, torch.full_like(xb, float("-inf"))).max(1)[0]
+        return self.finish(At.matmul(x_f), At.matmul(x_f * x_f), mn, mx, deg, b_n, int(b_n.max().item()) + 1)
+
+    def finish(self, wsum, wsq, mn, mx, deg, b_n, n_batch):
+        """The PNA block from its sufficient statistics per candidate:
+        count-weighted sums of x and x^2 (C, H), unweighted min/max over the
+        candidate's rules (C, H), degree = 1 + sum of counts (C,), and the
+        candidate's batch row b_n (C,)."""
+        eps = self.eps
+        deg = deg.unsqueeze(-1)
+        mean = wsum / deg.clamp(min=eps)
+        sq_mean = wsq / deg.clamp(min=eps)
         std = (sq_mean - mean * mean).clamp(min=eps).sqrt()
         feats = torch.cat([mean, mn, mx, std], -1)     # (C, 4H)
         s = deg.log()
-        s_sum = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add_(0, b_n, s.squeeze(-1))
-        s_cnt = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add_(0, b_n, torch.ones_like(s.squeeze(-1)))
+        s_sum = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add(0, b_n, s.squeeze(-1))
+        s_cnt = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add(0, b_n, torch.ones_like(s.squeeze(-1)))
         s = s / (s_sum / s_cnt.clamp(min=eps))[b_n].unsqueeze(-1).clamp(min=eps)
         scales = torch.cat([torch.ones_like(s), s, 1 / s.clamp(min=eps)], -1)  # (C, 3)
         upd = (feats.unsqueeze(-1) * scales.unsqueeze(-2)).flatten(-2)

@@ -16,6 +16,7 @@ import ctypes
 import logging
 import math
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -45,7 +46,6 @@ class _NativeRules(object):
     """Per-device rnnl_rules handle (prefix tries of the rule bodies)."""
 
     def __init__(self, graph, rules, device):
-        import numpy as np
         flat, ptr = [], [0]
         for head, body in rules:
             flat.append(head)
@@ -62,6 +62,9 @@ class _NativeRules(object):
         _native.call("rnnl_rules_info", h, info)
         self.n_rules, self.n_nodes, self.max_depth = info[0], info[1], info[2]
         self.record_bytes = (info[3], info[4])
+        n2r = np.zeros(max(len(rules), 1), dtype=np.int32)
+        _native.call("rnnl_rules_node_of_rule", h, n2r.ctypes.data_as(ctypes.c_void_p))
+        self.node_of_rule = torch.from_numpy(n2r[:len(rules)].astype(np.int64)).to(torch.device("cuda", device))
 
     @property
     def ptr(self):
@@ -342,10 +345,132 @@ class PredictorPlus(torch.nn.Module):
             mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
+    # ------------------------------------------------------------------ autograd (training) path
+    def ground_coo(self, all_h, all_r, edges_to_remove=None):
+        """The grounding of every rule of every row as the COO of the
+        reference's stacked rule_count matrix (HIP: rnnl_ground + export).
+
+        Returns (row (C,), entity (C,), cand_of_entry (P,), node (P,), count (P,))
+        int64 device tensors: candidates in row-major order (= the reference's
+        nonzero order, predictors.py:239) and, per candidate, its (trie node,
+        path count) entries; node ids index `native_rules(device).node_of_rule`."""
+        device = all_h.device
+        if device.type != "cuda":
+            raise RuntimeError("PredictorPlus runs on the HIP path: move inputs and model to a GPU")
+        all_h = all_h.to(torch.int64).contiguous()
+        all_r = all_r.to(torch.int64).contiguous()
+        etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
+        nq = all_h.numel()
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        while True:
+            scale = self.capacity_scale
+            ws = self._workspace(device, nq, scale)
+            _native.call("rnnl_ground", g, nr.ptr, all_h.data_ptr(), all_r.data_ptr(),
+                         etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
+                         ws.numel(), scale, stream)
+            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
+            if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
+                self.capacity_scale *= 2
+                continue
+            _native.check(rc)
+            break
+        nc = n_cand.to(torch.int64)
+        cand_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
+        torch.cumsum(nc, 0, out=cand_off[1:])
+        C = int(cand_off[-1].item())
+        ent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
+        nent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
+        _native.call("rnnl_ground_export_candidates", ws.data_ptr(), nq, scale, n_cand.data_ptr(),
+                     cand_off.data_ptr(), ent.data_ptr(), nent.data_ptr(), stream)
+        ent, nent = ent[:C].to(torch.int64), nent[:C].to(torch.int64)
+        row = torch.repeat_interleave(torch.arange(nq, device=device), nc)
+        per_row = torch.zeros(nq, dtype=torch.int64, device=device).index_add_(0, row, nent)
+        ent_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
+        torch.cumsum(per_row, 0, out=ent_off[1:])
+        P = int(ent_off[-1].item())
+        node = torch.empty(max(P, 1), dtype=torch.int32, device=device)
+        count = torch.empty(max(P, 1), dtype=torch.int32, device=device)
+        _native.call("rnnl_ground_export_entries", ws.data_ptr(), nq, scale, n_cand.data_ptr(), ent_off.data_ptr(),
+                     node.data_ptr(), count.data_ptr(), stream)
+        cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent)
+        return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64)
+
+    def forward_autograd(self, all_h, all_r, edges_to_remove):
+        """Differentiable forward (training): the HIP grounding's COO, then the
+        reference's aggregation / MLP / entity feature as torch ops on it, so
+        autograd yields the reference's gradients (predictors.py:210-271,
+        layers.py:53-126, embedding.py:45-70)."""
+        device = all_h.device
+        all_h = all_h.to(torch.int64)
+        all_r = all_r.to(torch.int64)
+        nq, E = all_h.numel(), self.num_entities
+        row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
+        C = ent.numel()
+        if C == 0:
+            # predictors.py:230-237 early return
+            zero = torch.zeros((nq, E), device=device)
+            if self.entity_feature == "bias":
+                return zero + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
+            if self.entity_feature == "RotatE":
+                return zero + self.RotatE.forward_torch(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
+                                                                                 device=device)
+            return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
+        nr = self.native_rules(device)
+        rels = torch.unique(all_r).tolist()
+        ridx = torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
+        if self.type == "emb":
+            x_f = self.rule_emb[ridx]
+        else:
+            x_f = self.encode_rules(self.rule_features.to(device)[ridx])
+        nodes = nr.node_of_rule[ridx]
+        H = self.hidden_dim
+        cnt = count.to(x_f.dtype).unsqueeze(-1)
+        node_sum = torch.zeros((nr.n_nodes, H), device=device, dtype=x_f.dtype).index_add(0, nodes, x_f)
+        wsum = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sum[node])
+        if self.aggregator == "sum":
+            out = self.rule_to_entity.finish(wsum)
+        else:
+            node_sq = torch.zeros((nr.n_nodes, H), device=device, dtype=x_f.dtype).index_add(0, nodes, x_f * x_f)
+            node_n = torch.zeros(nr.n_nodes, device=device, dtype=x_f.dtype).index_add(
+                0, nodes, torch.ones_like(nodes, dtype=x_f.dtype))
+            idx_n = nodes.unsqueeze(-1).expand(-1, H)
+            node_min = torch.full((nr.n_nodes, H), float("inf"), device=device, dtype=x_f.dtype).scatter_reduce(
+                0, idx_n, x_f, "amin", include_self=True)
+            node_max = torch.full((nr.n_nodes, H), float("-inf"), device=device, dtype=x_f.dtype).scatter_reduce(
+                0, idx_n, x_f, "amax", include_self=True)
+            wsq = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sq[node])
+            deg = torch.zeros(C, device=device, dtype=x_f.dtype).index_add(0, ce, cnt.squeeze(-1) * node_n[node]) + 1
+            idx_c = ce.unsqueeze(-1).expand(-1, H)
+            mn = torch.full((C, H), float("inf"), device=device, dtype=x_f.dtype).scatter_reduce(
+                0, idx_c, node_min[node], "amin", include_self=True)
+            mx = torch.full((C, H), float("-inf"), device=device, dtype=x_f.dtype).scatter_reduce(
+                0, idx_c, node_max[node], "amax", include_self=True)
+            out = self.rule_to_entity.finish(wsum, wsq, mn, mx, deg, row, nq)
+        rel = self.relation_emb(all_r[row])
+        output = self.score_model(torch.cat([out, rel], dim=-1)).squeeze(-1)
+        score = torch.zeros(nq * E, device=device, dtype=output.dtype).scatter(0, row * E + ent, output).view(nq, E)
+        if self.entity_feature == "bias":
+            return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
+        if self.entity_feature == "RotatE":
+            return score + self.RotatE.forward_torch(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
+                                                                                device=device)
+        mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
+        return score.masked_fill(~mask, float("-inf")), mask
+
+    def _needs_grad(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
     def forward(self, all_h, all_r, edges_to_remove):
-        """predictors.py:210-271: one single-relation batch -> (score, mask)."""
+        """predictors.py:210-271: one single-relation batch -> (score, mask).
+
+        With autograd active (training) the differentiable path runs
+        (forward_autograd); otherwise the fused HIP kernels (forward_rows)."""
         query_r = all_r[0].item()
         assert (all_r != query_r).sum() == 0
+        if self._needs_grad():
+            return self.forward_autograd(all_h, all_r, edges_to_remove)
         score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
         if self.entity_feature not in ("bias", "RotatE") and int(n_cand.sum().item()) == 0:
             # reference early return `mask - float('-inf')` (predictors.py:236-237): +inf, mask all False

@@ -52,7 +52,15 @@ class Fixture:
         return datasets.rotate_path(self.cfg["data"], int(emb.split(":")[1]))
 
 
-ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("_"))
+ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("_", "train_")))
+# training-path fixtures (tools/make_golden_train.py)
+TRAIN_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("train_") and f.endswith(".npz"))
+TRAIN_SPECS = {  # dataset, PredictorPlus kwargs, RotatE dir — mirrors tools/make_golden_train.py CASES
+    "train_umls_lstm_sum_bias": ("umls", dict(type="lstm", entity_feature="bias", aggregator="sum"), None),
+    "train_umls_emb_pna_rotate": ("umls", dict(type="emb", entity_feature="RotatE", aggregator="pna"), 200),
+    "train_kinship_lstm_sum_none": ("kinship", dict(type="lstm", entity_feature="none", aggregator="sum"), None),
+    "train_kinship_emb_pna_bias": ("kinship", dict(type="emb", entity_feature="bias", aggregator="pna"), None),
+}
 SMALL_CASES = [c for c in ALL_CASES if c.startswith(("umls", "kinship"))]
 
 

@@ -1,0 +1,119 @@
+"""Training path parity on the MI355X box.
+
+The first three optimizer steps of TrainerPredictor.train on the seeded
+model — batch order (DistributedSampler, world 1), batch contents (edge ids to
+remove), loss per step, and every parameter gradient of step 0 — against the
+reference's own values (tests/golden/train_*.npz, tools/make_golden_train.py).
+The grounding runs in HIP (rnnl_ground + COO export); the aggregation, MLP and
+RotatE run as torch autograd on the exported COO.
+"""
+import numpy as np
+import pytest
+import torch
+from torch.utils import data as torch_data
+
+from conftest import GOLDEN, TRAIN_CASES, TRAIN_SPECS
+
+pytestmark = pytest.mark.gpu
+
+LOSS_TOL = 2e-5      # step-0 loss, relative
+# gradients: fp32 accumulation order differs (index_add vs the reference's
+# expanded index_select backward), and RotatE's d|x|/dx = x/|x| amplifies the
+# rounding of near-zero distances, so the absolute tolerance scales with the
+# tensor's gradient magnitude
+GRAD_RTOL, GRAD_ATOL_MIN, GRAD_ATOL_REL = 2e-4, 2e-6, 2e-3
+LATER_LOSS_TOL = 5e-4  # steps 1-2 follow Adam updates of step-0 gradients (relative)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("case", TRAIN_CASES)
+def test_train_steps_match_reference(case, dev):
+    import os
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset
+    from rnnlogic_amd.predictors import PredictorPlus
+    from rnnlogic_amd.utils import set_seed
+
+    z = np.load(os.path.join(GOLDEN, case + ".npz"), allow_pickle=False)
+    data, kw, dim = TRAIN_SPECS[case]
+    path = datasets.materialize(data)
+    set_seed(1)
+    graph = KnowledgeGraph(path)
+    train_set = TrainDataset(graph, 32)
+    ValidDataset(graph, 32)
+    TestDataset(graph, 32)
+    model = PredictorPlus(graph, num_layers=3, hidden_dim=16,
+                          embedding_path=datasets.rotate_path(data, dim) if dim else None, **kw)
+    model.set_rules(datasets.rule_file(data))
+    sd = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd/")}
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected and all(k.startswith("RotatE.") for k in missing)
+    model = model.to(dev)
+    optim = torch.optim.Adam(model.parameters(), lr=0.005, weight_decay=0)
+    train_set.make_batches()
+    sampler = torch_data.DistributedSampler(train_set, 1, 0)
+    sampler.set_epoch(0)
+    order = list(iter(sampler))[:len(z["order"])]
+    np.testing.assert_array_equal(order, z["order"])
+    model.train()
+    for k, idx in enumerate(order):
+        all_h, all_r, all_t, target, etr = train_set[idx]
+        p = "s%d/" % k
+        for name, got in (("h", all_h), ("r", all_r), ("t", all_t), ("etr", etr)):
+            np.testing.assert_array_equal(got.numpy(), z[p + name], err_msg="%s step %d %s" % (case, k, name))
+        target_t = torch.nn.functional.one_hot(all_t, graph.entity_size)
+        target = (target * 0.2 + target_t * 0.8).to(dev)
+        logits, mask = model(all_h.to(dev), all_r.to(dev), etr.to(dev))
+        want = float(z[p + "loss"])
+        if mask.sum().item() == 0:
+            assert np.isnan(want)
+            continue
+        logits = (torch.softmax(logits, dim=1) + 1e-8).log()
+        loss = -(logits[mask] * target[mask]).sum() / torch.clamp(target[mask].sum(), min=1)
+        loss.backward()
+        tol = LOSS_TOL if k == 0 else LATER_LOSS_TOL
+        assert abs(loss.item() - want) <= tol * abs(want), (case, k, loss.item(), want)
+        if k == 0:
+            for n, prm in model.named_parameters():
+                key = "g/" + n
+                if key not in z.files:
+                    assert prm.grad is None or float(prm.grad.abs().max()) == 0.0, (case, n)
+                    continue
+                g = prm.grad.detach().cpu().numpy()
+                atol = max(GRAD_ATOL_MIN, GRAD_ATOL_REL * float(np.abs(z[key]).max()))
+                np.testing.assert_allclose(g, z[key], atol=atol, rtol=GRAD_RTOL, err_msg="%s grad %s" % (case, n))
+        optim.step()
+        optim.zero_grad()
+
+
+def test_trainer_end_to_end_umls(dev):
+    """TrainerPredictor on the GPU: evaluate() of the seeded model (one
+    forward_rows launch + device ranks) against the reference's evaluate()
+    MRR, then a few train() steps and a second evaluate()."""
+    from conftest import Fixture
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset
+    from rnnlogic_amd.predictors import PredictorPlus
+    from rnnlogic_amd.trainer import TrainerPredictor
+    from rnnlogic_amd.utils import set_seed
+    fx = Fixture("umls_lstm_sum_bias")
+    set_seed(1)
+    graph = KnowledgeGraph(datasets.materialize("umls"))
+    train_set, valid_set, test_set = TrainDataset(graph, 32), ValidDataset(graph, 32), TestDataset(graph, 32)
+    model = PredictorPlus(graph, type="lstm", num_layers=3, hidden_dim=16, entity_feature="bias", aggregator="sum")
+    model.set_rules(datasets.rule_file("umls"))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in fx.sd.items()})
+    optim = torch.optim.Adam(model.parameters(), lr=0.005)
+    solver = TrainerPredictor(model, train_set, valid_set, test_set, optim, gpus=[0])
+    mrr0 = solver.evaluate("test", expectation=True)
+    # the reference breaks exact fp32 ties by row position
+    assert abs(mrr0 - float(fx.z["eval/mrr"])) < 2e-3, (mrr0, float(fx.z["eval/mrr"]))
+    solver.train(batch_per_epoch=8, smoothing=0.2, print_every=4)
+    mrr1 = solver.evaluate("valid", expectation=True)
+    assert 0.0 < mrr1 <= 1.0

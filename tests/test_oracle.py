@@ -8,7 +8,7 @@ import random
 import numpy as np
 import pytest
 
-from conftest import ALL_CASES, SMALL_CASES
+from conftest import ALL_CASES, SMALL_CASES, TRAIN_CASES
 from oracle import reference_np as ref
 
 _graphs = {}
@@ -98,3 +98,32 @@ def test_oracle_batches_and_eval(case, fixtures):
             assert abs(m[key] - float(fx.z["eval/" + key])) <= 5e-7
         mo = ref.rank_metrics(ours_keys, len(ours_keys))
         assert abs(mo["MRR"] - m["MRR"]) < 2e-3
+
+
+@pytest.mark.parametrize("case", TRAIN_CASES)
+def test_oracle_train_loss(case):
+    """The restatement reproduces the reference's step-0 training loss
+    (label smoothing 0.2, softmax cross-entropy over the mask, trainer.py:79-91)
+    on the reference's own training batch (tests/golden/train_*.npz)."""
+    import os
+    from conftest import GOLDEN, TRAIN_SPECS
+    from rnnlogic_amd import datasets
+    z = np.load(os.path.join(GOLDEN, case + ".npz"), allow_pickle=False)
+    data, kw, dim = TRAIN_SPECS[case]
+    g = ref.Graph(datasets.materialize(data))
+    rules = ref.Rules(datasets.rule_file(data), g.relation_size)
+    sd = {k[3:]: z[k] for k in z.files if k.startswith("sd/")}
+    rot = ref.load_rotate(datasets.rotate_path(data, dim)) if dim else None
+    h, r, t, etr = z["s0/h"], z["s0/r"], z["s0/t"], z["s0/etr"]
+    score, mask = ref.predictorplus_forward(sd, dict(kw), g, rules, h, r, etr, rot)
+    E = g.entity_size
+    target = np.zeros((len(h), E), np.float64)
+    for k in range(len(h)):
+        target[k, g.hr2o.get(int(r[k]) * E + int(h[k]), [])] = 1
+    target = target * 0.2
+    target[np.arange(len(h)), t] += 0.8
+    s = score.astype(np.float64)
+    s = s - s.max(1, keepdims=True)
+    logp = np.log(np.exp(s) / np.exp(s).sum(1, keepdims=True) + 1e-8)
+    loss = -(logp[mask] * target[mask]).sum() / max(target[mask].sum(), 1)
+    assert abs(loss - float(z["s0/loss"])) <= 2e-5 * abs(loss), (loss, float(z["s0/loss"]))
