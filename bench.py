@@ -163,6 +163,24 @@ def main():
     base_ms = float(np.mean([e["base"].elapsed_time(e["ground"]) for e in evs]))
     ground_ms = float(np.mean([e["ground"].elapsed_time(e["end"]) for e in evs]))
 
+    # effective shader clock under the RotatE kernel's load (one extra, untimed
+    # launch with the kernel's per-block clock stamps on; rnnl_debug_clock)
+    clock_ghz = None
+    if args.feature == "RotatE":
+        from rnnlogic_amd import _native
+        clk = torch.zeros(2, dtype=torch.int64, device=dev)
+        _native.call("rnnl_debug_clock", clk.data_ptr())
+        try:
+            with torch.no_grad():
+                tmp = torch.empty((nq, graph.entity_size), dtype=torch.float32, device=dev)
+                model.RotatE.score_into(h, r, tmp)
+            torch.cuda.synchronize(dev)
+        finally:
+            _native.call("rnnl_debug_clock", None)
+        ticks, real = clk.tolist()
+        clock_ghz = 0.1 * ticks / max(real, 1)
+        del tmp
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -184,16 +202,19 @@ def main():
     if args.feature == "RotatE":
         ach = rotate_flops / (base_ms * 1e-3) / 1e12
         mode = "direct" if model.RotatE.mode == 0 else "mfma"
-        # VALU issue: cycles per 64 terms on one SIMD at the 2.4 GHz nominal
-        # clock, against the measured floor of the kernel's instruction mix
+        # VALU issue: cycles per 64 terms on one SIMD at the kernel's measured
+        # clock (DVFS lowers it under VALU load), against the floor of the
+        # kernel's instruction mix
         # (tools/micro/valu_rates.hip: sub,sub,mul,fma + pipelined sqrt + add
         # = 19.1; bf16 MFMA + sqrt + add = 13.1)
-        cyc = base_ms * 1e-3 * 2.4e9 * 1024 / (nq * E * D / 64.0)
+        ghz = clock_ghz or 2.4
+        cyc = base_ms * 1e-3 * ghz * 1e9 * 1024 / (nq * E * D / 64.0)
         floor = 19.1 if mode == "direct" else 13.1
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": None, "kernel": "rotate_%s_kernel" % mode,
                 "ms": round(base_ms, 3), "alg_flops": rotate_flops,
-                "valu_issue": {"cycles_per_64_terms": round(cyc, 2), "floor": floor, "frac": round(floor / cyc, 3)},
+                "valu_issue": {"cycles_per_64_terms": round(cyc, 2), "floor": floor, "frac": round(floor / cyc, 3),
+                               "clock_ghz": round(ghz, 3), "clock": "measured in-kernel" if clock_ghz else "nominal"},
                 "note": "fp32 compute-bound on the VALU issue port (sub, sub, mul, fma, one quarter-rate sqrt and "
                         "an add per term; the sqrt inside the reduction keeps it off the matrix cores); "
                         "157.3 TF/s is the fp32 peak shared by VALU and MFMA; entity-table bytes %.3g per launch"

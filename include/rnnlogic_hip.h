@@ -151,6 +151,10 @@ int rnnl_ground_export_entries(void *workspace, int32_t n_queries, int32_t capac
  * counters into dev_counters (12 x uint64: prologue, grounding, candidates,
  * queries, contributions, candidates, then candidate sub-phases). */
 int rnnl_debug_profile(void *dev_counters);
+/* Diagnostic: when non-NULL, later RotatE launches add (shader-clock ticks,
+ * 100 MHz real-time ticks) of every block into dev_counters (2 x uint64); the
+ * ratio x 0.1 GHz is the effective shader clock under that kernel's load. */
+int rnnl_debug_clock(void *dev_counters);
 
 /* --------------------------------------------------------- entity feature --
  * Base-score fills (reference src/predictors.py:260-269). */

@@ -41,6 +41,7 @@ SIGNATURES = [
     ("rnnl_ground_export_candidates", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_ground_export_entries", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
+    ("rnnl_debug_clock", ctypes.c_int, [_P]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
     ("rnnl_rotate_table_sizes", ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P]),

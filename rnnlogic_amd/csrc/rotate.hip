@@ -29,6 +29,26 @@ namespace rnnl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Diagnostic clock (rnnl_debug_clock): when set, thread 0 of every RotatE
+// block adds its (shader-clock ticks, 100 MHz real-time ticks) into
+// clk[0..1]; their ratio x 0.1 GHz is the effective clock under this load.
+static unsigned long long *g_clk = nullptr;
+struct ClockStamp {
+  unsigned long long t0, r0;
+  __device__ __forceinline__ void begin(const unsigned long long *clk) {
+    if (clk && threadIdx.x == 0) {
+      t0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ __forceinline__ void end(unsigned long long *clk) {
+    if (clk && threadIdx.x == 0) {
+      atomicAdd(&clk[0], __builtin_amdgcn_s_memtime() - t0);
+      atomicAdd(&clk[1], __builtin_amdgcn_s_memrealtime() - r0);
+    }
+  }
+};
+
 __host__ __device__ constexpr int64_t ent_pad(int64_t E) { return (E + 255) / 256 * 256; }
 
 // torch computes vec / (range / pi) in fp32 with the python-float divisor
@@ -140,7 +160,8 @@ __global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const f
                                                           const float2 *__restrict__ rtab, int D, float gamma,
                                                           const int64_t *__restrict__ all_h,
                                                           const int64_t *__restrict__ all_r, int nq, int E,
-                                                          float *__restrict__ score, int accumulate) {
+                                                          float *__restrict__ score, int accumulate,
+                                                          unsigned long long *clk) {
   __shared__ __attribute__((aligned(16))) uint2 sA[2][MDC][4][MQ];
   __shared__ __attribute__((aligned(16))) float sN[2][MDC][MQ];
   const int tid = threadIdx.x;
@@ -149,6 +170,8 @@ __global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const f
   const int64_t Ep = ent_pad(E);
   int et, qt;
   if (!xcd_tile((int)(Ep / ME), (nq + MQ - 1) / MQ, et, qt)) return;
+  ClockStamp cs;
+  cs.begin(clk);
   const int q0 = qt * MQ;
   const int e_base = et * ME + wave * 16 * WE;
   const int nchunk = (D + MDC - 1) / MDC;
@@ -241,6 +264,7 @@ __global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const f
     }
     if (c + 1 < nchunk) store_chunk(c + 1, buf ^ 1);
   }
+  cs.end(clk);
   // D layout: lane holds entity column i16 of group g, query rows 4k + j of group qg
 #pragma unroll
   for (int qg = 0; qg < WQ; ++qg)
@@ -262,18 +286,26 @@ __global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const f
 // Direct formulation (mode RNNL_ROTATE_DIRECT, the default): the reference's
 // arithmetic term by term — (hr_re - a), (hr_im - b), sqrt of the sum of
 // squares — on the VALU, so no cancellation beyond the reference's own
-// rounding.  Each lane owns one entity; a wave owns DQ = 16 queries whose
+// rounding.  Each lane owns one entity; a wave owns DQ = 20 queries whose
 // h o r values for the current dim are wave-uniform and come in as SGPR
 // operands (s_load from the per-call hr workspace, built by rotate_hr_kernel)
 // — per term the VALU issues exactly sub, sub, mul, fma, sqrt, add.
 // Sums are kept per DCH-dim chunk and folded into the row total, which keeps
-// the fp32 summation error of a 1000-term row near the reference's.
+// the fp32 summation error of a 1000-term row near the reference's.  Entity
+// values come LCH = 2 dims at a time into fixed register slots, one block
+// ahead.  DQ = 20 / LCH = 2 measured best (75 ms vs 88 ms for 16 / 1 on the
+// FB15k-237 bench shape): more terms per dim amortise the per-dim loads and
+// address work, at 5 waves per SIMD.
 constexpr int RB = 256;   // entities per block (one per lane)
 #ifndef RNNL_DQ
-#define RNNL_DQ 16
+#define RNNL_DQ 20
 #endif
 constexpr int DQ = RNNL_DQ;  // queries per block (SGPR-resident)
 constexpr int DCH = 32;   // dims per partial sum
+#ifndef RNNL_LCH
+#define RNNL_LCH 2
+#endif
+constexpr int LCH = RNNL_LCH;  // dims per entity-value prefetch block (divides DCH)
 
 // hr[g][d][0..15 | 16..31] = (re | im) of (h o r)_d for queries 16 g + k
 __global__ void rotate_hr_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D,
@@ -295,10 +327,12 @@ __global__ void rotate_hr_kernel(const float *__restrict__ eemb, const float2 *_
 __global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restrict__ ptab,
                                                            const float *__restrict__ hr, int D, float gamma,
                                                            int nq, int E, float *__restrict__ score,
-                                                           int accumulate) {
+                                                           int accumulate, unsigned long long *clk) {
   const int64_t Ep = ent_pad(E);
   int et, qt;
   if (!xcd_tile((int)(Ep / RB), (nq + DQ - 1) / DQ, et, qt)) return;
+  ClockStamp cs;
+  cs.begin(clk);
   const int e = et * RB + threadIdx.x;  // < Ep: the table is padded
   const int q0 = qt * DQ;
   const float *hp = hr + (int64_t)qt * D * 2 * DQ;
@@ -309,25 +343,45 @@ __global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restri
   float acc[DQ], sq[DQ];
 #pragma unroll
   for (int k = 0; k < DQ; ++k) acc[k] = sq[k] = 0.f;
-  float va = ap[0], vb = ap[Ep];
+  // entity values: LCH dims at a time, loaded one LCH-block ahead (fixed
+  // register slots per dim, so the prefetch never waits on a rotation)
+  float va[LCH], vb[LCH], na[LCH], nb[LCH];
+#pragma unroll
+  for (int j = 0; j < LCH; ++j) {
+    const int64_t d = min(j, D - 1);
+    va[j] = ap[d * 2 * Ep];
+    vb[j] = ap[d * 2 * Ep + Ep];
+  }
   for (int d0 = 0; d0 < D; d0 += DCH) {
-    const int nd = min(DCH, D - d0);
     float part[DQ];
 #pragma unroll
     for (int k = 0; k < DQ; ++k) part[k] = 0.f;
-    for (int dd = 0; dd < nd; ++dd) {
-      const int d = d0 + dd;
-      const float a = va, b = vb;
-      const int64_t dn = min(d + 1, D - 1);  // prefetch the next dim's entity values
-      va = ap[dn * 2 * Ep];
-      vb = ap[dn * 2 * Ep + Ep];
-      const float *h = hp + (int64_t)d * 2 * DQ;  // wave-uniform: s_load
+    for (int d1 = d0; d1 < min(d0 + DCH, D); d1 += LCH) {
 #pragma unroll
-      for (int k = 0; k < DQ; ++k) {
-        part[k] += __builtin_amdgcn_sqrtf(sq[k]);  // dim d - 1 (sqrt(0) = 0 before the first)
-        const float x = h[k] - a;
-        const float y = h[DQ + k] - b;
-        sq[k] = fmaf(x, x, y * y);
+      for (int j = 0; j < LCH; ++j) {
+        const int64_t d = min(d1 + LCH + j, D - 1);
+        na[j] = ap[d * 2 * Ep];
+        nb[j] = ap[d * 2 * Ep + Ep];
+      }
+#pragma unroll
+      for (int j = 0; j < LCH; ++j) {
+        const int d = d1 + j;
+        if (d < D) {  // wave-uniform
+          const float a = va[j], b = vb[j];
+          const float *h = hp + (int64_t)d * 2 * DQ;  // wave-uniform: s_load
+#pragma unroll
+          for (int k = 0; k < DQ; ++k) {
+            part[k] += __builtin_amdgcn_sqrtf(sq[k]);  // dim d - 1 (sqrt(0) = 0 before the first)
+            const float x = h[k] - a;
+            const float y = h[DQ + k] - b;
+            sq[k] = fmaf(x, x, y * y);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < LCH; ++j) {
+        va[j] = na[j];
+        vb[j] = nb[j];
       }
     }
 #pragma unroll
@@ -335,6 +389,7 @@ __global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restri
   }
 #pragma unroll
   for (int k = 0; k < DQ; ++k) acc[k] += __builtin_amdgcn_sqrtf(sq[k]);  // v_sqrt_f32 (1 ulp)
+  cs.end(clk);
   if (e < E) {
 #pragma unroll
     for (int k = 0; k < DQ; ++k) {
@@ -454,6 +509,11 @@ int rnnl_fill_value(float v, int64_t n, float *score, void *stream) {
   return RNNL_OK;
 }
 
+int rnnl_debug_clock(void *dev_counters) {
+  g_clk = static_cast<unsigned long long *>(dev_counters);
+  return RNNL_OK;
+}
+
 static bool valid_mode(int32_t mode) { return mode == RNNL_ROTATE_DIRECT || mode == RNNL_ROTATE_MFMA; }
 
 int rnnl_rotate_table_sizes(int32_t E, int32_t D, int32_t n_rel_total, int32_t mode, size_t *entity_bytes,
@@ -525,11 +585,11 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
     RNNL_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(rotate_direct_kernel, dim3(xcd_grid(ent_pad(E) / RB, (nq + DQ - 1) / DQ)), dim3(RB), 0,
                        (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E, score,
-                       accumulate);
+                       accumulate, g_clk);
   } else {
     hipLaunchKernelGGL(rotate_mfma_kernel, dim3(xcd_grid(ent_pad(E) / ME, (nq + MQ - 1) / MQ)), dim3(256), 0,
                        (hipStream_t)stream, eemb, (const uint2 *)etab, (const float2 *)rtab, D, gamma, all_h, all_r,
-                       nq, E, score, accumulate);
+                       nq, E, score, accumulate, g_clk);
   }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;

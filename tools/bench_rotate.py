@@ -99,7 +99,7 @@ def main():
             continue
         L = load(p)
         out.zero_()
-        t = run(L, _native.ROTATE_DIRECT if name.startswith('direct') else _native.ROTATE_MFMA, out, a.reps)
+        t = run(L, _native.ROTATE_MFMA if name.startswith('mfma') else _native.ROTATE_DIRECT, out, a.reps)
         print("%-20s %8.2f ms  maxdiff %.3g" % (name, sum(t) / len(t), (out - ref).abs().max().item()), flush=True)
 
 

@@ -254,6 +254,31 @@ __global__ void k_mix(float *out, unsigned long long *clk, float x) {
   stamp(clk, 1);
 }
 
+// the direct term with the query side from s_load (wave-uniform buffer reads,
+// as rotate_direct_kernel), entity values from VGPRs
+__constant__ float c_h[64 * 32];
+__global__ void k_direct_sgpr(float *out, unsigned long long *clk, float x) {
+  stamp(clk, 0);
+  const float *hq = c_h;  // 32 floats per iteration, uniform (s_load)
+  float acc[16], sq[16], a = x + threadIdx.x, b = x - threadIdx.x;
+  for (int j = 0; j < 16; ++j) acc[j] = sq[j] = 0;
+  for (int i = 0; i < ITERS / 2; ++i) {
+    const float *h = hq + (i & 63) * 32;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc[j] += __builtin_amdgcn_sqrtf(sq[j]);
+      const float dx = h[j] - a;
+      const float dy = h[16 + j] - b;
+      sq[j] = fmaf(dx, dx, dy * dy);
+    }
+    a += 1.0f;
+    b -= 1.0f;
+  }
+  float s = 0; for (int j = 0; j < 16; ++j) s += acc[j] + sq[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  stamp(clk, 1);
+}
+
 template <typename K>
 double run(K kern, float *out, unsigned long long *clk, int blocks, int threads, double *ghz) {
   hipEvent_t e0, e1;
@@ -291,6 +316,8 @@ int main() {
   printf("direct nosqrt:  %.3f ms %.2f GHz -> %.2f cyc/wave-term/SIMD\n", t, g, cyc(t, g, ITERS / 2 * 16.0));
   t = run(k_direct_pipe, out, clk, blocks, threads, &g);
   printf("direct pipelined: %.3f ms %.2f GHz -> %.2f cyc/wave-term/SIMD\n", t, g, cyc(t, g, ITERS / 2 * 16.0));
+  t = run(k_direct_sgpr, out, clk, blocks, threads, &g);
+  printf("direct sgpr-load pipelined: %.3f ms %.2f GHz -> %.2f cyc/wave-term/SIMD\n", t, g, cyc(t, g, ITERS / 2 * 16.0));
   t = run(k_mix, out, clk, blocks, threads, &g);
   printf("fma+sqrt mix:   %.3f ms %.2f GHz -> %.2f cyc/(fma+sqrt)/SIMD\n", t, g, cyc(t, g, ITERS / 2 * 16.0));
   t = run(k_sqrt, out, clk, blocks, threads, &g);
