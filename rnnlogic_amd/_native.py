@@ -10,6 +10,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
+# diagnostic A/B builds (tools/*_variants.sh) may be selected with RNNL_LIB
+LIB_PATH = os.environ.get("RNNL_LIB", LIB_PATH)
 
 RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL = 0, 1, 2, 3, 4, 5
 AGG_SUM, AGG_PNA = 0, 1

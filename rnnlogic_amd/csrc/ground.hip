@@ -38,6 +38,8 @@ constexpr int HCAP = 4096;   // phase-A hash slots ((node, entity) -> count)
 constexpr int WBITS = 11;    // phase-B entity window: WIN = 2048 entities
 constexpr int WIN = 1 << WBITS;
 constexpr int MAXWIN = 256;  // windows per graph (|E| <= 524288)
+constexpr int HB = 2048;     // phase-B candidate hash slots
+constexpr int HB_LOAD = 1536;  // max contributions per hash pass (load <= 0.75)
 constexpr int WG_PER_CU = 3;
 constexpr int NUM_CU = 256;
 constexpr int EMPTY = -1;
@@ -235,6 +237,12 @@ struct __align__(16) Smem {
       int off[WIN];
       int st[WIN];   // slot -> entity
     } b;
+    struct {
+      int key[HB];   // entity (EMPTY: free)
+      int cnt[HB];   // bucket size, then the scatter fill counter / degree
+      int off[HB];   // bucket start within the pass
+      int cid[HB];   // candidate index within the pass
+    } c;
   } u;
   int ent_v[BS], ent_fch[BS], item_off[BS];
   uint32_t ent_c[BS];
@@ -319,6 +327,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
     if (p.rl.node_nrules[root] > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
   }
   wg_sync_global();
+  if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
   int cur = 0, n_prev = 1;
   for (int d = 1; d <= depth; ++d) {
     const int nxt = cur ^ 1;
@@ -337,6 +346,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       const int ioff = block_scan(nch, S.ws, NI);
       S.item_off[tid] = ioff;
       __syncthreads();
+      PSTAMP(3);
       for (int ib = 0; ib < NI; ib += BS) {
         const int k = ib + tid;
         int deg = 0;
@@ -360,6 +370,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
         const int eoff = block_scan(deg, S.ws, NE);
         S.edge_off[tid] = eoff;
         __syncthreads();
+        PSTAMP(4);
         const int nit = min(BS, NI - ib);
         for (int eb = 0; eb < NE; eb += BS) {
           const int j = eb + tid;
@@ -378,6 +389,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
           }
         }
         __syncthreads();
+        PSTAMP(5);
       }
     }
     // compact the hash into the next frontier and clear it
@@ -390,6 +402,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       }
     }
     wg_sync_global();
+    PSTAMP(6);
     n_prev = min((int64_t)S.nd, p.fcap);
     __syncthreads();
     if (tid == 0) S.nd = 0;
@@ -489,6 +502,95 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   return nc;
 }
 
+// Sparse windows: contributions [beg, end) of consecutive entity windows
+// (end - beg <= HB_LOAD) bucketed through an LDS hash keyed by entity —
+// O(contributions) work and six barriers, against the dense window_pass's
+// O(WIN) passes.  Candidate order within the query is the hash order (nothing
+// downstream depends on it: scores scatter by entity, PNA's mean and the
+// digests are order-independent sums).  Same outputs as window_pass otherwise.
+__device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
+  uint32_t h = hash32((uint32_t)t) >> (32 - 11);
+#pragma unroll 1
+  for (int probe = 0; probe < HB; ++probe) {
+    const int k = insert ? atomicCAS(&S.u.c.key[h], EMPTY, t) : S.u.c.key[h];
+    if (k == t || (insert && k == EMPTY)) return (int)h;
+    h = (h + 1) & (HB - 1);
+  }
+  return -1;  // unreachable: at most HB_LOAD < HB distinct keys
+}
+
+__device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int end, int64_t cbase,
+                         bool degree_only) {
+  const int tid = threadIdx.x;
+  const int32_t *wt = sl.fn[0], *wn = sl.fv[0];
+  const uint32_t *wc = sl.fc[0];
+  for (int i = tid; i < HB; i += BS) {
+    S.u.c.key[i] = EMPTY;
+    S.u.c.cnt[i] = 0;
+  }
+  __syncthreads();
+  for (int i = beg + tid; i < end; i += BS) atomicAdd(&S.u.c.cnt[hb_slot(S, wt[i], true)], 1);
+  __syncthreads();
+  // one scan of (bucket size << 12 | occupied): bucket offsets and candidate ids
+  constexpr int PER = HB / BS;
+  int loc[PER];
+  int sum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int sidx = tid * PER + j;
+    loc[j] = (S.u.c.cnt[sidx] << 12) | (S.u.c.key[sidx] != EMPTY ? 1 : 0);
+    sum += loc[j];
+  }
+  int total;
+  int run = block_scan(sum, S.ws, total);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int sidx = tid * PER + j;
+    S.u.c.off[sidx] = run >> 12;
+    S.u.c.cid[sidx] = run & 4095;
+    run += loc[j];
+  }
+  const int nc = total & 4095;
+  __syncthreads();
+  if (degree_only) {
+    // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
+    for (int i = tid; i < HB; i += BS) S.u.c.cnt[i] = 0;
+    __syncthreads();
+    for (int i = beg + tid; i < end; i += BS)
+      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, wt[i], false)]),
+                wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
+    __syncthreads();
+    for (int i = tid; i < HB; i += BS) {
+      if (S.u.c.key[i] != EMPTY) {
+        const float degf = (float)((double)(uint32_t)S.u.c.cnt[i] + 1.0);
+        atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
+      }
+    }
+    __syncthreads();
+    return nc;
+  }
+  const int64_t qb = S.qbase;
+  for (int i = tid; i < HB; i += BS) {
+    if (S.u.c.key[i] != EMPTY) {
+      const int64_t c = cbase + S.u.c.cid[i];
+      p.c_t[c] = S.u.c.key[i];
+      p.c_beg[c] = (int32_t)(qb + beg + S.u.c.off[i]);
+      p.c_cnt[c] = S.u.c.cnt[i];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < HB; i += BS) S.u.c.cnt[i] = 0;
+  __syncthreads();
+  for (int i = beg + tid; i < end; i += BS) {  // scatter (node, count) into the buckets
+    const int sl2 = hb_slot(S, wt[i], false);
+    const int64_t pos = qb + beg + S.u.c.off[sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
+    p.b_node[pos] = wn[i];
+    p.b_cnt[pos] = wc[i];
+  }
+  __syncthreads();
+  return nc;
+}
+
 // Counting sort of the contributions by entity window into fn/fv/fc[0]
 // (free during phase B), then window_pass over every non-empty window.
 __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P, bool degree_only, bool sorted) {
@@ -519,11 +621,20 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
     }
     wg_sync_global();
   }
+  // consecutive windows are merged while their contributions fit one hash
+  // pass; a window heavier than that takes the dense direct-mapped pass
   int ncand = 0;
-  for (int w = 0; w < nwin; ++w) {
-    const int beg = S.wbeg[w], end = S.wbeg[w + 1];
-    if (beg == end) continue;
-    ncand += window_pass(p, S, sl, w << WBITS, beg, end, S.qbase + ncand, degree_only);
+  for (int w = 0; w < nwin;) {
+    const int beg = S.wbeg[w];
+    if (S.wbeg[w + 1] - beg > HB_LOAD) {
+      ncand += window_pass(p, S, sl, w << WBITS, beg, S.wbeg[w + 1], S.qbase + ncand, degree_only);
+      ++w;
+      continue;
+    }
+    int w2 = w + 1;
+    while (w2 < nwin && S.wbeg[w2 + 1] - beg <= HB_LOAD) ++w2;
+    if (S.wbeg[w2] > beg) ncand += hash_pass(p, S, sl, beg, S.wbeg[w2], S.qbase + ncand, degree_only);
+    w = w2;
   }
   return ncand;
 }
@@ -642,8 +753,10 @@ __global__ __launch_bounds__(BS) void ground_kernel(KParams p) {
     __syncthreads();
   }
   if (p.prof && tid == 0) {
+#pragma unroll
     for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[k], pr[k]);
-    for (int k = 0; k < 3; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
   }
 }
 
@@ -688,6 +801,9 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
     }
   }
   if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+#ifdef RNNL_SCORE_NOMLP  // diagnostic build: the node-sum gather alone
+  return (float)a1[0] + (float)a1[15];
+#endif
   constexpr double inv_fix = 1.0 / (double)(1 << kFixShift);
   float x1[16];
   if constexpr (AGG == RNNL_AGG_SUM) {

@@ -42,7 +42,8 @@ def main():
     print("queries %d  contributions/q %.1f  candidates/q %.1f" % (p[3], p[4] / nq, p[5] / nq))
     for name, v in zip(["prologue", "grounding(A)", "candidates(B)"], p[:3]):
         print("  %-14s %10.0f cycles/query" % (name, v / nq))
-    for name, v in zip(["B mark+slots", "B count+records", "B scatter", "-", "-", "-"], p[6:12]):
+    for name, v in zip(["B mark+slots", "B count+records", "B scatter", "A node+scan", "A item+scan",
+                        "A edges"], p[6:12]):
         print("  %-14s %10.0f cycles/query" % (name, v / nq))
     print("events ms: nodes %.3f base %.3f ground %.3f" % (ev["start"].elapsed_time(ev["base"]),
           ev["base"].elapsed_time(ev["ground"]), ev["ground"].elapsed_time(ev["end"])))
