@@ -79,13 +79,17 @@ int rnnl_rules_node_of_rule(rnnl_rules r, int32_t *node_of_rule);
 /* Per-node aggregate of rule embeddings (device): rule_emb is n_rules x H
  * (row stride `ld` floats), H == 16.  Writes node_w: n_nodes records of
  * info5[3 + aggregator] bytes.
- *   SUM record: int64 fix(sum x)[16]
+ *   SUM record: int32 fix_s(sum x)[16], members summed in rule-id order (f32),
+ *               then one shift s for the whole table (|fix| < 2^30; stored
+ *               in a trailer after the records)
  *   PNA record: int64 fix(sum x)[16] | int64 fix(sum x^2)[16] | f32 min x[16] | f32 max x[16]
- * where fix(v) = round(v * 2^28).  Members are summed in rule-id order (fp32),
- * and the per-candidate sums over nodes are then exact integer arithmetic, so
- * every score is a deterministic function of its per-rule path counts. */
+ * where fix(v) = round(v * 2^28).  The forward accumulates both in exact
+ * int64 arithmetic, so a score does not depend on the order in which the
+ * kernel meets a candidate's (node, count) entries.  Buffer size:
+ * rnnl_node_weights_size. */
 int rnnl_node_weights(rnnl_rules r, const float *rule_emb, int32_t ld, int32_t aggregator, void *node_w,
                       void *stream);
+int rnnl_node_weights_size(rnnl_rules r, int32_t aggregator, size_t *bytes);
 
 /* ------------------------------------------------------------- forward --
  * Replaces the body of PredictorPlus.forward (reference

@@ -11,7 +11,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
 # diagnostic A/B builds (tools/*_variants.sh) may be selected with RNNL_LIB
-LIB_PATH = os.environ.get("RNNL_LIB", LIB_PATH)
+LIB_PATH = os.environ.get("RNNL_LIB") or LIB_PATH
 
 RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL = 0, 1, 2, 3, 4, 5
 AGG_SUM, AGG_PNA = 0, 1
@@ -35,6 +35,7 @@ SIGNATURES = [
     ("rnnl_rules_info", ctypes.c_int, [_P, _P]),
     ("rnnl_rules_node_of_rule", ctypes.c_int, [_P, _P]),
     ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P]),
+    ("rnnl_node_weights_size", ctypes.c_int, [_P, _I32, _P]),
     ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     ("rnnl_predictorplus_forward", ctypes.c_int,
      [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),

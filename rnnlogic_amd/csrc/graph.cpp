@@ -202,6 +202,24 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
       return RNNL_ERR_INVALID;
     }
   }
+  // leaves per head (nodes where rules end), in node-id order
+  const int n_nodes_total = (int)node_rel.size();
+  std::vector<int32_t> head_leaf_ptr(R + 1, 0), head_leaf_node, node_leaf(n_nodes_total, -1);
+  int max_leaves = 0, max_head_nodes = 0;
+  for (int r = 0; r < R; ++r) {
+    head_leaf_ptr[r] = (int32_t)head_leaf_node.size();
+    if (head_root[r] >= 0) {
+      int nl = 0;
+      for (int n = head_root[r]; n < head_root[r] + head_nodes[r]; ++n)
+        if (node_nrules[n] > 0) {
+          node_leaf[n] = nl++;
+          head_leaf_node.push_back(n);
+        }
+      max_leaves = std::max(max_leaves, nl);
+      max_head_nodes = std::max(max_head_nodes, head_nodes[r]);
+    }
+  }
+  head_leaf_ptr[R] = (int32_t)head_leaf_node.size();
   auto *rs = new rnnl_rules_s;
   (void)hipGetDevice(&rs->device);
   rs->R = R;
@@ -211,6 +229,8 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   rs->d.max_depth = max_depth;
   rs->d.n_heads = R;
   rs->node_of_rule = std::move(node_of_rule);
+  rs->d.max_leaves = max_leaves;
+  rs->d.max_head_nodes = max_head_nodes;
   int rc = RNNL_OK;
   if ((rc = upload(head_root, &rs->mem[0], &rs->d.head_root)) ||
       (rc = upload(head_depth, &rs->mem[1], &rs->d.head_depth)) ||
@@ -221,7 +241,10 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
       (rc = upload(node_nrules, &rs->mem[6], &rs->d.node_nrules)) ||
       (rc = upload(node_rule_ptr, &rs->mem[7], &rs->d.node_rule_ptr)) ||
       (rc = upload(node_rules, &rs->mem[8], &rs->d.node_rules)) ||
-      (rc = upload(node_fp, &rs->mem[9], &rs->d.node_fp))) {
+      (rc = upload(node_fp, &rs->mem[9], &rs->d.node_fp)) ||
+      (rc = upload(head_leaf_ptr, &rs->mem[10], &rs->d.head_leaf_ptr)) ||
+      (rc = upload(head_leaf_node, &rs->mem[11], &rs->d.head_leaf_node)) ||
+      (rc = upload(node_leaf, &rs->mem[12], &rs->d.node_leaf))) {
     rnnl_rules_destroy(rs);
     return rc;
   }

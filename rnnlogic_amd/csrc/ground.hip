@@ -34,13 +34,23 @@ namespace rnnl {
 
 constexpr int BS = 256;      // threads per workgroup
 constexpr int NW = BS / 64;  // waves
-constexpr int HCAP = 4096;   // phase-A hash slots ((node, entity) -> count)
-constexpr int WBITS = 11;    // phase-B entity window: WIN = 2048 entities
+#ifndef RNNL_HBITS
+#define RNNL_HBITS 12
+#endif
+#ifndef RNNL_WBITS
+#define RNNL_WBITS 11
+#endif
+#ifndef RNNL_WG_PER_CU
+#define RNNL_WG_PER_CU 3
+#endif
+constexpr int HBITS = RNNL_HBITS;
+constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count)
+constexpr int WBITS = RNNL_WBITS;  // phase-B entity window: WIN entities
 constexpr int WIN = 1 << WBITS;
-constexpr int MAXWIN = 256;  // windows per graph (|E| <= 524288)
-constexpr int HB = 2048;     // phase-B candidate hash slots
-constexpr int HB_LOAD = 1536;  // max contributions per hash pass (load <= 0.75)
-constexpr int WG_PER_CU = 3;
+constexpr int MAXWIN = (1 << 19) >> WBITS;  // windows per graph (|E| <= 524288)
+constexpr int HB = WIN;            // phase-B candidate hash slots (one window at <= 0.75 load... or less)
+constexpr int HB_LOAD = HB * 3 / 4;  // max contributions per hash pass
+constexpr int WG_PER_CU = RNNL_WG_PER_CU;
 constexpr int NUM_CU = 256;
 constexpr int EMPTY = -1;
 
@@ -282,7 +292,7 @@ __device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, 
 
 // (node, entity) += c in the phase-A hash; false if the table is full.
 __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
-  uint32_t h = hash32((uint32_t)key) >> (32 - 12);
+  uint32_t h = hash32((uint32_t)key) >> (32 - HBITS);
 #pragma unroll 1
   for (int probe = 0; probe < 64; ++probe) {
     const int k = atomicCAS(&S.u.a.key[h], EMPTY, key);
@@ -509,7 +519,7 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
 // downstream depends on it: scores scatter by entity, PNA's mean and the
 // digests are order-independent sums).  Same outputs as window_pass otherwise.
 __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
-  uint32_t h = hash32((uint32_t)t) >> (32 - 11);
+  uint32_t h = hash32((uint32_t)t) >> (32 - WBITS);
 #pragma unroll 1
   for (int probe = 0; probe < HB; ++probe) {
     const int k = insert ? atomicCAS(&S.u.c.key[h], EMPTY, t) : S.u.c.key[h];
@@ -648,8 +658,11 @@ __device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, 
   if (p.n_cand) p.n_cand[q] = S.err ? -2 : -1;
 }
 
+#ifndef RNNL_GROUND_MINB
+#define RNNL_GROUND_MINB 1
+#endif
 template <int AGG>
-__global__ __launch_bounds__(BS) void ground_kernel(KParams p) {
+__global__ __launch_bounds__(BS, RNNL_GROUND_MINB) void ground_kernel(KParams p) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
@@ -941,6 +954,218 @@ __global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__res
   }
 }
 
+// ---------------------------------------------------------------- K2 (sum): staged scoring
+// FuncToNodeSum path.  The node records of a query's head relation (only its
+// leaves: <= a few hundred, f32 x 16 each) are staged into LDS once per run of
+// same-relation queries, so the per-entry gather reads LDS instead of ~128 B
+// of L2/MALL per (candidate, node) entry.  Sums are accumulated in fp64 from
+// the exact products count x f32: the result is independent of the entry
+// order (which comes from LDS atomics) short of a double rounding.
+#ifndef RNNL_QCHUNK
+#define RNNL_QCHUNK 1
+#endif
+#ifndef RNNL_SCORE_WG_PER_CU
+#define RNNL_SCORE_WG_PER_CU 8
+#endif
+constexpr int QCHUNK = RNNL_QCHUNK;  // consecutive queries dequeued together (same relation in batch order)
+
+struct SumStage {
+  float *rec;      // [max_leaves][16]
+  int *nr;         // [max_leaves] rules ending at the leaf
+  uint2 *fp;       // [max_leaves] node fingerprint (digest)
+  short *map;      // [max_head_nodes] node - root -> leaf index
+};
+
+__host__ __device__ inline int64_t sum_stage_bytes(int max_leaves, int max_head_nodes) {
+  return (int64_t)max_leaves * (64 + 4 + 8) + (int64_t)max_head_nodes * 2 + 64;
+}
+
+template <bool STAGED>
+__device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st, int root, int beg, int cnt,
+                                           float inv_scale, float f[16], long long &deg, uint64_t &fp) {
+  long long acc[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) acc[d] = 0;
+  deg = 0;
+  fp = 0;
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int n = p.b_node[e];
+    const uint32_t cu = p.b_cnt[e];
+    const long long c = cu;
+    const int *x;
+    int nr;
+    uint64_t nf;
+    if constexpr (STAGED) {
+      const int li = st.map[n - root];
+      x = reinterpret_cast<const int *>(st.rec) + li * 16;
+      nr = st.nr[li];
+      nf = ((uint64_t)st.fp[li].y << 32) | st.fp[li].x;
+    } else {
+      x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+      nr = p.rl.node_nrules[n];
+      nf = p.rl.node_fp[n];
+    }
+    if (cu < 0x80000000u) {  // one v_mad_i64_i32 per element
+      const int ci = (int)cu;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) acc[d] += (long long)ci * x[d];
+    } else {
+#pragma unroll
+      for (int d = 0; d < 16; ++d) acc[d] += c * x[d];
+    }
+    deg += c * nr;
+    fp += (uint64_t)c * nf;
+  }
+#pragma unroll
+  for (int d = 0; d < 16; ++d) f[d] = (float)((double)acc[d] * (double)inv_scale);
+}
+
+// FuncToNodeSum tail + score_model on the candidate's feature sums
+__device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const float *relb, const float f[16]) {
+  using L = WL<RNNL_AGG_SUM>;
+  float x1[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(f[i], wl[L::ADDW + o * 16 + i], acc);
+    x1[o] = acc + wl[L::ADDB + o];
+  }
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+  float out = 0.f;
+#pragma unroll 2
+  for (int o = 0; o < 128; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], wl[L::S0X + o * 16 + i], acc);
+    acc = fmaxf(acc + relb[o], 0.f);
+    out = fmaf(acc, wl[L::S1W + o], out);
+  }
+  return out + wl[L::S1B];
+}
+
+template <bool STAGED>
+__global__ __launch_bounds__(BS) void score_sum_kernel(KParams p, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_SUM>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+  float *s_w = reinterpret_cast<float *>(dyn);
+  float *s_relb = s_w + L::N;
+  SumStage st{};
+  if constexpr (STAGED) {
+    unsigned char *b = dyn + (L::N + 128) * 4;
+    st.fp = reinterpret_cast<uint2 *>(b);
+    b += (int64_t)p.rl.max_leaves * 8;
+    st.rec = reinterpret_cast<float *>(b);
+    b += (int64_t)p.rl.max_leaves * 64;
+    st.nr = reinterpret_cast<int *>(b);
+    b += (int64_t)p.rl.max_leaves * 4;
+    st.map = reinterpret_cast<short *>(b);
+  }
+  __shared__ int s_q0, s_r;
+  __shared__ unsigned long long s_dig;
+  const int tid = threadIdx.x;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  for (int i = tid; i < L::N; i += BS) {
+    float v = 0.f;
+    if (i < L::ADDB) v = W[W_ADDW + i];
+    else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
+    else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
+    else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
+    else if (i < L::S1W) v = W[W_S0X + i - L::S0X];
+    else if (i < L::S1B) v = W[W_S1W + i - L::S1W];
+    else if (i == L::S1B) v = W[W_S1B];
+    s_w[i] = v;
+  }
+  if (tid == 0) s_r = -1;
+  const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
+  const float inv_scale = ldexpf(1.f, -shift);
+#pragma unroll 1
+  while (true) {
+    __syncthreads();
+    if (tid == 0) s_q0 = (int)atomicAdd(&hdr[H_DEQUEUE2], (unsigned)QCHUNK);
+    __syncthreads();
+    const int q0 = s_q0;
+    if (q0 >= p.nq) break;
+    for (int q = q0; q < min(q0 + QCHUNK, p.nq); ++q) {
+      const int nc = p.n_cand[q];
+      if (nc <= 0) {
+        if (tid == 0 && p.digest && nc == 0) p.digest[q] = 0;
+        continue;
+      }
+      const int r = (int)p.all_r[q];
+      const int root = p.rl.head_root[r];
+      if (r != s_r) {
+        __syncthreads();  // every lane is done with the previous relation's stage and bias
+        if (tid < 128) {
+          // relation half of score_model.layers.0 folded into a per-query bias
+          float acc = p.s0_b[tid];
+          for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[tid * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+          s_relb[tid] = acc;
+        }
+        if constexpr (STAGED) {
+          const int lp = p.rl.head_leaf_ptr[r], nl = p.rl.head_leaf_ptr[r + 1] - lp;
+          for (int i = tid; i < p.rl.head_nodes[r]; i += BS) st.map[i] = (short)p.rl.node_leaf[root + i];
+          for (int i = tid; i < nl * 16; i += BS) {
+            const int n = p.rl.head_leaf_node[lp + i / 16];
+            st.rec[i] = reinterpret_cast<const float *>(p.node_w + (int64_t)n * kStrideSum)[i % 16];  // int32 bits
+          }
+          for (int i = tid; i < nl; i += BS) {
+            const int n = p.rl.head_leaf_node[lp + i];
+            st.nr[i] = p.rl.node_nrules[n];
+            const uint64_t f = p.rl.node_fp[n];
+            st.fp[i] = make_uint2((unsigned)f, (unsigned)(f >> 32));
+          }
+        }
+        if (tid == 0) {
+          s_r = r;
+          s_dig = 0ull;
+        }
+        __syncthreads();
+      } else if (p.digest) {
+        __syncthreads();
+        if (tid == 0) s_dig = 0ull;
+        __syncthreads();
+      }
+      const int64_t qb = p.q_base[q];
+      for (int s2 = tid; s2 < nc; s2 += BS) {
+        const int t = p.c_t[qb + s2];
+        float f[16];
+        long long deg;
+        uint64_t fp;
+        gather_sum<STAGED>(p, st, root, p.c_beg[qb + s2], p.c_cnt[qb + s2], inv_scale, f, deg, fp);
+        if (p.digest) atomicAdd(&s_dig, (unsigned long long)mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp))));
+        // keep the loop-invariant LDS weight reads inside the loop (hoisted,
+        // they would pin ~200 VGPRs and starve occupancy)
+        asm volatile("" ::: "memory");
+        const float out = mlp_sum(s_w, s_relb, f);
+        const int64_t idx = (int64_t)q * p.g.E + t;
+        if (p.feature == RNNL_FEATURE_NONE)
+          p.score[idx] = out;
+        else
+          p.score[idx] = out + p.score[idx];
+        if (p.mask) p.mask[idx] = 1;
+      }
+      if (p.digest) {
+        __syncthreads();
+        if (tid == 0) p.digest[q] = s_dig;
+      }
+    }
+  }
+}
+
 // Packs the MLP weights behind the workspace header (layout W_* above).
 __global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
   const int kin = p.agg == RNNL_AGG_SUM ? 16 : 192;
@@ -982,8 +1207,9 @@ __global__ void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, 
   }
   const double sc = (double)(1 << kFixShift);
   if (agg == RNNL_AGG_SUM) {
-    long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStrideSum);
-    rec[d] = llrint((double)s1 * sc);
+    // f32 sum for now; node_fix_kernel turns it into int32 fixed point
+    reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = s1;
+    atomicMax(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStrideSum), __float_as_uint(fabsf(s1)));
   } else {
     long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStridePna);
     rec[d] = llrint((double)s1 * sc);
@@ -1025,6 +1251,25 @@ __global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent
   }
 }
 
+// SUM records -> int32 fixed point with one shift for the whole table:
+// |fix| < 2^30 for the largest |sum|, so a candidate's int64 sum of
+// count x fix is exact (deterministic in any entry order) with ~2^-30
+// relative resolution.  Trailer: u32 max|x| bits, i32 shift.
+__global__ void node_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
+  unsigned int *trailer = reinterpret_cast<unsigned int *>(out + (int64_t)n_nodes * kStrideSum);
+  const float mx = __uint_as_float(trailer[0]);
+  int e = 0;
+  if (mx > 0.f) frexpf(mx, &e);  // mx < 2^e
+  const int shift = min(max(30 - e, 0), 60);
+  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = (unsigned)shift;
+  const float sc = ldexpf(1.f, min(shift, 120));
+  const int64_t n = (int64_t)n_nodes * 16;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float *f = reinterpret_cast<float *>(out) + i;
+    reinterpret_cast<int *>(out)[i] = (int)rintf(*f * sc);
+  }
+}
+
 }  // namespace rnnl
 
 using namespace rnnl;
@@ -1037,11 +1282,26 @@ int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, v
     return RNNL_ERR_INVALID;
   }
   const int64_t n = (int64_t)r->d.n_nodes * 16;
+  unsigned char *out = static_cast<unsigned char *>(node_w);
+  if (agg == RNNL_AGG_SUM)
+    RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * kStrideSum, 0, 8, (hipStream_t)stream));
   if (n == 0) return RNNL_OK;
   const int bs = 256;
   hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, (hipStream_t)stream,
-                     r->d, emb, ld, agg, static_cast<unsigned char *>(node_w));
+                     r->d, emb, ld, agg, out);
+  if (agg == RNNL_AGG_SUM)
+    hipLaunchKernelGGL(node_fix_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 4096)), dim3(bs), 0,
+                       (hipStream_t)stream, r->d.n_nodes, out);
   RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_node_weights_size(rnnl_rules r, int32_t agg, size_t *bytes) {
+  if (!r || !bytes || (agg != RNNL_AGG_SUM && agg != RNNL_AGG_PNA)) {
+    set_error("rnnl_node_weights_size: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = (size_t)r->d.n_nodes * (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna) + 64;
   return RNNL_OK;
 }
 
@@ -1137,7 +1397,18 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
   if (pp->aggregator == RNNL_AGG_SUM) {
     hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
-    hipLaunchKernelGGL(score_kernel<RNNL_AGG_SUM>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
+    // staged path while the largest head's leaves fit the LDS budget
+    const int64_t base_lds = (int64_t)(WL<RNNL_AGG_SUM>::N + 128) * 4;
+    const int64_t stage = sum_stage_bytes(r->d.max_leaves, r->d.max_head_nodes);
+    const unsigned sgrid = (unsigned)std::min<int64_t>((nq + QCHUNK - 1) / QCHUNK, (int64_t)NUM_CU * RNNL_SCORE_WG_PER_CU);
+#ifndef RNNL_STAGE_LIMIT
+#define RNNL_STAGE_LIMIT 0  // staging measured slower (lower occupancy); kept for A/B
+#endif
+    if (base_lds + stage <= RNNL_STAGE_LIMIT)
+      hipLaunchKernelGGL(score_sum_kernel<true>, dim3(sgrid), dim3(BS), (size_t)(base_lds + stage), st, p,
+                         (const float *)W);
+    else
+      hipLaunchKernelGGL(score_sum_kernel<false>, dim3(sgrid), dim3(BS), (size_t)base_lds, st, p, (const float *)W);
   } else {
     hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
     hipLaunchKernelGGL(score_kernel<RNNL_AGG_PNA>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);

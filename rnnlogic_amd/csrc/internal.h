@@ -39,11 +39,16 @@ struct RulesDev {
   const int32_t *node_rule_ptr = nullptr;  // n_nodes + 1
   const int32_t *node_rules = nullptr;     // member rule ids, ascending
   const uint64_t *node_fp = nullptr;       // sum of mix64(rule id) of members (digest only)
+  // leaves (nodes where >= 1 rule ends), numbered per head for LDS staging
+  int32_t max_leaves = 0, max_head_nodes = 0;
+  const int32_t *head_leaf_ptr = nullptr;   // R + 1
+  const int32_t *head_leaf_node = nullptr;  // leaf node ids, head-major, ascending node id
+  const int32_t *node_leaf = nullptr;       // n_nodes: local leaf index within its head, -1 if none
 };
 
 // Node-weight records (bytes per node); see rnnl_node_weights.
 constexpr int kHidden = 16;
-constexpr int kStrideSum = 128;  // int64 fix(sum x)[16]
+constexpr int kStrideSum = 64;   // f32 sum x[16]
 constexpr int kStridePna = 384;  // int64 fix(sum x)[16] | int64 fix(sum x^2)[16] | f32 min[16] | f32 max[16]
 constexpr int kFixShift = 28;    // fix(v) = round(v * 2^28)
 
@@ -61,7 +66,7 @@ struct rnnl_rules_s {
   rnnl::RulesDev d;
   int device = 0;
   int32_t R = 0, E = 0;
-  void *mem[11] = {};
+  void *mem[16] = {};
   std::vector<int32_t> node_of_rule;  // host: trie node where each rule's body ends
 };
 

@@ -247,8 +247,9 @@ class PredictorPlus(torch.nn.Module):
         with torch.no_grad():
             emb = self.all_rule_embeddings().detach().float().contiguous()
         agg = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
-        nbytes = nr.record_bytes[agg] * max(nr.n_nodes, 1)
-        w = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        nbytes = ctypes.c_size_t()
+        _native.call("rnnl_node_weights_size", nr.ptr, agg, ctypes.byref(nbytes))
+        w = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
         _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg, w.data_ptr(),
                      torch.cuda.current_stream(device).cuda_stream)
         self._node_cache[device] = (key, w, emb)
