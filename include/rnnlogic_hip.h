@@ -91,6 +91,16 @@ int rnnl_node_weights(rnnl_rules r, const float *rule_emb, int32_t ld, int32_t a
                       void *stream);
 int rnnl_node_weights_size(rnnl_rules r, int32_t aggregator, size_t *bytes);
 
+/* Rule encoder (reference src/predictors.py:201-208, type 'lstm'): for each
+ * rule, the top-layer output of torch.nn.LSTM(16, 16, layers) at its last
+ * non-pad token.  vocab: (R+1) x 16 (vocab_emb.weight); w_ih / w_hh:
+ * layers x 64 x 16 and b_ih / b_hh: layers x 64 (rnn.weight_ih_l{k} ...,
+ * torch gate order i, f, g, o); tokens: n_rules x seq_len int32 padded with
+ * `pad`; out: n_rules rows of ld_out floats. */
+int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, const float *b_ih, const float *b_hh,
+                     int32_t layers, int32_t hidden, const int32_t *tokens, int32_t n_rules, int32_t seq_len,
+                     int32_t pad, float *out, int32_t ld_out, void *stream);
+
 /* ------------------------------------------------------------- forward --
  * Replaces the body of PredictorPlus.forward (reference
  * src/predictors.py:210-271) for n_queries rows — one reference batch, or

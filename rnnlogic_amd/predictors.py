@@ -230,10 +230,33 @@ class PredictorPlus(torch.nn.Module):
         return [self.vocab_emb.weight] + list(self.rnn.parameters())
 
     def all_rule_embeddings(self):
-        """(num_rules, 16) embeddings of every rule, in rule-id order."""
+        """(num_rules, 16) embeddings of every rule, in rule-id order.  For
+        type 'lstm' without autograd this is the fused HIP encoder
+        (rnnl_lstm_encode); otherwise the torch modules."""
         if self.type == "emb":
             return self.rule_emb
-        return self.encode_rules(self.rule_features.to(self.vocab_emb.weight.device))
+        device = self.vocab_emb.weight.device
+        if self.type == "lstm" and device.type == "cuda" and not self._needs_grad():
+            return self._encode_rules_hip(device)
+        return self.encode_rules(self.rule_features.to(device))
+
+    def _encode_rules_hip(self, device):
+        L = self.num_layers
+        rnn = self.rnn
+        cat = lambda name: torch.stack([getattr(rnn, "%s_l%d" % (name, k)).detach().float()  # noqa: E731
+                                        for k in range(L)]).contiguous()
+        w_ih, w_hh, b_ih, b_hh = cat("weight_ih"), cat("weight_hh"), cat("bias_ih"), cat("bias_hh")
+        vocab = self.vocab_emb.weight.detach().float().contiguous()
+        key = (self._device_index(device), "tok")
+        tok = self._node_cache.get(key)
+        if tok is None:
+            tok = self.rule_features.to(device=device, dtype=torch.int32).contiguous()
+            self._node_cache[key] = tok
+        out = torch.empty((self.num_rules, self.hidden_dim), dtype=torch.float32, device=device)
+        _native.call("rnnl_lstm_encode", vocab.data_ptr(), w_ih.data_ptr(), w_hh.data_ptr(), b_ih.data_ptr(),
+                     b_hh.data_ptr(), L, self.hidden_dim, tok.data_ptr(), self.num_rules, tok.size(1),
+                     self.padding_index, out.data_ptr(), out.stride(0), torch.cuda.current_stream(device).cuda_stream)
+        return out
 
     def node_weights(self, device):
         """Per-trie-node aggregates of the rule embeddings (HIP), cached until a

@@ -240,3 +240,21 @@ def test_rotate_scores_vs_float64(source, mode, dev):
         assert err <= bound, (err, bound)
         return
     assert err <= TOL, "%s/%s: max |score - f64| = %g" % (source, mode, err)
+
+
+@pytest.mark.parametrize("data", ["umls", "kinship", "FB15k-237", "wn18rr"])
+def test_lstm_encoder_matches_torch(data, dev):
+    """rnnl_lstm_encode == PredictorPlus.encode_rules (torch LSTM) for every rule."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph
+    from rnnlogic_amd.predictors import PredictorPlus
+    torch.manual_seed(3)
+    graph = graph_for(datasets.materialize(data))
+    model = PredictorPlus(graph, type="lstm", num_layers=3, hidden_dim=16)
+    model.set_rules(datasets.rule_file(data))
+    model = model.to(dev).eval()
+    with torch.no_grad():
+        want = model.encode_rules(model.rule_features.to(dev))
+        got = model._encode_rules_hip(dev)
+    err = float((got - want).abs().max())
+    assert err <= 2e-6, err
