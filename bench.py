@@ -181,6 +181,15 @@ def main():
         clock_ghz = 0.1 * ticks / max(real, 1)
         del tmp
 
+    # HBM traffic per launch from the committed PMC summary of this workload
+    # (tools/pmc_traffic.py; bench.py cannot read counters itself)
+    traffic = {}
+    tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % args.feature.lower())
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        traffic = {k.split("::")[-1].split("<")[0]: v["bytes"] for k, v in tj.get("kernels", {}).items()}
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -195,9 +204,11 @@ def main():
     D = model.RotatE.emb_dim if args.feature == "RotatE" else 0
     rotate_flops = 7.0 * nq * E * D
     rotate_bytes = 8.0 * D * E * ((nq + 15) // 16) + 8.0 * D * nq + 4.0 * nq * E
+    gt = [traffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_kernel")]
+    gt = sum(x for x in gt if x) or None
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-              "traffic": None, "kernel": "predictorplus_kernel", "ms": round(ground_ms, 3),
+              "traffic": gt, "kernel": "ground_kernel + score_kernel", "ms": round(ground_ms, 3),
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
     if args.feature == "RotatE":
         ach = rotate_flops / (base_ms * 1e-3) / 1e12
@@ -211,7 +222,8 @@ def main():
         cyc = base_ms * 1e-3 * ghz * 1e9 * 1024 / (nq * E * D / 64.0)
         floor = 19.1 if mode == "direct" else 13.1
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": None, "kernel": "rotate_%s_kernel" % mode,
+                "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": traffic.get("rotate_%s_kernel" % mode),
+                "kernel": "rotate_%s_kernel" % mode,
                 "ms": round(base_ms, 3), "alg_flops": rotate_flops,
                 "valu_issue": {"cycles_per_64_terms": round(cyc, 2), "floor": floor, "frac": round(floor / cyc, 3),
                                "clock_ghz": round(ghz, 3), "clock": "measured in-kernel" if clock_ghz else "nominal"},
@@ -241,8 +253,8 @@ def main():
                                   model.num_rules, " and RotatE tables" if args.feature == "RotatE" else ""),
                    "batch_size": 32, "parallelism": "dp%d (queries sharded, KG replicated)" % world},
         "roofline": dominant,
-        "kernels_ms": {"node_weights+lstm": round(nodes_ms, 3), "base_score": round(base_ms, 3),
-                       "predictorplus_kernel": round(ground_ms, 3)},
+        "kernels_ms": {"rule_encoder+node_weights": round(nodes_ms, 3), "base_score": round(base_ms, 3),
+                       "ground+score": round(ground_ms, 3)},
         "roofline_grounding": ground,
     }
     if not args.no_cpu_baseline and world == 1:
