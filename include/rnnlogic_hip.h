@@ -75,6 +75,10 @@ int rnnl_rules_info(rnnl_rules r, int32_t *info5);
  * rules share a node when one body is a prefix-equal duplicate; node ids are
  * those of the grounding COO (rnnl_ground_export_entries). */
 int rnnl_rules_node_of_rule(rnnl_rules r, int32_t *node_of_rule);
+/* host out: head_root (R) = the trie root node of each head relation (-1:
+ * no rule), *max_head_nodes = the largest trie (the row stride `ld` of
+ * rnnl_predictor_rule_stats). */
+int rnnl_rules_head_roots(rnnl_rules r, int32_t *head_root, int32_t *max_head_nodes);
 
 /* Per-node aggregate of rule embeddings (device): rule_emb is n_rules x H
  * (row stride `ld` floats), H == 16.  Writes node_w: n_nodes records of
@@ -169,6 +173,40 @@ int rnnl_debug_profile(void *dev_counters);
  * 100 MHz real-time ticks) of every block into dev_counters (2 x uint64); the
  * ratio x 0.1 GHz is the effective shader clock under that kernel's load. */
 int rnnl_debug_clock(void *dev_counters);
+
+/* ------------------------------------------------------- EM Predictor --
+ * The EM loop's rule-weight predictor (reference src/predictors.py:17-119,
+ * Predictor.forward / compute_H; run_rnnlogic.py:72-83).
+ *
+ * rnnl_linear_node_weights: per trie node, the sum of its rules' weights
+ * (rule_weights: n_rules floats, fp64 sum) as int32 fixed point with one
+ * shift for the table (trailer after the n_nodes values); buffer size from
+ * rnnl_linear_node_weights_size.  Replaces the per-rule `x * rule_weights[i]`
+ * products of predictors.py:62-66: rules ending at one node share its counts.
+ *
+ * rnnl_predictor_forward: grounding (as rnnl_ground, with the batch's edge
+ * removal) + score[q, t] (+)= sum over the candidate's (node, count) entries
+ * of count x node weight, exact int64 sums.  feature RNNL_FEATURE_ADD adds
+ * into pre-filled bias rows (rnnl_fill_rows; predictors.py:73-75),
+ * RNNL_FEATURE_NONE writes candidates into -inf-filled rows and sets mask
+ * (predictors.py:76-78).  The whole-batch early return (predictors.py:68-72)
+ * is the caller's (it needs the batch boundaries).
+ *
+ * rnnl_predictor_rule_stats: after rnnl_ground / rnnl_predictor_forward on
+ * the same workspace, per row q and per node k of its head's trie (local
+ * index node - root < ld, ld >= max_head_nodes): pos[q*ld + k] = path count
+ * of node k at all_t[q], tot[q*ld + k] = its sum over all candidates.  The
+ * caller zero-fills pos.  compute_H's pos_score / neg_score
+ * (predictors.py:106-113) are w x pos and w x tot / n_cand. */
+int rnnl_linear_node_weights_size(rnnl_rules r, size_t *bytes);
+int rnnl_linear_node_weights(rnnl_rules r, const float *rule_weights, int32_t n_rules, void *node_w, void *stream);
+int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32_t feature, const int64_t *all_h,
+                           const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries, float *score,
+                           uint8_t *mask, int32_t *n_cand, void *workspace, size_t workspace_bytes,
+                           int32_t capacity_scale, void *stream);
+int rnnl_predictor_rule_stats(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
+                              rnnl_rules r, const int64_t *all_r, const int64_t *all_t, int32_t ld, int64_t *pos,
+                              int64_t *tot, void *stream);
 
 /* --------------------------------------------------------- entity feature --
  * Base-score fills (reference src/predictors.py:260-269). */

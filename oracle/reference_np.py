@@ -15,6 +15,8 @@ Reference anchors (file:line in /root/reference):
   make_*_batches        src/data.py:186-196, 232-238, 269-275 (python `random` call order)
   lstm_encode           src/predictors.py:201-208 (3-layer LSTM, output at last non-pad token)
   predictorplus_forward src/predictors.py:210-271
+  predictor_forward     src/predictors.py:53-80   (EM rule-weight Predictor)
+  predictor_compute_H   src/predictors.py:82-119
   func_to_node_sum      src/layers.py:63-77
   func_to_node_pna      src/layers.py:89-126
   mlp                   src/layers.py:35-51
@@ -289,6 +291,59 @@ def predictorplus_forward(sd, cfg, g, rules, h, r, edges_to_remove, rotate=None)
         return score + rotate_forward(*rotate, h, r), np.ones((B, E), bool)
     m = mask != 0
     return np.where(m, score, -np.inf).astype(np.float32), m
+
+
+def predictor_forward(sd, feature, g, rules, h, r, edges_to_remove):
+    """Predictor.forward (predictors.py:53-80) -> (score (B,|E|) f32, mask bool):
+    score = sum over the relation's rules, in rule order, of count * weight (fp32)."""
+    h = np.asarray(h, dtype=np.int64)
+    r = np.asarray(r, dtype=np.int64)
+    q = int(r[0])
+    assert (r != q).sum() == 0
+    B, E = len(h), g.entity_size
+    w = sd["rule_weights"].astype(np.float32)
+    score = np.zeros((B, E), np.float32)
+    mask = np.zeros((B, E), np.float32)
+    for i, (hd, body) in rules.relation2rules[q]:
+        x = grounding(g, h, hd, body, edges_to_remove)
+        score += x.astype(np.float32) * w[i]
+        mask += x
+    if mask.sum() == 0:
+        if feature == "bias":
+            return mask + sd["bias"][None], (1 - mask).astype(bool)
+        return mask - float("-inf"), mask.astype(bool)
+    if feature == "bias":
+        return score + sd["bias"][None], np.ones((B, E), bool)
+    m = mask != 0
+    return np.where(m, score, -np.inf).astype(np.float32), m
+
+
+def predictor_compute_H(sd, g, rules, h, r, t, edges_to_remove):
+    """Predictor.compute_H (predictors.py:82-119) -> (H (R_q,) f32, rule index) or (None, None):
+    per row, pos = count at t times w, neg = sum over candidates of count times w
+    divided by the candidate count; softmax over the rules, summed over rows."""
+    h = np.asarray(h, dtype=np.int64)
+    r = np.asarray(r, dtype=np.int64)
+    t = np.asarray(t, dtype=np.int64)
+    q = int(r[0])
+    B, E = len(h), g.entity_size
+    w = sd["rule_weights"].astype(np.float32)
+    scores, index = [], []
+    mask = np.zeros((B, E), np.float32)
+    for i, (hd, body) in rules.relation2rules[q]:
+        x = grounding(g, h, hd, body, edges_to_remove)
+        scores.append(x.astype(np.float32) * w[i])
+        index.append(i)
+        mask += x
+    if not scores:
+        return None, None
+    neg = mask != 0
+    nneg = np.maximum(neg.sum(1), 1).astype(np.float32)
+    rows = np.arange(B)
+    Hs = np.stack([s[rows, t] - (s * neg).sum(1, dtype=np.float32) / nneg for s in scores], -1)
+    Hs = Hs - Hs.max(-1, keepdims=True)
+    e = np.exp(Hs.astype(np.float64))
+    return (e / e.sum(-1, keepdims=True)).sum(0).astype(np.float32), np.asarray(index, dtype=np.int64)
 
 
 # --------------------------------------------------------------------------- evaluation

@@ -34,6 +34,7 @@ SIGNATURES = [
     ("rnnl_rules_destroy", ctypes.c_int, [_P]),
     ("rnnl_rules_info", ctypes.c_int, [_P, _P]),
     ("rnnl_rules_node_of_rule", ctypes.c_int, [_P, _P]),
+    ("rnnl_rules_head_roots", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P]),
     ("rnnl_node_weights_size", ctypes.c_int, [_P, _I32, _P]),
     ("rnnl_lstm_encode", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _I32, _P]),
@@ -44,6 +45,11 @@ SIGNATURES = [
     ("rnnl_ground", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_ground_export_candidates", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_ground_export_entries", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
+    ("rnnl_linear_node_weights_size", ctypes.c_int, [_P, _P]),
+    ("rnnl_linear_node_weights", ctypes.c_int, [_P, _P, _I32, _P, _P]),
+    ("rnnl_predictor_forward", ctypes.c_int,
+     [_P, _P, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
+    ("rnnl_predictor_rule_stats", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_debug_clock", ctypes.c_int, [_P]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),

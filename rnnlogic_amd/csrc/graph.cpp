@@ -229,6 +229,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   rs->d.max_depth = max_depth;
   rs->d.n_heads = R;
   rs->node_of_rule = std::move(node_of_rule);
+  rs->head_root = head_root;
   rs->d.max_leaves = max_leaves;
   rs->d.max_head_nodes = max_head_nodes;
   int rc = RNNL_OK;
@@ -266,6 +267,16 @@ int rnnl_rules_node_of_rule(rnnl_rules r, int32_t *node_of_rule) {
     return RNNL_ERR_INVALID;
   }
   std::copy(r->node_of_rule.begin(), r->node_of_rule.end(), node_of_rule);
+  return RNNL_OK;
+}
+
+int rnnl_rules_head_roots(rnnl_rules r, int32_t *head_root, int32_t *max_head_nodes) {
+  if (!r || !head_root || !max_head_nodes) {
+    set_error("rnnl_rules_head_roots: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  std::copy(r->head_root.begin(), r->head_root.end(), head_root);
+  *max_head_nodes = r->d.max_head_nodes;
   return RNNL_OK;
 }
 

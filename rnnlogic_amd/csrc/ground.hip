@@ -1270,6 +1270,101 @@ __global__ void node_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
   }
 }
 
+// ---------------------------------------------------------------- EM Predictor (a12)
+// Predictor.forward (reference src/predictors.py:53-80): score = sum over the
+// relation's rules of path count x rule weight.  Rules ending at the same trie
+// node have identical counts, so the grounding COO's (node, count) entries
+// need one scalar per node: the sum of its rules' weights.  As for the SUM
+// records, that is int32 fixed point with one shift for the table, so the
+// per-candidate int64 sum of count x fix is exact and independent of the
+// order of the entries.  Layout: int32 fix[n_nodes], then (at
+// lin_trailer_off) u32 max|sum| bits, i32 shift.
+__host__ __device__ inline int64_t lin_trailer_off(int n_nodes) { return ((int64_t)n_nodes * 4 + 15) & ~int64_t(15); }
+
+__global__ void lin_node_kernel(RulesDev rl, const float *__restrict__ w, unsigned char *__restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= rl.n_nodes) return;
+  double s = 0.0;
+  for (int k = rl.node_rule_ptr[n]; k < rl.node_rule_ptr[n + 1]; ++k) s += (double)w[rl.node_rules[k]];
+  const float f = (float)s;
+  reinterpret_cast<float *>(out)[n] = f;
+  atomicMax(reinterpret_cast<unsigned int *>(out + lin_trailer_off(rl.n_nodes)), __float_as_uint(fabsf(f)));
+}
+
+__global__ void lin_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
+  unsigned int *trailer = reinterpret_cast<unsigned int *>(out + lin_trailer_off(n_nodes));
+  const float mx = __uint_as_float(trailer[0]);
+  int e = 0;
+  if (mx > 0.f) frexpf(mx, &e);  // mx < 2^e
+  const int shift = min(max(30 - e, 0), 60);
+  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = (unsigned)shift;
+  const float sc = ldexpf(1.f, min(shift, 120));
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_nodes; i += gridDim.x * blockDim.x) {
+    const float f = reinterpret_cast<float *>(out)[i];
+    reinterpret_cast<int *>(out)[i] = (int)rintf(f * sc);
+  }
+}
+
+// One workgroup per query (grid-stride), one lane per candidate: the
+// candidate's exact sum, added into the pre-filled bias row (entity_feature
+// 'bias') or written (otherwise; the rows were pre-filled with -inf).
+__global__ __launch_bounds__(BS) void score_linear_kernel(KParams p, const int *__restrict__ fix) {
+  const int shift = (int)reinterpret_cast<const unsigned int *>(reinterpret_cast<const unsigned char *>(fix) +
+                                                                lin_trailer_off(p.rl.n_nodes))[1];
+  const double inv = ldexp(1.0, -shift);
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    const int nc = p.n_cand[q];
+    if (nc <= 0) continue;
+    const int64_t qb = p.q_base[q];
+    for (int s = threadIdx.x; s < nc; s += BS) {
+      const int t = p.c_t[qb + s];
+      const int beg = p.c_beg[qb + s], cnt = p.c_cnt[qb + s];
+      long long acc = 0;
+      for (int e = beg; e < beg + cnt; ++e) acc += (long long)p.b_cnt[e] * fix[p.b_node[e]];
+      const float out = (float)((double)acc * inv);
+      const int64_t idx = (int64_t)q * p.g.E + t;
+      if (p.feature == RNNL_FEATURE_NONE)
+        p.score[idx] = out;
+      else
+        p.score[idx] = out + p.score[idx];
+      if (p.mask) p.mask[idx] = 1;
+    }
+  }
+}
+
+// Predictor.compute_H (src/predictors.py:82-119) needs, per (row, rule):
+// the path count at the row's true tail and the total over all candidates.
+// Both only depend on the rule's trie node: per row, for every node of the
+// head's trie (local index node - root < ld), pos = count at all_t[q] and
+// tot = sum over candidates.  One workgroup per row; tot is summed in LDS.
+__global__ __launch_bounds__(BS) void rule_stats_kernel(KParams p, const int64_t *__restrict__ all_t, int ld,
+                                                        long long *__restrict__ pos, long long *__restrict__ tot) {
+  extern __shared__ unsigned long long s_tot[];
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    const int nc = p.n_cand[q];
+    if (nc <= 0) continue;
+    const int r = (int)p.all_r[q];
+    const int root = p.rl.head_root[r], nh = min(p.rl.head_nodes[r], ld);
+    for (int i = threadIdx.x; i < nh; i += BS) s_tot[i] = 0ull;
+    __syncthreads();
+    const int64_t qb = p.q_base[q];
+    const int tq = (int)all_t[q];
+    for (int s = threadIdx.x; s < nc; s += BS) {
+      const int t = p.c_t[qb + s];
+      const int beg = p.c_beg[qb + s], cnt = p.c_cnt[qb + s];
+      for (int e = beg; e < beg + cnt; ++e) {
+        const int k = p.b_node[e] - root;
+        const unsigned long long c = p.b_cnt[e];
+        atomicAdd(&s_tot[k], c);
+        if (t == tq) pos[(int64_t)q * ld + k] += (long long)c;  // one lane owns the true tail
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nh; i += BS) tot[(int64_t)q * ld + i] = (long long)s_tot[i];
+    __syncthreads();
+  }
+}
+
 }  // namespace rnnl
 
 using namespace rnnl;
@@ -1469,6 +1564,80 @@ int rnnl_ground_export_entries(void *ws, int32_t nq, int32_t scale, const int32_
   const KParams p = export_params(ws, nq, scale, n_cand);
   hipLaunchKernelGGL(export_entries_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0,
                      (hipStream_t)stream, p, ent_off, out_node, out_count);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_linear_node_weights_size(rnnl_rules r, size_t *bytes) {
+  if (!r || !bytes) {
+    set_error("rnnl_linear_node_weights_size: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = (size_t)(lin_trailer_off(r->d.n_nodes) + 64);
+  return RNNL_OK;
+}
+
+int rnnl_linear_node_weights(rnnl_rules r, const float *rule_weights, int32_t n_rules, void *node_w, void *stream) {
+  if (!r || !rule_weights || !node_w || n_rules != r->d.n_rules) {
+    set_error("rnnl_linear_node_weights: bad arguments (rule_weights must hold n_rules floats)");
+    return RNNL_ERR_INVALID;
+  }
+  unsigned char *out = static_cast<unsigned char *>(node_w);
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(out + lin_trailer_off(r->d.n_nodes), 0, 8, st));
+  const int n = r->d.n_nodes;
+  if (n == 0) return RNNL_OK;
+  hipLaunchKernelGGL(lin_node_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, r->d, rule_weights, out);
+  hipLaunchKernelGGL(lin_fix_kernel, dim3((unsigned)std::min((n + 255) / 256, 1024)), dim3(256), 0, st, n, out);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32_t feature, const int64_t *all_h,
+                           const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
+                           int32_t *n_cand, void *ws, size_t ws_bytes, int32_t scale, void *stream) {
+  if (!node_w || !score || (feature != RNNL_FEATURE_ADD && feature != RNNL_FEATURE_NONE)) {
+    set_error("rnnl_predictor_forward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p;
+  if (int rc = setup_params("rnnl_predictor_forward", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale, p))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  p.agg = RNNL_AGG_SUM;
+  p.feature = feature;
+  p.score = score;
+  p.mask = mask;
+  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+  hipLaunchKernelGGL(score_linear_kernel, dim3((unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8)), dim3(BS), 0, st,
+                     p, static_cast<const int *>(node_w));
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictor_rule_stats(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand, rnnl_rules r,
+                              const int64_t *all_r, const int64_t *all_t, int32_t ld, int64_t *pos, int64_t *tot,
+                              void *stream) {
+  if (!ws || nq < 0 || scale < 1 || !n_cand || !r || !all_r || !all_t || !pos || !tot ||
+      ld < r->d.max_head_nodes || ld < 1) {
+    set_error("rnnl_predictor_rule_stats: bad arguments (ld >= max_head_nodes)");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  if ((int64_t)ld * 8 > 64 * 1024) {
+    set_error("rnnl_predictor_rule_stats: head trie too large for the LDS table");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p = export_params(ws, nq, scale, n_cand);
+  p.rl = r->d;
+  p.all_r = all_r;
+  const Layout Ly = make_layout(nq, scale);
+  p.c_beg = reinterpret_cast<int32_t *>(static_cast<unsigned char *>(ws) + Ly.off_cbeg);
+  hipLaunchKernelGGL(rule_stats_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(BS), (size_t)ld * 8,
+                     (hipStream_t)stream, p, all_t, ld, reinterpret_cast<long long *>(pos),
+                     reinterpret_cast<long long *>(tot));
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -68,6 +68,7 @@ struct rnnl_rules_s {
   int32_t R = 0, E = 0;
   void *mem[16] = {};
   std::vector<int32_t> node_of_rule;  // host: trie node where each rule's body ends
+  std::vector<int32_t> head_root;     // host copy of d.head_root (R)
 };
 
 #define RNNL_HIP_CHECK(expr)                                                              \

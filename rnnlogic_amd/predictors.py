@@ -10,6 +10,12 @@ the HIP path:
     base score  bias row / RotatE / -inf   rnnl_fill_rows / rnnl_rotate_score (HIP)
     grounding + aggregation + MLP          rnnl_predictorplus_forward (HIP, one launch)
 
+Predictor (the EM loop's rule-weight model) runs on the same grounding:
+score = exact fixed-point sums of count x per-node rule-weight sums
+(rnnl_predictor_forward), compute_H from per-node path statistics
+(rnnl_predictor_rule_stats).  Training forwards of both run torch autograd on
+the exported grounding COO.
+
 There is no CPU fallback: on a CPU tensor forward() raises.
 """
 import ctypes
@@ -71,11 +77,119 @@ class _NativeRules(object):
         return self.handle.ptr
 
 
-class Predictor(torch.nn.Module):
+class _HipGrounding(object):
+    """Grounding plumbing shared by Predictor and PredictorPlus: the per-device
+    rules handle (prefix tries), the forward workspace with its overflow retry,
+    and the grounding COO export.  Needs self.graph, self.rules,
+    self._native_rules, self._ws and self.capacity_scale."""
+
+    def _device_index(self, device):
+        return device.index if device.index is not None else torch.cuda.current_device()
+
+    def native_rules(self, device):
+        key = self._device_index(device)
+        if key not in self._native_rules:
+            self._native_rules[key] = _NativeRules(self.graph, self.rules, key)
+        return self._native_rules[key]
+
+    def _workspace(self, device, nq, scale):
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        need = ctypes.c_size_t()
+        _native.call("rnnl_forward_workspace_size", g, nr.ptr, nq, scale, ctypes.byref(need))
+        ws = self._ws.get(device)
+        if ws is None or ws.numel() < need.value:
+            ws = torch.empty(need.value, dtype=torch.uint8, device=device)
+            self._ws[device] = ws
+        return ws
+
+    @staticmethod
+    def _rows(all_h, all_r, edges_to_remove):
+        device = all_h.device
+        if device.type != "cuda":
+            raise RuntimeError("the predictors run on the HIP path: move inputs and model to a GPU")
+        all_h = all_h.to(torch.int64).contiguous()
+        all_r = all_r.to(device, torch.int64).contiguous()
+        etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
+        return device, all_h, all_r, etr
+
+    def _launch(self, device, nq, run):
+        """run(ws, scale) launches onto the workspace; retried with a doubled
+        capacity_scale while the launch reports overflow.  Returns (ws, scale)."""
+        stream = torch.cuda.current_stream(device).cuda_stream
+        while True:
+            scale = self.capacity_scale
+            ws = self._workspace(device, nq, scale)
+            run(ws, scale)
+            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
+            if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
+                self.capacity_scale *= 2
+                logging.info("%s: workspace overflow, capacity_scale -> %d", type(self).__name__,
+                             self.capacity_scale)
+                continue
+            _native.check(rc)
+            return ws, scale
+
+    def ground(self, all_h, all_r, edges_to_remove=None):
+        """Grounding of every rule of every row into the workspace (HIP
+        rnnl_ground).  Returns (ws, scale, n_cand (n,) int32)."""
+        device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
+        nq = all_h.numel()
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+
+        def run(ws, scale):
+            _native.call("rnnl_ground", g, nr.ptr, all_h.data_ptr(), all_r.data_ptr(),
+                         etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
+                         ws.numel(), scale, stream)
+        ws, scale = self._launch(device, nq, run)
+        return ws, scale, n_cand
+
+    def ground_coo(self, all_h, all_r, edges_to_remove=None):
+        """The grounding of every rule of every row as the COO of the
+        reference's stacked rule_count matrix (HIP: rnnl_ground + export).
+
+        Returns (row (C,), entity (C,), cand_of_entry (P,), node (P,), count (P,))
+        int64 device tensors: candidates in row-major order (= the reference's
+        nonzero order, predictors.py:239) and, per candidate, its (trie node,
+        path count) entries; node ids index `native_rules(device).node_of_rule`."""
+        device = all_h.device
+        nq = all_h.numel()
+        ws, scale, n_cand = self.ground(all_h, all_r, edges_to_remove)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        nc = n_cand.to(torch.int64)
+        cand_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
+        torch.cumsum(nc, 0, out=cand_off[1:])
+        C = int(cand_off[-1].item())
+        ent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
+        nent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
+        _native.call("rnnl_ground_export_candidates", ws.data_ptr(), nq, scale, n_cand.data_ptr(),
+                     cand_off.data_ptr(), ent.data_ptr(), nent.data_ptr(), stream)
+        ent, nent = ent[:C].to(torch.int64), nent[:C].to(torch.int64)
+        row = torch.repeat_interleave(torch.arange(nq, device=device), nc)
+        per_row = torch.zeros(nq, dtype=torch.int64, device=device).index_add_(0, row, nent)
+        ent_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
+        torch.cumsum(per_row, 0, out=ent_off[1:])
+        P = int(ent_off[-1].item())
+        node = torch.empty(max(P, 1), dtype=torch.int32, device=device)
+        count = torch.empty(max(P, 1), dtype=torch.int32, device=device)
+        _native.call("rnnl_ground_export_entries", ws.data_ptr(), nq, scale, n_cand.data_ptr(), ent_off.data_ptr(),
+                     node.data_ptr(), count.data_ptr(), stream)
+        cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent)
+        return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64)
+
+    def _needs_grad(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
+
+class Predictor(_HipGrounding, torch.nn.Module):
     """Rule-weight predictor of the EM loop (reference src/predictors.py:17-119).
 
-    score = sum_rho count_rho * w_rho (+ bias).  Grounds through
-    KnowledgeGraph.grounding (torch ops on the batch's device)."""
+    score = sum over the relation's rules of path count x rule weight
+    (+ bias).  Eval forwards run the HIP grounding and an exact fixed-point
+    per-candidate sum (rnnl_predictor_forward); compute_H reads per-node path
+    statistics from the same grounding (rnnl_predictor_rule_stats); training
+    forwards are torch autograd on the grounding COO.  No CPU fallback."""
 
     def __init__(self, graph, entity_feature="bias"):
         super(Predictor, self).__init__()
@@ -85,6 +199,11 @@ class Predictor(torch.nn.Module):
         self.entity_feature = entity_feature
         if entity_feature == "bias":
             self.bias = torch.nn.parameter.Parameter(torch.zeros(self.num_entities))
+        self._native_rules = {}
+        self._ws = {}
+        self._lin_cache = {}
+        self._roots = {}
+        self.capacity_scale = 1
 
     def set_rules(self, input):
         self.rules = _read_rules(input)
@@ -95,53 +214,136 @@ class Predictor(torch.nn.Module):
         for index, rule in enumerate(self.rules):
             self.relation2rules[rule[0]].append([index, rule])
         self.rule_weights = torch.nn.parameter.Parameter(torch.zeros(self.num_rules))
+        self._native_rules = {}
+        self._lin_cache = {}
+        self._roots = {}
 
-    def _counts(self, all_h, all_r, edges_to_remove):
+    # ------------------------------------------------------------------ native plumbing
+    def node_weights(self, device):
+        """Per-trie-node sums of the rule weights (HIP, int32 fixed point),
+        cached until rule_weights changes."""
+        nr = self.native_rules(device)
+        key = (self._device_index(device), self.rule_weights.data_ptr(), self.rule_weights._version)
+        hit = self._lin_cache.get(device)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        w = self.rule_weights.detach().float().contiguous()
+        nbytes = ctypes.c_size_t()
+        _native.call("rnnl_linear_node_weights_size", nr.ptr, ctypes.byref(nbytes))
+        out = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+        _native.call("rnnl_linear_node_weights", nr.ptr, w.data_ptr(), self.num_rules, out.data_ptr(),
+                     torch.cuda.current_stream(device).cuda_stream)
+        self._lin_cache[device] = (key, out, w)
+        return out
+
+    def head_roots(self, device):
+        key = self._device_index(device)
+        if key not in self._roots:
+            nr = self.native_rules(device)
+            roots = (ctypes.c_int32 * max(self.num_relations, 1))()
+            mh = ctypes.c_int32()
+            _native.call("rnnl_rules_head_roots", nr.ptr, roots, ctypes.byref(mh))
+            self._roots[key] = (list(roots)[:self.num_relations], max(int(mh.value), 1))
+        return self._roots[key]
+
+    def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False):
+        """Forward for any rows (one or many reference batches, mixed
+        relations): (score (n, |E|) f32, mask (n, |E|) bool[, n_cand])."""
+        device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
+        nq, E = all_h.numel(), self.num_entities
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        node_w = self.node_weights(device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        bias_mode = self.entity_feature == "bias"
+        feature = _native.FEATURE_ADD if bias_mode else _native.FEATURE_NONE
+        score = torch.empty((nq, E), dtype=torch.float32, device=device)
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        mask8 = None if bias_mode else torch.empty((nq, E), dtype=torch.uint8, device=device)
+        bias = self.bias.detach().float().contiguous() if bias_mode else None
+
+        def run(ws, scale):
+            if bias_mode:
+                _native.call("rnnl_fill_rows", bias.data_ptr(), nq, E, score.data_ptr(), stream)
+            else:
+                _native.call("rnnl_fill_value", float("-inf"), score.numel(), score.data_ptr(), stream)
+                mask8.zero_()
+            _native.call("rnnl_predictor_forward", g, nr.ptr, node_w.data_ptr(), feature, all_h.data_ptr(),
+                         all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
+                         mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(), ws.data_ptr(),
+                         ws.numel(), scale, stream)
+        self._launch(device, nq, run)
+        mask = torch.ones((nq, E), dtype=torch.bool, device=device) if bias_mode else mask8.bool()
+        return (score, mask, n_cand) if return_ncand else (score, mask)
+
+    # ------------------------------------------------------------------ reference API
+    def forward(self, all_h, all_r, edges_to_remove):
+        """predictors.py:53-80: one single-relation batch -> (score, mask)."""
         query_r = all_r[0].item()
         assert (all_r != query_r).sum() == 0
-        for index, (r_head, r_body) in self.relation2rules[query_r]:
-            assert r_head == query_r
-            yield index, self.graph.grounding(all_h, r_head, r_body, edges_to_remove)
+        if self._needs_grad():
+            return self.forward_autograd(all_h, all_r, edges_to_remove)
+        score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
+        if self.entity_feature != "bias" and int(n_cand.sum().item()) == 0:
+            # early return `mask - float('-inf')` (predictors.py:68-72): +inf, mask all False
+            score.fill_(float("inf"))
+        return score, mask
 
-    def forward(self, all_h, all_r, edges_to_remove):
-        device = all_r.device
-        score = torch.zeros(all_r.size(0), self.num_entities, device=device)
-        mask = torch.zeros(all_r.size(0), self.num_entities, device=device)
-        for index, x in self._counts(all_h, all_r, edges_to_remove):
-            score = score + x * self.rule_weights[index]
-            mask += x
-        if mask.sum().item() == 0:
+    def forward_autograd(self, all_h, all_r, edges_to_remove):
+        """Differentiable forward (training): the HIP grounding's COO, then
+        score = scatter of sum(count x node weight) with node weight = the sum
+        of its rules' rule_weights — torch autograd yields the reference's
+        gradients (predictors.py:53-80)."""
+        device = all_h.device
+        nq, E = all_h.numel(), self.num_entities
+        row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
+        C = ent.numel()
+        if C == 0:
+            zero = torch.zeros((nq, E), device=device)
             if self.entity_feature == "bias":
-                return mask + self.bias.unsqueeze(0), (1 - mask).bool()
-            return mask - float("-inf"), mask.bool()
+                return zero + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
+            return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
+        nr = self.native_rules(device)
+        w = self.rule_weights
+        node_w = torch.zeros(nr.n_nodes, device=device, dtype=w.dtype).index_add(0, nr.node_of_rule, w)
+        val = torch.zeros(C, device=device, dtype=w.dtype).index_add(0, ce, count.to(w.dtype) * node_w[node])
+        score = torch.zeros(nq * E, device=device, dtype=w.dtype).scatter(0, row * E + ent, val).view(nq, E)
         if self.entity_feature == "bias":
-            return score + self.bias.unsqueeze(0), torch.ones_like(mask).bool()
-        mask = mask != 0
+            return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
+        mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
         return score.masked_fill(~mask, float("-inf")), mask
 
+    @torch.no_grad()
     def compute_H(self, all_h, all_r, all_t, edges_to_remove):
-        """Per-rule H scores (predictors.py:82-119)."""
-        device = all_r.device
-        rule_score, rule_index = [], []
-        mask = torch.zeros(all_r.size(0), self.num_entities, device=device)
-        for index, x in self._counts(all_h, all_r, edges_to_remove):
-            rule_score.append(x * self.rule_weights[index])
-            rule_index.append(index)
-            mask += x
-        if len(rule_score) == 0:
+        """Per-rule H scores (predictors.py:82-119): per row, pos = w x count at
+        the true tail, neg = w x (sum of counts over candidates) / #candidates;
+        softmax over the relation's rules, summed over rows.  Grounding and
+        the per-node path statistics run on the HIP path."""
+        query_r = all_r[0].item()
+        assert (all_r != query_r).sum() == 0
+        device = all_h.device
+        rules = self.relation2rules[query_r]
+        if len(rules) == 0:
             return None, None
-        rule_index = torch.tensor(rule_index, dtype=torch.long, device=device)
-        pos = torch.nn.functional.one_hot(all_t, self.num_entities).bool().to(device)
-        neg = mask != 0
-        H = []
-        for s in rule_score:
-            ps = (s * pos).sum(1) / torch.clamp(pos.sum(1), min=1)
-            ns = (s * neg).sum(1) / torch.clamp(neg.sum(1), min=1)
-            H.append((ps - ns).unsqueeze(-1))
-        return torch.softmax(torch.cat(H, dim=-1), dim=-1).sum(0), rule_index
+        nq = all_h.numel()
+        ws, scale, n_cand = self.ground(all_h, all_r, edges_to_remove)
+        nr = self.native_rules(device)
+        roots, ld = self.head_roots(device)
+        all_r = all_r.to(device, torch.int64).contiguous()
+        all_t = all_t.to(device, torch.int64).contiguous()
+        pos = torch.zeros((nq, ld), dtype=torch.int64, device=device)
+        tot = torch.zeros((nq, ld), dtype=torch.int64, device=device)
+        _native.call("rnnl_predictor_rule_stats", ws.data_ptr(), nq, scale, n_cand.data_ptr(), nr.ptr,
+                     all_r.data_ptr(), all_t.data_ptr(), ld, pos.data_ptr(), tot.data_ptr(),
+                     torch.cuda.current_stream(device).cuda_stream)
+        rule_index = torch.tensor([i for i, _ in rules], dtype=torch.long, device=device)
+        k = nr.node_of_rule[rule_index] - roots[query_r]
+        w = self.rule_weights.detach()[rule_index]
+        pos_score = pos[:, k].to(w.dtype) * w
+        neg_score = tot[:, k].to(w.dtype) * w / torch.clamp(n_cand.to(w.dtype), min=1).unsqueeze(1)
+        return torch.softmax(pos_score - neg_score, dim=-1).sum(0), rule_index
 
 
-class PredictorPlus(torch.nn.Module):
+class PredictorPlus(_HipGrounding, torch.nn.Module):
     """Reference src/predictors.py:121-271, forward on the HIP path."""
 
     def __init__(self, graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="bias", aggregator="sum",
@@ -215,15 +417,6 @@ class PredictorPlus(torch.nn.Module):
         return output.gather(1, idx.view(-1, 1, 1).expand(-1, 1, self.hidden_dim)).squeeze(1)
 
     # ------------------------------------------------------------------ native plumbing
-    def _device_index(self, device):
-        return device.index if device.index is not None else torch.cuda.current_device()
-
-    def native_rules(self, device):
-        key = self._device_index(device)
-        if key not in self._native_rules:
-            self._native_rules[key] = _NativeRules(self.graph, self.rules, key)
-        return self._native_rules[key]
-
     def _embedding_sources(self):
         if self.type == "emb":
             return [self.rule_emb]
@@ -277,16 +470,6 @@ class PredictorPlus(torch.nn.Module):
                      torch.cuda.current_stream(device).cuda_stream)
         self._node_cache[device] = (key, w, emb)
         return w
-
-    def _workspace(self, device, nq, scale):
-        g, nr = self.graph.device_graph(device), self.native_rules(device)
-        need = ctypes.c_size_t()
-        _native.call("rnnl_forward_workspace_size", g, nr.ptr, nq, scale, ctypes.byref(need))
-        ws = self._ws.get(device)
-        if ws is None or ws.numel() < need.value:
-            ws = torch.empty(need.value, dtype=torch.uint8, device=device)
-            self._ws[device] = ws
-        return ws
 
     def _params(self, device, node_w):
         rte, sm = self.rule_to_entity, self.score_model
@@ -370,57 +553,6 @@ class PredictorPlus(torch.nn.Module):
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
     # ------------------------------------------------------------------ autograd (training) path
-    def ground_coo(self, all_h, all_r, edges_to_remove=None):
-        """The grounding of every rule of every row as the COO of the
-        reference's stacked rule_count matrix (HIP: rnnl_ground + export).
-
-        Returns (row (C,), entity (C,), cand_of_entry (P,), node (P,), count (P,))
-        int64 device tensors: candidates in row-major order (= the reference's
-        nonzero order, predictors.py:239) and, per candidate, its (trie node,
-        path count) entries; node ids index `native_rules(device).node_of_rule`."""
-        device = all_h.device
-        if device.type != "cuda":
-            raise RuntimeError("PredictorPlus runs on the HIP path: move inputs and model to a GPU")
-        all_h = all_h.to(torch.int64).contiguous()
-        all_r = all_r.to(torch.int64).contiguous()
-        etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
-        nq = all_h.numel()
-        g, nr = self.graph.device_graph(device), self.native_rules(device)
-        stream = torch.cuda.current_stream(device).cuda_stream
-        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        while True:
-            scale = self.capacity_scale
-            ws = self._workspace(device, nq, scale)
-            _native.call("rnnl_ground", g, nr.ptr, all_h.data_ptr(), all_r.data_ptr(),
-                         etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
-                         ws.numel(), scale, stream)
-            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
-            if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
-                self.capacity_scale *= 2
-                continue
-            _native.check(rc)
-            break
-        nc = n_cand.to(torch.int64)
-        cand_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
-        torch.cumsum(nc, 0, out=cand_off[1:])
-        C = int(cand_off[-1].item())
-        ent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
-        nent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
-        _native.call("rnnl_ground_export_candidates", ws.data_ptr(), nq, scale, n_cand.data_ptr(),
-                     cand_off.data_ptr(), ent.data_ptr(), nent.data_ptr(), stream)
-        ent, nent = ent[:C].to(torch.int64), nent[:C].to(torch.int64)
-        row = torch.repeat_interleave(torch.arange(nq, device=device), nc)
-        per_row = torch.zeros(nq, dtype=torch.int64, device=device).index_add_(0, row, nent)
-        ent_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
-        torch.cumsum(per_row, 0, out=ent_off[1:])
-        P = int(ent_off[-1].item())
-        node = torch.empty(max(P, 1), dtype=torch.int32, device=device)
-        count = torch.empty(max(P, 1), dtype=torch.int32, device=device)
-        _native.call("rnnl_ground_export_entries", ws.data_ptr(), nq, scale, n_cand.data_ptr(), ent_off.data_ptr(),
-                     node.data_ptr(), count.data_ptr(), stream)
-        cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent)
-        return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64)
-
     def forward_autograd(self, all_h, all_r, edges_to_remove):
         """Differentiable forward (training): the HIP grounding's COO, then the
         reference's aggregation / MLP / entity feature as torch ops on it, so
@@ -482,9 +614,6 @@ class PredictorPlus(torch.nn.Module):
                                                                                 device=device)
         mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
         return score.masked_fill(~mask, float("-inf")), mask
-
-    def _needs_grad(self):
-        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     def forward(self, all_h, all_r, edges_to_remove):
         """predictors.py:210-271: one single-relation batch -> (score, mask).

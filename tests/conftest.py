@@ -52,7 +52,7 @@ class Fixture:
         return datasets.rotate_path(self.cfg["data"], int(emb.split(":")[1]))
 
 
-ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("_", "train_")))
+ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("_", "train_", "pred_")))
 # training-path fixtures (tools/make_golden_train.py)
 TRAIN_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("train_") and f.endswith(".npz"))
 TRAIN_SPECS = {  # dataset, PredictorPlus kwargs, RotatE dir — mirrors tools/make_golden_train.py CASES
@@ -61,6 +61,8 @@ TRAIN_SPECS = {  # dataset, PredictorPlus kwargs, RotatE dir — mirrors tools/m
     "train_kinship_lstm_sum_none": ("kinship", dict(type="lstm", entity_feature="none", aggregator="sum"), None),
     "train_kinship_emb_pna_bias": ("kinship", dict(type="emb", entity_feature="bias", aggregator="pna"), None),
 }
+# EM rule-weight Predictor fixtures (tools/make_golden_predictor.py)
+PRED_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("pred_") and f.endswith(".npz"))
 SMALL_CASES = [c for c in ALL_CASES if c.startswith(("umls", "kinship"))]
 
 
