@@ -32,8 +32,12 @@
 
 namespace rnnl {
 
-constexpr int BS = 256;      // threads per workgroup
-constexpr int NW = BS / 64;  // waves
+constexpr int BS = 256;      // threads per workgroup (scoring kernels)
+#ifndef RNNL_GBS
+#define RNNL_GBS 256
+#endif
+constexpr int GBS = RNNL_GBS;  // threads per grounding workgroup
+constexpr int GNW = GBS / 64;  // its waves
 #ifndef RNNL_HBITS
 #define RNNL_HBITS 12
 #endif
@@ -47,7 +51,10 @@ constexpr int HBITS = RNNL_HBITS;
 constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count)
 constexpr int WBITS = RNNL_WBITS;  // phase-B entity window: WIN entities
 constexpr int WIN = 1 << WBITS;
-constexpr int MAXWIN = (1 << 19) >> WBITS;  // windows per graph (|E| <= 524288)
+#ifndef RNNL_MAXE_BITS
+#define RNNL_MAXE_BITS 19
+#endif
+constexpr int MAXWIN = (1 << RNNL_MAXE_BITS) >> WBITS;  // windows per graph (|E| <= 2^RNNL_MAXE_BITS)
 constexpr int HB = WIN;            // phase-B candidate hash slots (one window at <= 0.75 load... or less)
 constexpr int HB_LOAD = HB * 3 / 4;  // max contributions per hash pass
 constexpr int WG_PER_CU = RNNL_WG_PER_CU;
@@ -102,11 +109,9 @@ struct KParams {
   unsigned char *slots;
   int64_t *q_base;   // per query: first pool index of its run
   float *q_scale;    // per query: PNA mean log-degree
-  int32_t *c_t;      // per pool index: candidate entity (first n_cand entries of a run)
-  int32_t *c_beg;    //                 candidate bucket start (pool index)
-  int32_t *c_cnt;    //                 candidate bucket length
-  int32_t *b_node;   // bucket entries: trie node
-  uint32_t *b_cnt;   //                 path count
+  int4 *cand;        // per pool index: candidate record (entity, bucket start, bucket length, 0)
+                     // (the first n_cand entries of a query's run)
+  int2 *bent;        // bucket entries: (trie node, path count bits)
   unsigned long long *prof;  // diagnostic phase cycle counters (nullable)
 };
 
@@ -121,11 +126,20 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 
 __device__ __forceinline__ uint32_t hash32(uint32_t k) { return k * 2654435761u; }
 
+// Per-slot scratch: two frontier buffers (node | entity | count planes of
+// fcap entries each) then the contribution planes.  Buffer pointers are
+// computed, not indexed from an array: a runtime index into a pointer array
+// would put the array in scratch memory.
 struct Slot {
-  int32_t *fn[2], *fv[2];
-  uint32_t *fc[2];
+  int32_t *f0;
+  int64_t fcap;
   int32_t *ct, *cn;
   uint32_t *cc;
+  __device__ __forceinline__ int32_t *fn(int k) const { return f0 + (int64_t)(3 * k) * fcap; }
+  __device__ __forceinline__ int32_t *fv(int k) const { return f0 + (int64_t)(3 * k + 1) * fcap; }
+  __device__ __forceinline__ uint32_t *fc(int k) const {
+    return reinterpret_cast<uint32_t *>(f0 + (int64_t)(3 * k + 2) * fcap);
+  }
 };
 
 __host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) { return 2 * fcap * 12 + pcap * 12; }
@@ -133,14 +147,9 @@ __host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) { retu
 __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, int64_t pcap) {
   unsigned char *b = base + (int64_t)slot * slot_bytes(fcap, pcap);
   Slot s;
-  for (int k = 0; k < 2; ++k) {
-    s.fn[k] = reinterpret_cast<int32_t *>(b);
-    b += fcap * 4;
-    s.fv[k] = reinterpret_cast<int32_t *>(b);
-    b += fcap * 4;
-    s.fc[k] = reinterpret_cast<uint32_t *>(b);
-    b += fcap * 4;
-  }
+  s.f0 = reinterpret_cast<int32_t *>(b);
+  s.fcap = fcap;
+  b += 2 * fcap * 12;
   s.ct = reinterpret_cast<int32_t *>(b);
   b += pcap * 4;
   s.cn = reinterpret_cast<int32_t *>(b);
@@ -152,7 +161,7 @@ __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, in
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
-  int64_t off_qbase, off_qscale, off_ct, off_cbeg, off_ccnt, off_bnode, off_bcnt, off_slots, total;
+  int64_t off_qbase, off_qscale, off_cand, off_bent, off_slots, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -168,16 +177,10 @@ static Layout make_layout(int64_t nq, int64_t scale) {
   o += 8 * std::max<int64_t>(nq, 1);
   L.off_qscale = o = align256(o);
   o += 4 * std::max<int64_t>(nq, 1);
-  L.off_ct = o = align256(o);
-  o += 4 * L.pool_cap;
-  L.off_cbeg = o = align256(o);
-  o += 4 * L.pool_cap;
-  L.off_ccnt = o = align256(o);
-  o += 4 * L.pool_cap;
-  L.off_bnode = o = align256(o);
-  o += 4 * L.pool_cap;
-  L.off_bcnt = o = align256(o);
-  o += 4 * L.pool_cap;
+  L.off_cand = o = align256(o);
+  o += 16 * L.pool_cap;
+  L.off_bent = o = align256(o);
+  o += 8 * L.pool_cap;
   L.off_slots = o = align256(o);
   o += L.nslots * slot_bytes(L.fcap, L.pcap);
   L.total = o;
@@ -197,16 +200,16 @@ __device__ __forceinline__ int block_scan(int x, int *s_ws, int &total) {
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < GNW; ++w) {
       int t = s_ws[w];
       s_ws[w] = acc;
       acc += t;
     }
-    s_ws[NW] = acc;
+    s_ws[GNW] = acc;
   }
   __syncthreads();
   const int res = v - x + s_ws[wid];
-  total = s_ws[NW];
+  total = s_ws[GNW];
   __syncthreads();
   return res;
 }
@@ -254,11 +257,11 @@ struct __align__(16) Smem {
       int cid[HB];   // candidate index within the pass
     } c;
   } u;
-  int ent_v[BS], ent_fch[BS], item_off[BS];
-  uint32_t ent_c[BS];
-  int it_child[BS], it_beg[BS], it_flags[BS], edge_off[BS];
-  uint32_t it_c[BS];
-  int ws[NW + 1];
+  int ent_v[GBS], ent_fch[GBS], item_off[GBS];
+  uint32_t ent_c[GBS];
+  int it_child[GBS], it_beg[GBS], it_flags[GBS], edge_off[GBS];
+  uint32_t it_c[GBS];
+  int ws[GNW + 1];
   int q, nd, np, ovf, err;
   long long qbase;
   unsigned long long t0;
@@ -282,9 +285,9 @@ __device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, 
                                               uint32_t c) {
   const int pos = atomicAdd(&S.nd, 1);
   if (pos < fcap) {
-    sl.fn[buf][pos] = node;
-    sl.fv[buf][pos] = v;
-    sl.fc[buf][pos] = c;
+    sl.fn(buf)[pos] = node;
+    sl.fv(buf)[pos] = v;
+    sl.fc(buf)[pos] = c;
   } else {
     S.ovf = 1;
   }
@@ -331,9 +334,9 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
   const int E = p.g.E, R = p.g.R;
   const int depth = p.rl.head_depth[r];
   if (tid == 0) {
-    sl.fn[0][0] = root;
-    sl.fv[0][0] = h;
-    sl.fc[0][0] = 1u;
+    sl.fn(0)[0] = root;
+    sl.fv(0)[0] = h;
+    sl.fc(0)[0] = 1u;
     if (p.rl.node_nrules[root] > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
   }
   wg_sync_global();
@@ -341,14 +344,14 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
   int cur = 0, n_prev = 1;
   for (int d = 1; d <= depth; ++d) {
     const int nxt = cur ^ 1;
-    for (int cb = 0; cb < n_prev; cb += BS) {
+    for (int cb = 0; cb < n_prev; cb += GBS) {
       if (watchdog(S)) break;
-      const int ne = min(BS, n_prev - cb);
+      const int ne = min(GBS, n_prev - cb);
       int nch = 0;
       if (tid < ne) {
-        const int node = sl.fn[cur][cb + tid];
-        S.ent_v[tid] = sl.fv[cur][cb + tid];
-        S.ent_c[tid] = sl.fc[cur][cb + tid];
+        const int node = sl.fn(cur)[cb + tid];
+        S.ent_v[tid] = sl.fv(cur)[cb + tid];
+        S.ent_c[tid] = sl.fc(cur)[cb + tid];
         S.ent_fch[tid] = p.rl.node_child[node];
         nch = p.rl.node_nchild[node];
       }
@@ -357,7 +360,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       S.item_off[tid] = ioff;
       __syncthreads();
       PSTAMP(3);
-      for (int ib = 0; ib < NI; ib += BS) {
+      for (int ib = 0; ib < NI; ib += GBS) {
         const int k = ib + tid;
         int deg = 0;
         if (k < NI) {
@@ -381,8 +384,8 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
         S.edge_off[tid] = eoff;
         __syncthreads();
         PSTAMP(4);
-        const int nit = min(BS, NI - ib);
-        for (int eb = 0; eb < NE; eb += BS) {
+        const int nit = min(GBS, NI - ib);
+        for (int eb = 0; eb < NE; eb += GBS) {
           const int j = eb + tid;
           if (j < NE) {
             const int it = upper_idx(S.edge_off, nit, j);
@@ -403,7 +406,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       }
     }
     // compact the hash into the next frontier and clear it
-    for (int s = tid; s < HCAP; s += BS) {
+    for (int s = tid; s < HCAP; s += GBS) {
       const int k = S.u.a.key[s];
       if (k != EMPTY) {
         emit_frontier(S, sl, nxt, p.fcap, root + k / E, k % E, S.u.a.val[s]);
@@ -424,7 +427,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
 // ---------------------------------------------------------------- phase B
 // Exclusive scan of WIN ints in place (PER consecutive per thread); returns the total.
 __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
-  constexpr int PER = WIN / BS;
+  constexpr int PER = WIN / GBS;
   const int tid = threadIdx.x;
   int loc[PER];
   int sum = 0;
@@ -451,17 +454,17 @@ __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
 __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, int beg, int end, int64_t cbase,
                            bool degree_only) {
   const int tid = threadIdx.x;
-  const int32_t *wt = sl.fn[0], *wn = sl.fv[0];
-  const uint32_t *wc = sl.fc[0];
+  const int32_t *wt = sl.fn(0), *wn = sl.fv(0);
+  const uint32_t *wc = sl.fc(0);
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
-  for (int i = tid; i < WIN; i += BS) S.u.b.map[i] = 0;
+  for (int i = tid; i < WIN; i += GBS) S.u.b.map[i] = 0;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += BS) S.u.b.map[wt[i] - lo] = 1;  // mark present entities
+  for (int i = beg + tid; i < end; i += GBS) S.u.b.map[wt[i] - lo] = 1;  // mark present entities
   __syncthreads();
-  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = S.u.b.map[i];
+  for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = S.u.b.map[i];
   __syncthreads();
   const int nc = scan_win(S.u.b.cnt, S.ws);  // slots in ascending entity order
-  for (int i = tid; i < WIN; i += BS) {
+  for (int i = tid; i < WIN; i += GBS) {
     if (S.u.b.map[i]) {
       const int slot = S.u.b.cnt[i];
       S.u.b.map[i] = slot;
@@ -469,43 +472,40 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
     }
   }
   __syncthreads();
-  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
+  for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = 0;
   __syncthreads();
   PSTAMP(0);
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
-    for (int i = beg + tid; i < end; i += BS)
+    for (int i = beg + tid; i < end; i += GBS)
       atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[wt[i] - lo]]),
                 wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
     __syncthreads();
-    for (int s2 = tid; s2 < nc; s2 += BS) {
+    for (int s2 = tid; s2 < nc; s2 += GBS) {
       const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
       atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
     }
     __syncthreads();
     return nc;
   }
-  for (int i = beg + tid; i < end; i += BS) atomicAdd(&S.u.b.cnt[S.u.b.map[wt[i] - lo]], 1);  // bucket sizes
+  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.b.cnt[S.u.b.map[wt[i] - lo]], 1);  // bucket sizes
   __syncthreads();
-  for (int i = tid; i < WIN; i += BS) S.u.b.off[i] = S.u.b.cnt[i];
+  for (int i = tid; i < WIN; i += GBS) S.u.b.off[i] = S.u.b.cnt[i];
   __syncthreads();
   scan_win(S.u.b.off, S.ws);
   // candidate records
   const int64_t qb = S.qbase;
-  for (int s2 = tid; s2 < nc; s2 += BS) {
-    p.c_t[cbase + s2] = S.u.b.st[s2];
-    p.c_beg[cbase + s2] = (int32_t)(qb + beg + S.u.b.off[s2]);
-    p.c_cnt[cbase + s2] = S.u.b.cnt[s2];
+  for (int s2 = tid; s2 < nc; s2 += GBS) {
+    p.cand[cbase + s2] = make_int4(S.u.b.st[s2], (int32_t)(qb + beg + S.u.b.off[s2]), S.u.b.cnt[s2], 0);
   }
   __syncthreads();
-  for (int i = tid; i < WIN; i += BS) S.u.b.cnt[i] = 0;
+  for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = 0;
   __syncthreads();
   PSTAMP(1);
-  for (int i = beg + tid; i < end; i += BS) {  // scatter (node, count) into the buckets
+  for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
     const int s2 = S.u.b.map[wt[i] - lo];
     const int64_t pos = qb + beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
-    p.b_node[pos] = wn[i];
-    p.b_cnt[pos] = wc[i];
+    p.bent[pos] = make_int2(wn[i], (int)wc[i]);
   }
   __syncthreads();
   PSTAMP(2);
@@ -532,17 +532,17 @@ __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
 __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int end, int64_t cbase,
                          bool degree_only) {
   const int tid = threadIdx.x;
-  const int32_t *wt = sl.fn[0], *wn = sl.fv[0];
-  const uint32_t *wc = sl.fc[0];
-  for (int i = tid; i < HB; i += BS) {
+  const int32_t *wt = sl.fn(0), *wn = sl.fv(0);
+  const uint32_t *wc = sl.fc(0);
+  for (int i = tid; i < HB; i += GBS) {
     S.u.c.key[i] = EMPTY;
     S.u.c.cnt[i] = 0;
   }
   __syncthreads();
-  for (int i = beg + tid; i < end; i += BS) atomicAdd(&S.u.c.cnt[hb_slot(S, wt[i], true)], 1);
+  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, wt[i], true)], 1);
   __syncthreads();
   // one scan of (bucket size << 12 | occupied): bucket offsets and candidate ids
-  constexpr int PER = HB / BS;
+  constexpr int PER = HB / GBS;
   int loc[PER];
   int sum = 0;
 #pragma unroll
@@ -564,13 +564,13 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int
   __syncthreads();
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
-    for (int i = tid; i < HB; i += BS) S.u.c.cnt[i] = 0;
+    for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
     __syncthreads();
-    for (int i = beg + tid; i < end; i += BS)
+    for (int i = beg + tid; i < end; i += GBS)
       atomicAdd(reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, wt[i], false)]),
                 wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
     __syncthreads();
-    for (int i = tid; i < HB; i += BS) {
+    for (int i = tid; i < HB; i += GBS) {
       if (S.u.c.key[i] != EMPTY) {
         const float degf = (float)((double)(uint32_t)S.u.c.cnt[i] + 1.0);
         atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
@@ -580,22 +580,19 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int
     return nc;
   }
   const int64_t qb = S.qbase;
-  for (int i = tid; i < HB; i += BS) {
+  for (int i = tid; i < HB; i += GBS) {
     if (S.u.c.key[i] != EMPTY) {
       const int64_t c = cbase + S.u.c.cid[i];
-      p.c_t[c] = S.u.c.key[i];
-      p.c_beg[c] = (int32_t)(qb + beg + S.u.c.off[i]);
-      p.c_cnt[c] = S.u.c.cnt[i];
+      p.cand[c] = make_int4(S.u.c.key[i], (int32_t)(qb + beg + S.u.c.off[i]), S.u.c.cnt[i], 0);
     }
   }
   __syncthreads();
-  for (int i = tid; i < HB; i += BS) S.u.c.cnt[i] = 0;
+  for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += BS) {  // scatter (node, count) into the buckets
+  for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
     const int sl2 = hb_slot(S, wt[i], false);
     const int64_t pos = qb + beg + S.u.c.off[sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
-    p.b_node[pos] = wn[i];
-    p.b_cnt[pos] = wc[i];
+    p.bent[pos] = make_int2(wn[i], (int)wc[i]);
   }
   __syncthreads();
   return nc;
@@ -607,9 +604,9 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
   const int tid = threadIdx.x;
   const int nwin = (p.g.E + WIN - 1) >> WBITS;
   if (!sorted) {
-    for (int i = tid; i < nwin; i += BS) S.whist[i] = 0;
+    for (int i = tid; i < nwin; i += GBS) S.whist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < P; i += BS) atomicAdd(&S.whist[sl.ct[i] >> WBITS], 1);
+    for (int i = tid; i < P; i += GBS) atomicAdd(&S.whist[sl.ct[i] >> WBITS], 1);
     __syncthreads();
     if (tid == 0) {
       int acc = 0;
@@ -622,12 +619,12 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
       S.wbeg[nwin] = acc;
     }
     __syncthreads();
-    for (int i = tid; i < P; i += BS) {
+    for (int i = tid; i < P; i += GBS) {
       const int t = sl.ct[i];
       const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
-      sl.fn[0][pos] = t;
-      sl.fv[0][pos] = sl.cn[i];
-      sl.fc[0][pos] = sl.cc[i];
+      sl.fn(0)[pos] = t;
+      sl.fv(0)[pos] = sl.cn[i];
+      sl.fc(0)[pos] = sl.cc[i];
     }
     wg_sync_global();
   }
@@ -662,13 +659,13 @@ __device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, 
 #define RNNL_GROUND_MINB 1
 #endif
 template <int AGG>
-__global__ __launch_bounds__(BS, RNNL_GROUND_MINB) void ground_kernel(KParams p) {
+__global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
   unsigned long long *pool_ctr = reinterpret_cast<unsigned long long *>(p.ws + 64);
   const Slot sl = make_slot(p.slots, blockIdx.x, p.fcap, p.pcap);
-  for (int s = tid; s < HCAP; s += BS) {
+  for (int s = tid; s < HCAP; s += GBS) {
     S.u.a.key[s] = EMPTY;
     S.u.a.val[s] = 0u;
   }
@@ -730,7 +727,7 @@ __global__ __launch_bounds__(BS, RNNL_GROUND_MINB) void ground_kernel(KParams p)
     }
     __syncthreads();
     if (S.ovf || P > p.pcap || S.err) {
-      for (int s = tid; s < HCAP; s += BS) {  // leave the LDS hash clean for the next query
+      for (int s = tid; s < HCAP; s += GBS) {  // leave the LDS hash clean for the next query
         S.u.a.key[s] = EMPTY;
         S.u.a.val[s] = 0u;
       }
@@ -759,7 +756,7 @@ __global__ __launch_bounds__(BS, RNNL_GROUND_MINB) void ground_kernel(KParams p)
         pr[5] += ncand;
       }
     }
-    for (int s = tid; s < HCAP; s += BS) {  // restore the phase-A hash (phase B reused its LDS)
+    for (int s = tid; s < HCAP; s += GBS) {  // restore the phase-A hash (phase B reused its LDS)
       S.u.a.key[s] = EMPTY;
       S.u.a.val[s] = 0u;
     }
@@ -795,8 +792,9 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
   long long deg = 0;
   uint64_t fp = 0;
   for (int e = beg; e < beg + cnt; ++e) {
-    const int n = p.b_node[e];
-    const long long c = p.b_cnt[e];
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const long long c = (uint32_t)be.y;
     const long long *rec = reinterpret_cast<const long long *>(p.node_w + (int64_t)n * STRIDE);
 #pragma unroll
     for (int d = 0; d < 16; ++d) a1[d] += c * rec[d];
@@ -934,12 +932,13 @@ __global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__res
     const int64_t qb = p.q_base[q];
     const float ms = AGG == RNNL_AGG_PNA ? p.q_scale[q] : 0.f;
     for (int s = tid; s < nc; s += BS) {
-      const int t = p.c_t[qb + s];
+      const int4 cr = p.cand[qb + s];
+      const int t = cr.x;
       uint64_t dg = 0;
       // keep the loop-invariant LDS weight reads inside the loop (hoisted,
       // they would pin ~200 VGPRs and starve occupancy)
       asm volatile("" ::: "memory");
-      const float out = score_one<AGG>(p, s_w, s_relb, p.c_beg[qb + s], p.c_cnt[qb + s], ms,
+      const float out = score_one<AGG>(p, s_w, s_relb, cr.y, cr.z, ms,
                                        p.digest ? &dg : nullptr, t);
       if (p.digest) atomicAdd(&s_dig, (unsigned long long)dg);
       const int64_t idx = (int64_t)q * p.g.E + t;
@@ -980,7 +979,7 @@ __host__ __device__ inline int64_t sum_stage_bytes(int max_leaves, int max_head_
   return (int64_t)max_leaves * (64 + 4 + 8) + (int64_t)max_head_nodes * 2 + 64;
 }
 
-template <bool STAGED>
+template <bool STAGED, bool DIGEST>
 __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st, int root, int beg, int cnt,
                                            float inv_scale, float f[16], long long &deg, uint64_t &fp) {
   long long acc[16];
@@ -989,21 +988,28 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
   deg = 0;
   fp = 0;
   for (int e = beg; e < beg + cnt; ++e) {
-    const int n = p.b_node[e];
-    const uint32_t cu = p.b_cnt[e];
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const uint32_t cu = (uint32_t)be.y;
     const long long c = cu;
     const int *x;
     int nr;
     uint64_t nf;
+    nr = 0;
+    nf = 0;
     if constexpr (STAGED) {
       const int li = st.map[n - root];
       x = reinterpret_cast<const int *>(st.rec) + li * 16;
-      nr = st.nr[li];
-      nf = ((uint64_t)st.fp[li].y << 32) | st.fp[li].x;
+      if constexpr (DIGEST) {
+        nr = st.nr[li];
+        nf = ((uint64_t)st.fp[li].y << 32) | st.fp[li].x;
+      }
     } else {
       x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
-      nr = p.rl.node_nrules[n];
-      nf = p.rl.node_fp[n];
+      if constexpr (DIGEST) {  // the digest's degree / fingerprint terms only
+        nr = p.rl.node_nrules[n];
+        nf = p.rl.node_fp[n];
+      }
     }
     if (cu < 0x80000000u) {  // one v_mad_i64_i32 per element
       const int ci = (int)cu;
@@ -1057,8 +1063,12 @@ __device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const flo
   return out + wl[L::S1B];
 }
 
-template <bool STAGED>
-__global__ __launch_bounds__(BS) void score_sum_kernel(KParams p, const float *__restrict__ W) {
+#ifndef RNNL_SCORE_WAVES
+#define RNNL_SCORE_WAVES 8
+#endif
+template <bool STAGED, bool DIGEST>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_WAVES, 8))) void score_sum_kernel(
+    KParams p, const float *__restrict__ W) {
   using L = WL<RNNL_AGG_SUM>;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   float *s_w = reinterpret_cast<float *>(dyn);
@@ -1141,24 +1151,25 @@ __global__ __launch_bounds__(BS) void score_sum_kernel(KParams p, const float *_
       }
       const int64_t qb = p.q_base[q];
       for (int s2 = tid; s2 < nc; s2 += BS) {
-        const int t = p.c_t[qb + s2];
+        const int4 cr = p.cand[qb + s2];
+        const int t = cr.x;
         float f[16];
         long long deg;
         uint64_t fp;
-        gather_sum<STAGED>(p, st, root, p.c_beg[qb + s2], p.c_cnt[qb + s2], inv_scale, f, deg, fp);
-        if (p.digest) atomicAdd(&s_dig, (unsigned long long)mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp))));
+        const int64_t idx = (int64_t)q * p.g.E + t;
+        // the base score's load is issued before the gather (its latency hides under it)
+        const float base = p.feature == RNNL_FEATURE_NONE ? 0.f : p.score[idx];
+        gather_sum<STAGED, DIGEST>(p, st, root, cr.y, cr.z, inv_scale, f, deg, fp);
+        if constexpr (DIGEST)
+          atomicAdd(&s_dig, (unsigned long long)mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp))));
         // keep the loop-invariant LDS weight reads inside the loop (hoisted,
         // they would pin ~200 VGPRs and starve occupancy)
         asm volatile("" ::: "memory");
         const float out = mlp_sum(s_w, s_relb, f);
-        const int64_t idx = (int64_t)q * p.g.E + t;
-        if (p.feature == RNNL_FEATURE_NONE)
-          p.score[idx] = out;
-        else
-          p.score[idx] = out + p.score[idx];
+        p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + base;
         if (p.mask) p.mask[idx] = 1;
       }
-      if (p.digest) {
+      if (DIGEST) {
         __syncthreads();
         if (tid == 0) p.digest[q] = s_dig;
       }
@@ -1233,8 +1244,9 @@ __global__ void export_candidates_kernel(KParams p, const int64_t *__restrict__ 
     if (nc <= 0) continue;
     const int64_t qb = p.q_base[q], o = cand_off[q];
     for (int s = threadIdx.x; s < nc; s += blockDim.x) {
-      out_t[o + s] = p.c_t[qb + s];
-      out_nent[o + s] = p.c_cnt[qb + s];
+      const int4 cr = p.cand[qb + s];
+      out_t[o + s] = cr.x;
+      out_nent[o + s] = cr.z;
     }
   }
 }
@@ -1245,8 +1257,9 @@ __global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent
     if (p.n_cand[q] <= 0) continue;
     const int64_t qb = p.q_base[q], o = ent_off[q], n = ent_off[q + 1] - o;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      out_node[o + i] = p.b_node[qb + i];
-      out_count[o + i] = (int32_t)p.b_cnt[qb + i];
+      const int2 be = p.bent[qb + i];
+      out_node[o + i] = be.x;
+      out_count[o + i] = be.y;
     }
   }
 }
@@ -1317,10 +1330,13 @@ __global__ __launch_bounds__(BS) void score_linear_kernel(KParams p, const int *
     if (nc <= 0) continue;
     const int64_t qb = p.q_base[q];
     for (int s = threadIdx.x; s < nc; s += BS) {
-      const int t = p.c_t[qb + s];
-      const int beg = p.c_beg[qb + s], cnt = p.c_cnt[qb + s];
+      const int4 cr = p.cand[qb + s];
+      const int t = cr.x;
       long long acc = 0;
-      for (int e = beg; e < beg + cnt; ++e) acc += (long long)p.b_cnt[e] * fix[p.b_node[e]];
+      for (int e = cr.y; e < cr.y + cr.z; ++e) {
+        const int2 be = p.bent[e];
+        acc += (long long)(uint32_t)be.y * fix[be.x];
+      }
       const float out = (float)((double)acc * inv);
       const int64_t idx = (int64_t)q * p.g.E + t;
       if (p.feature == RNNL_FEATURE_NONE)
@@ -1350,11 +1366,12 @@ __global__ __launch_bounds__(BS) void rule_stats_kernel(KParams p, const int64_t
     const int64_t qb = p.q_base[q];
     const int tq = (int)all_t[q];
     for (int s = threadIdx.x; s < nc; s += BS) {
-      const int t = p.c_t[qb + s];
-      const int beg = p.c_beg[qb + s], cnt = p.c_cnt[qb + s];
-      for (int e = beg; e < beg + cnt; ++e) {
-        const int k = p.b_node[e] - root;
-        const unsigned long long c = p.b_cnt[e];
+      const int4 cr = p.cand[qb + s];
+      const int t = cr.x;
+      for (int e = cr.y; e < cr.y + cr.z; ++e) {
+        const int2 be = p.bent[e];
+        const int k = be.x - root;
+        const unsigned long long c = (uint32_t)be.y;
         atomicAdd(&s_tot[k], c);
         if (t == tq) pos[(int64_t)q * ld + k] += (long long)c;  // one lane owns the true tail
       }
@@ -1448,11 +1465,8 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
   p.slots = base + Ly.off_slots;
   p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
   p.q_scale = reinterpret_cast<float *>(base + Ly.off_qscale);
-  p.c_t = reinterpret_cast<int32_t *>(base + Ly.off_ct);
-  p.c_beg = reinterpret_cast<int32_t *>(base + Ly.off_cbeg);
-  p.c_cnt = reinterpret_cast<int32_t *>(base + Ly.off_ccnt);
-  p.b_node = reinterpret_cast<int32_t *>(base + Ly.off_bnode);
-  p.b_cnt = reinterpret_cast<uint32_t *>(base + Ly.off_bcnt);
+  p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
+  p.bent = reinterpret_cast<int2 *>(base + Ly.off_bent);
   p.prof = g_prof;
   return RNNL_OK;
 }
@@ -1491,7 +1505,7 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
   const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
   if (pp->aggregator == RNNL_AGG_SUM) {
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
     // staged path while the largest head's leaves fit the LDS budget
     const int64_t base_lds = (int64_t)(WL<RNNL_AGG_SUM>::N + 128) * 4;
     const int64_t stage = sum_stage_bytes(r->d.max_leaves, r->d.max_head_nodes);
@@ -1499,13 +1513,16 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
 #ifndef RNNL_STAGE_LIMIT
 #define RNNL_STAGE_LIMIT 0  // staging measured slower (lower occupancy); kept for A/B
 #endif
-    if (base_lds + stage <= RNNL_STAGE_LIMIT)
-      hipLaunchKernelGGL(score_sum_kernel<true>, dim3(sgrid), dim3(BS), (size_t)(base_lds + stage), st, p,
-                         (const float *)W);
+    const bool staged = base_lds + stage <= RNNL_STAGE_LIMIT;
+    const size_t lds = (size_t)(staged ? base_lds + stage : base_lds);
+    if (staged)
+      hipLaunchKernelGGL((score_sum_kernel<true, true>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
+    else if (p.digest)
+      hipLaunchKernelGGL((score_sum_kernel<false, true>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
     else
-      hipLaunchKernelGGL(score_sum_kernel<false>, dim3(sgrid), dim3(BS), (size_t)base_lds, st, p, (const float *)W);
+      hipLaunchKernelGGL((score_sum_kernel<false, false>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
   } else {
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(BS), 0, st, p);
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(GBS), 0, st, p);
     hipLaunchKernelGGL(score_kernel<RNNL_AGG_PNA>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
   }
   RNNL_HIP_CHECK(hipGetLastError());
@@ -1520,7 +1537,7 @@ int rnnl_ground(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t 
   RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
   if (nq == 0) return RNNL_OK;
   p.agg = RNNL_AGG_SUM;
-  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
@@ -1533,10 +1550,8 @@ static KParams export_params(void *ws, int32_t nq, int32_t scale, const int32_t 
   p.nq = nq;
   p.n_cand = const_cast<int32_t *>(n_cand);
   p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
-  p.c_t = reinterpret_cast<int32_t *>(base + Ly.off_ct);
-  p.c_cnt = reinterpret_cast<int32_t *>(base + Ly.off_ccnt);
-  p.b_node = reinterpret_cast<int32_t *>(base + Ly.off_bnode);
-  p.b_cnt = reinterpret_cast<uint32_t *>(base + Ly.off_bcnt);
+  p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
+  p.bent = reinterpret_cast<int2 *>(base + Ly.off_bent);
   return p;
 }
 
@@ -1610,7 +1625,7 @@ int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32
   p.feature = feature;
   p.score = score;
   p.mask = mask;
-  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(BS), 0, st, p);
+  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
   hipLaunchKernelGGL(score_linear_kernel, dim3((unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8)), dim3(BS), 0, st,
                      p, static_cast<const int *>(node_w));
   RNNL_HIP_CHECK(hipGetLastError());
@@ -1633,8 +1648,6 @@ int rnnl_predictor_rule_stats(void *ws, int32_t nq, int32_t scale, const int32_t
   KParams p = export_params(ws, nq, scale, n_cand);
   p.rl = r->d;
   p.all_r = all_r;
-  const Layout Ly = make_layout(nq, scale);
-  p.c_beg = reinterpret_cast<int32_t *>(static_cast<unsigned char *>(ws) + Ly.off_cbeg);
   hipLaunchKernelGGL(rule_stats_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(BS), (size_t)ld * 8,
                      (hipStream_t)stream, p, all_t, ld, reinterpret_cast<long long *>(pos),
                      reinterpret_cast<long long *>(tot));
