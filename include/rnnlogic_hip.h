@@ -142,6 +142,21 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
                                const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries,
                                float *score, uint8_t *mask, int32_t *n_cand, uint64_t *digest, void *workspace,
                                size_t workspace_bytes, int32_t capacity_scale, void *stream);
+/* The same forward in two halves, so that the grounding (independent of the
+ * base score) can run on a second stream beside rnnl_rotate_score:
+ * rnnl_predictorplus_ground fills the workspace (grounding + candidate
+ * buckets, and for PNA the per-row mean log-degree) and n_cand;
+ * rnnl_predictorplus_score then updates score / mask from that workspace
+ * (same n_queries, capacity_scale, rows).  rnnl_predictorplus_forward ==
+ * ground then score on one stream. */
+int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, const int64_t *all_h,
+                              const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries,
+                              int32_t *n_cand, void *workspace, size_t workspace_bytes, int32_t capacity_scale,
+                              void *stream);
+int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p, const int64_t *all_h,
+                             const int64_t *all_r, int32_t n_queries, float *score, uint8_t *mask, int32_t *n_cand,
+                             uint64_t *digest, void *workspace, size_t workspace_bytes, int32_t capacity_scale,
+                             void *stream);
 /* After a forward: RNNL_OK, or RNNL_ERR_OVERFLOW if any query exceeded the
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */

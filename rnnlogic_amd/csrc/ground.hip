@@ -1006,6 +1006,9 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
       }
     } else {
       x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+#ifdef RNNL_DIAG_NOGATHER  // diagnostic build: one shared record instead of the per-node gather
+      x = reinterpret_cast<const int *>(p.node_w);
+#endif
       if constexpr (DIGEST) {  // the digest's degree / fingerprint terms only
         nr = p.rl.node_nrules[n];
         nf = p.rl.node_fp[n];
@@ -1158,14 +1161,32 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
         uint64_t fp;
         const int64_t idx = (int64_t)q * p.g.E + t;
         // the base score's load is issued before the gather (its latency hides under it)
+#ifdef RNNL_DIAG_NOSCORE
+        const float base = 0.f;
+#else
         const float base = p.feature == RNNL_FEATURE_NONE ? 0.f : p.score[idx];
+#endif
+#ifdef RNNL_DIAG_NOENTRIES  // diagnostic build: no bucket-entry walk
+        for (int d = 0; d < 16; ++d) f[d] = (float)(cr.z * d);
+        deg = 0;
+        fp = 0;
+#else
         gather_sum<STAGED, DIGEST>(p, st, root, cr.y, cr.z, inv_scale, f, deg, fp);
+#endif
         if constexpr (DIGEST)
           atomicAdd(&s_dig, (unsigned long long)mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp))));
         // keep the loop-invariant LDS weight reads inside the loop (hoisted,
         // they would pin ~200 VGPRs and starve occupancy)
         asm volatile("" ::: "memory");
+#ifdef RNNL_DIAG_NOMLP  // diagnostic build: no MLP
+        const float out = f[0] + f[15];
+#else
         const float out = mlp_sum(s_w, s_relb, f);
+#endif
+#ifdef RNNL_DIAG_NOSCORE  // diagnostic build: no score/mask traffic
+        if (out == 1234.5f) p.score[idx] = base;
+        continue;
+#endif
         p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + base;
         if (p.mask) p.mask[idx] = 1;
       }
@@ -1471,21 +1492,16 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
   return RNNL_OK;
 }
 
-int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
-                               const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
-                               int32_t *n_cand, uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale,
-                               void *stream) {
-  if (!pp || !score || !pp->node_w || (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA)) {
-    set_error("rnnl_predictorplus_forward: bad arguments");
-    return RNNL_ERR_INVALID;
-  }
-  KParams p;
-  if (int rc = setup_params("rnnl_predictorplus_forward", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
-                            p))
-    return rc;
-  hipStream_t st = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
-  if (nq == 0) return RNNL_OK;
+// Kernel sequences shared by the one-call forward and its two halves.
+static void launch_ground(const KParams &p, int agg, hipStream_t st) {
+  if (agg == RNNL_AGG_SUM)
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
+  else
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(GBS), 0, st, p);
+}
+
+static void set_score_params(KParams &p, const rnnl_predictor_params *pp, float *score, uint8_t *mask,
+                             uint64_t *digest) {
   p.agg = pp->aggregator;
   p.feature = pp->feature;
   p.node_w = static_cast<const unsigned char *>(pp->node_w);
@@ -1501,11 +1517,13 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
   p.score = score;
   p.mask = mask;
   p.digest = digest;
+}
+
+static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st) {
+  const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
-  const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
-  if (pp->aggregator == RNNL_AGG_SUM) {
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
+  if (p.agg == RNNL_AGG_SUM) {
     // staged path while the largest head's leaves fit the LDS budget
     const int64_t base_lds = (int64_t)(WL<RNNL_AGG_SUM>::N + 128) * 4;
     const int64_t stage = sum_stage_bytes(r->d.max_leaves, r->d.max_head_nodes);
@@ -1522,9 +1540,73 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
     else
       hipLaunchKernelGGL((score_sum_kernel<false, false>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
   } else {
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(GBS), 0, st, p);
+    const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
     hipLaunchKernelGGL(score_kernel<RNNL_AGG_PNA>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
   }
+}
+
+static bool bad_params(const rnnl_predictor_params *pp, const float *score) {
+  return !pp || !score || !pp->node_w || (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA);
+}
+
+int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
+                               const int64_t *all_r, const int64_t *etr, int32_t nq, float *score, uint8_t *mask,
+                               int32_t *n_cand, uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale,
+                               void *stream) {
+  if (bad_params(pp, score)) {
+    set_error("rnnl_predictorplus_forward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p;
+  if (int rc = setup_params("rnnl_predictorplus_forward", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
+                            p))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  set_score_params(p, pp, score, mask, digest);
+  launch_ground(p, pp->aggregator, st);
+  launch_score(p, r, st);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, const int64_t *all_h,
+                              const int64_t *all_r, const int64_t *etr, int32_t nq, int32_t *n_cand, void *ws,
+                              size_t ws_bytes, int32_t scale, void *stream) {
+  if (aggregator != RNNL_AGG_SUM && aggregator != RNNL_AGG_PNA) {
+    set_error("rnnl_predictorplus_ground: bad aggregator");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p;
+  if (int rc = setup_params("rnnl_predictorplus_ground", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
+                            p))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  p.agg = aggregator;
+  launch_ground(p, aggregator, st);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
+                             const int64_t *all_r, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
+                             uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, void *stream) {
+  if (bad_params(pp, score) || !n_cand) {
+    set_error("rnnl_predictorplus_score: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p;
+  if (int rc = setup_params("rnnl_predictorplus_score", g, r, all_h, all_r, nullptr, nq, n_cand, ws, ws_bytes,
+                            scale, p))
+    return rc;
+  if (nq == 0) return RNNL_OK;
+  set_score_params(p, pp, score, mask, digest);
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(p.ws + 4 * H_DEQUEUE2, 0, 4, st));  // the scoring dequeue counter
+  launch_score(p, r, st);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

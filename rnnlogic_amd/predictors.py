@@ -19,6 +19,7 @@ the exported grounding COO.
 There is no CPU fallback: on a CPU tensor forward() raises.
 """
 import ctypes
+import os
 import logging
 import math
 
@@ -389,7 +390,14 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._native_rules = {}
         self._node_cache = {}
         self._ws = {}
+        self._ws_chunks = {}
+        self._side = {}
         self.capacity_scale = 1
+        # RotatE base score: rows are split into this many chunks; the grounding
+        # runs on a side stream beside the RotatE kernel and each chunk's
+        # scoring pass starts as soon as its RotatE rows are written
+        # (DESIGN.md "Stream overlap").  1 disables the overlap.
+        self.overlap_chunks = int(os.environ.get("RNNL_OVERLAP_CHUNKS", "2"))
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -525,6 +533,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        if self.entity_feature == "RotatE" and self.overlap_chunks > 1 and nq >= 2 * self.overlap_chunks:
+            self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec)
+            del keep
+            return (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device), n_cand) \
+                if return_ncand else (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device))
         while True:
             mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
             scale = self.capacity_scale
@@ -551,6 +564,78 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         else:
             mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
         return (score, mask, n_cand) if return_ncand else (score, mask)
+
+    def _chunk_workspace(self, device, k, nq, scale):
+        need = ctypes.c_size_t()
+        _native.call("rnnl_forward_workspace_size", self.graph.device_graph(device), self.native_rules(device).ptr,
+                     nq, scale, ctypes.byref(need))
+        key = (self._device_index(device), k)
+        ws = self._ws_chunks.get(key)
+        if ws is None or ws.numel() < need.value:
+            ws = torch.empty(need.value, dtype=torch.uint8, device=device)
+            self._ws_chunks[key] = ws
+        return ws
+
+    def _side_streams(self, device):
+        key = self._device_index(device)
+        if key not in self._side:
+            self._side[key] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+        return self._side[key]
+
+    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec):
+        """RotatE entity feature: the same kernels as the one-stream path, in
+        row chunks over three streams — RotatE rows on the current stream,
+        the grounding of every chunk on side stream A (it does not read the
+        base score, and it is latency-bound where RotatE is VALU-bound), and
+        each chunk's scoring pass on side stream B once both its grounding and
+        its RotatE rows are done.  Results are bit-identical to the
+        one-stream path (same kernels, same inputs per row)."""
+        main = torch.cuda.current_stream(device)
+        side_g, side_s = self._side_streams(device)
+        nq = all_h.numel()
+        K = self.overlap_chunks
+        bounds = [nq * k // K for k in range(K + 1)]
+        agg = params.aggregator
+        while True:
+            scale = self.capacity_scale
+            wss = [self._chunk_workspace(device, k, bounds[k + 1] - bounds[k], scale) for k in range(K)]
+            side_g.wait_stream(main)  # inputs, node aggregates, workspaces
+            side_s.wait_stream(main)
+            rec("base")
+            ev_g, ev_r = [], []
+            for k in range(K):
+                lo, hi = bounds[k], bounds[k + 1]
+                _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h[lo:].data_ptr(),
+                             all_r[lo:].data_ptr(), etr[lo:].data_ptr() if etr is not None else None, hi - lo,
+                             n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, side_g.cuda_stream)
+                ev_g.append(torch.cuda.Event())
+                ev_g[-1].record(side_g)
+            for k in range(K):
+                lo, hi = bounds[k], bounds[k + 1]
+                self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=False)
+                ev_r.append(torch.cuda.Event())
+                ev_r[-1].record(main)
+            rec("ground")
+            for k in range(K):
+                lo, hi = bounds[k], bounds[k + 1]
+                side_s.wait_event(ev_g[k])
+                side_s.wait_event(ev_r[k])
+                _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
+                             all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None, n_cand[lo:].data_ptr(),
+                             digest[lo:].data_ptr() if digest is not None else None, wss[k].data_ptr(),
+                             wss[k].numel(), scale, side_s.cuda_stream)
+            main.wait_stream(side_s)
+            main.wait_stream(side_g)
+            rec("end")
+            rcs = [_native.lib().rnnl_forward_status(ws.data_ptr(), main.cuda_stream) for ws in wss]
+            bad = [rc for rc in rcs if rc != _native.RNNL_OK]
+            if bad and all(rc == _native.RNNL_ERR_OVERFLOW for rc in bad) and self.capacity_scale < 64:
+                self.capacity_scale *= 2
+                logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
+                continue
+            for rc in bad:
+                _native.check(rc)
+            break
 
     # ------------------------------------------------------------------ autograd (training) path
     def forward_autograd(self, all_h, all_r, edges_to_remove):
