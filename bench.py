@@ -118,6 +118,36 @@ def cpu_baseline(path, model, rows, threads, budget_s=20.0):
                       "%d pthreads), %.1f s" % (sample, threads, sec)}
 
 
+def reference_pytorch_baseline(model, graph, test_set, dev, feature, budget_s=15.0):
+    """The reference PyTorch predictor (its dense torch-eager formulation,
+    oracle/reference_torch.py, op for op after src/data.py:136-173 and
+    src/predictors.py:210-271) on the same GPU, same weights and rules, over
+    the first test batches in TestDataset order until ~budget_s elapse."""
+    from oracle import reference_np as ref
+    from oracle import reference_torch as rt
+    g = ref.Graph(graph.data_path)
+    rules = ref.Rules(datasets.rule_file("FB15k-237"), g.relation_size)
+    rot = ref.load_rotate(datasets.rotate_path("FB15k-237")) if feature == "RotatE" else None
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items() if not k.startswith("RotatE.")}
+    m = rt.Model(sd, {"type": model.type, "num_layers": model.num_layers, "aggregator": model.aggregator,
+                      "entity_feature": feature}, g, rules, dev, rot)
+    b0 = test_set.batches[0]
+    m.forward([x[0] for x in b0], [x[1] for x in b0], None)  # warm-up (allocator, kernels)
+    torch.cuda.synchronize(dev)
+    n, nb, t0 = 0, 0, time.perf_counter()
+    for b in test_set.batches:
+        m.forward([x[0] for x in b], [x[1] for x in b], None)
+        n += len(b)
+        nb += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    torch.cuda.synchronize(dev)
+    sec = time.perf_counter() - t0
+    return {"value": round(n / sec, 2), "unit": "queries/s", "device": "cuda:0 (same GPU)", "kind": "port",
+            "sample": "first %d FB15k-237 test batches (%d queries) in TestDataset order, %.1f s" % (nb, n, sec),
+            "note": "reference PyTorch predictor, dense torch-eager (oracle/reference_torch.py)"}
+
+
 def algorithmic_work(model, graph, rows, threads):
     """Exact per-rule work counts of the SURVEY §8(d) formula from the C oracle:
     F (frontier expansions), T (edge traversals), P ((rule, dest) pairs)."""
@@ -248,6 +278,17 @@ def main():
     # rule-weight Predictor over the same test split (a12)
     extra = {}
     if rank == 0 and world == 1:
+        # the same step with duplicate (h, r) rows computed once (bit-identical
+        # output; forward_rows(dedupe=True)) — reported beside `value`, not as it
+        def dd_step():
+            model.invalidate_cache()
+            return model.forward_rows(h, r, None, dedupe=True)
+        with torch.no_grad():
+            sec = time_forward(dd_step, 3)
+        nu = int(torch.unique(r * graph.entity_size + h).numel())
+        extra["dedup_forward"] = {"queries_per_s": round(nq / sec, 1), "ms": round(sec * 1e3, 3), "rows": nq,
+                                  "distinct_rows": nu,
+                                  "note": "eval rows with equal (h, r) computed once and copied (bit-identical)"}
         with contextlib.redirect_stdout(sys.stderr):
             th, tr, te, nb = train_rows(model.train_set, nq)
         th, tr, te = th.to(dev), tr.to(dev), te.to(dev)
@@ -351,6 +392,8 @@ def main():
     out.update(extra)
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(graph.data_path, model, rows, threads)
+        with contextlib.redirect_stdout(sys.stderr):
+            out["reference_pytorch"] = reference_pytorch_baseline(model, graph, test_set, dev, args.feature)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -509,12 +509,25 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         """Drop cached per-node rule aggregates (recomputed on the next forward)."""
         self._node_cache = {}
 
-    def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False, digest=None, events=None):
+    def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False, digest=None, events=None,
+                     dedupe=False):
         """Forward for any rows (one or many reference batches, mixed relations).
 
         Returns (score (n, |E|) f32, mask (n, |E|) bool[, n_cand (n,) int32]).
         `events`, if a dict, receives torch.cuda.Events bracketing the node
-        aggregate, base-score and grounding kernels (all on the current stream)."""
+        aggregate, base-score and grounding kernels (all on the current stream).
+        `dedupe` (eval rows only): an eval-mode row's output depends on (h, r)
+        alone, so each distinct (h, r) is computed once and its row copied to
+        the duplicates — bit-identical output (the FB15k-237 test split has
+        22,850 distinct (h, r) among 40,932 rows)."""
+        if dedupe and edges_to_remove is None and digest is None and events is None and all_h.numel() > 1:
+            key = all_r.to(torch.int64) * self.num_entities + all_h.to(torch.int64)
+            uniq, inv = torch.unique(key, return_inverse=True)  # sorted by relation, then head
+            if uniq.numel() < key.numel():
+                uh, ur = uniq % self.num_entities, uniq // self.num_entities
+                score, mask, n_cand = self.forward_rows(uh, ur, None, return_ncand=True)
+                score, mask, n_cand = score.index_select(0, inv), mask.index_select(0, inv), n_cand[inv]
+                return (score, mask, n_cand) if return_ncand else (score, mask)
         device = all_h.device
         if device.type != "cuda":
             raise RuntimeError("PredictorPlus runs on the HIP path: move inputs and model to a GPU")

@@ -161,6 +161,23 @@ def test_stream_overlap_is_bit_identical(case, dev):
     np.testing.assert_array_equal(outs[1][3].view(np.uint64), want_d)
 
 
+@pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "umls_emb_pna_rotate", "kinship_lstm_sum_none"])
+def test_dedupe_is_bit_identical(case, dev):
+    """forward_rows(dedupe=True) computes each distinct (h, r) once: same
+    scores, masks and candidate counts as the row-by-row forward."""
+    fx = Fixture(case)
+    model = build_model(fx, dev)
+    test = np.asarray(graph_for(fx.dataset_path()).test_facts, dtype=np.int64)[:4000]
+    h = torch.from_numpy(test[:, 0]).to(dev)
+    r = torch.from_numpy(test[:, 1]).to(dev)
+    with torch.no_grad():
+        a = model.forward_rows(h, r, None, return_ncand=True)
+        b = model.forward_rows(h, r, None, return_ncand=True, dedupe=True)
+    assert len(torch.unique(r * 100000 + h)) < len(h)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+
+
 @pytest.mark.parametrize("data,dim,mrr", [("umls", 200, 0.659847), ("umls", 50, 0.344034),
                                           ("kinship", 1000, 0.637454)])
 def test_rotate_known_answer_mrr(data, dim, mrr, dev):

@@ -127,3 +127,23 @@ def test_oracle_train_loss(case):
     logp = np.log(np.exp(s) / np.exp(s).sum(1, keepdims=True) + 1e-8)
     loss = -(logp[mask] * target[mask]).sum() / max(target[mask].sum(), 1)
     assert abs(loss - float(z["s0/loss"])) <= 2e-5 * abs(loss), (loss, float(z["s0/loss"]))
+
+
+@pytest.mark.parametrize("case", SMALL_CASES + ["fb_lstm_sum_bias"])
+def test_reference_torch_forward(case, fixtures):
+    """The torch-eager restatement (oracle/reference_torch.py, the 'reference
+    PyTorch predictor' bench.py times on the GPU) reproduces the reference's
+    own outputs."""
+    import torch
+    from oracle import reference_torch as rt
+    fx = fixtures(case)
+    m = rt.from_fixture(fx, torch.device("cpu"))
+    n = fx.ncalls if not case.startswith("fb") else 2
+    for k in range(0, n, max(1, n // 8)):
+        c = fx.call(k)
+        score, mask = m.forward(c["h"], c["r"], c["etr"])
+        score, mask = score.numpy(), mask.numpy()
+        np.testing.assert_array_equal(mask, c["mask"])
+        fin = np.isfinite(c["score"])
+        np.testing.assert_array_equal(np.isfinite(score), fin)
+        np.testing.assert_allclose(score[fin], c["score"][fin], atol=2e-5, rtol=0)
