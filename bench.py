@@ -148,6 +148,29 @@ def reference_pytorch_baseline(model, graph, test_set, dev, feature, budget_s=15
             "note": "reference PyTorch predictor, dense torch-eager (oracle/reference_torch.py)"}
 
 
+def isolated_ground_ms(model, graph, h, r, dev):
+    """Device time of the grounding + scoring kernels alone: one untimed
+    one-stream rnnl_predictorplus_forward over all rows into a scratch score."""
+    import ctypes
+    from rnnlogic_amd import _native
+    nq = h.numel()
+    with torch.no_grad():
+        scratch = torch.zeros((nq, graph.entity_size), dtype=torch.float32, device=dev)
+        ncs = torch.empty(nq, dtype=torch.int32, device=dev)
+        params, keep = model._params(dev, model.node_weights(dev))
+        ws = model._workspace(dev, nq, model.capacity_scale)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        e0.record()
+        _native.call("rnnl_predictorplus_forward", model.graph.device_graph(dev), model.native_rules(dev).ptr,
+                     ctypes.byref(params), h.data_ptr(), r.data_ptr(), None, nq, scratch.data_ptr(), None,
+                     ncs.data_ptr(), None, ws.data_ptr(), ws.numel(), model.capacity_scale, st)
+        e1.record()
+        _native.check(_native.lib().rnnl_forward_status(ws.data_ptr(), st))
+        del scratch, keep
+        return e0.elapsed_time(e1)
+
+
 def algorithmic_work(model, graph, rows, threads):
     """Exact per-rule work counts of the SURVEY §8(d) formula from the C oracle:
     F (frontier expansions), T (edge traversals), P ((rule, dest) pairs)."""
@@ -166,6 +189,9 @@ def main():
     ap.add_argument("--feature", default="RotatE", choices=["RotatE", "bias"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--profile-only", action="store_true",
+                    help="only the timed steps (no extra lines, baselines or clock probe): the command the "
+                         "committed rocprofv3 summaries profile, so every launch of a kernel has the same shape")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,31 +251,19 @@ def main():
     tail_ms = float(np.mean([e["ground"].elapsed_time(e["end"]) for e in evs]))
     overlapped = args.feature == "RotatE" and model.overlap_chunks > 1
     n_rot = model.overlap_chunks if overlapped else 1  # RotatE launches per step
-    # the grounding + scoring kernels alone (one untimed one-stream launch into
-    # a scratch score), for their roofline
-    from rnnlogic_amd import _native
-    import ctypes
-    with torch.no_grad():
-        scratch = torch.zeros((nq, graph.entity_size), dtype=torch.float32, device=dev)
-        ncs = torch.empty(nq, dtype=torch.int32, device=dev)
-        node_w = model.node_weights(dev)
-        params, keep = model._params(dev, node_w)
-        ws = model._workspace(dev, nq, model.capacity_scale)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        st = torch.cuda.current_stream(dev).cuda_stream
-        e0.record()
-        _native.call("rnnl_predictorplus_forward", model.graph.device_graph(dev), model.native_rules(dev).ptr,
-                     ctypes.byref(params), h.data_ptr(), r.data_ptr(), None, nq, scratch.data_ptr(), None,
-                     ncs.data_ptr(), None, ws.data_ptr(), ws.numel(), model.capacity_scale, st)
-        e1.record()
-        _native.check(_native.lib().rnnl_forward_status(ws.data_ptr(), st))
-        ground_ms = e0.elapsed_time(e1)
-        del scratch, keep
+    # the grounding + scoring kernels alone (one untimed one-stream launch), for their roofline
+    if not args.profile_only:
+        ground_ms, ground_how = isolated_ground_ms(model, graph, h, r, dev), \
+            "one untimed one-stream launch over all rows (isolated from RotatE)"
+    elif args.feature != "RotatE":
+        ground_ms, ground_how = tail_ms, "timed steps (one stream)"
+    else:
+        ground_ms, ground_how = None, None
 
     # effective shader clock under the RotatE kernel's load (one extra, untimed
     # launch with the kernel's per-block clock stamps on; rnnl_debug_clock)
     clock_ghz = None
-    if args.feature == "RotatE":
+    if args.feature == "RotatE" and not args.profile_only:
         from rnnlogic_amd import _native
         clk = torch.zeros(2, dtype=torch.int64, device=dev)
         _native.call("rnnl_debug_clock", clk.data_ptr())
@@ -266,18 +280,25 @@ def main():
 
     # HBM traffic per launch from the committed PMC summary of this workload
     # (tools/pmc_traffic.py; bench.py cannot read counters itself)
-    traffic = {}
-    tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % args.feature.lower())
-    if os.path.exists(tpath):
+    # (tools/pmc_traffic.py; bench.py cannot read counters itself).  RotatE
+    # kernels: traffic_rotate.json (the overlapped chunk launches, as timed);
+    # grounding kernels: traffic_bias.json (one launch over all rows, as the
+    # isolated grounding time)
+    def load_traffic(name):
+        tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % name)
+        if not os.path.exists(tpath):
+            return {}
         with open(tpath) as f:
             tj = json.load(f)
-        traffic = {k.split("::")[-1].split("<")[0]: v["bytes"] for k, v in tj.get("kernels", {}).items()}
+        return {k.split("::")[-1].split("<")[0]: v["bytes"] for k, v in tj.get("kernels", {}).items()}
+    traffic = load_traffic(args.feature.lower())
+    gtraffic = load_traffic("bias")
 
     # secondary lines (untimed by the driver; not `value`): the train-mode
     # forward with per-row edge removal, and the EM loop's
     # rule-weight Predictor over the same test split (a12)
     extra = {}
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.profile_only:
         # the same step with duplicate (h, r) rows computed once (bit-identical
         # output; forward_rows(dedupe=True)) — reported beside `value`, not as it
         def dd_step():
@@ -325,13 +346,17 @@ def main():
     D = model.RotatE.emb_dim if args.feature == "RotatE" else 0
     rotate_flops = 7.0 * nq * E * D
     rotate_bytes = 8.0 * D * E * ((nq + 15) // 16) + 8.0 * D * nq + 4.0 * nq * E
-    gt = [traffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_kernel")]
+    if ground_ms is None:  # --profile-only with the RotatE overlap: no isolated grounding time
+        ground_ms = float("nan")
+    gt = [gtraffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_kernel")]
     gt = sum(x for x in gt if x) or None
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
               "traffic": gt, "kernel": "ground_kernel + score_kernel", "ms": round(ground_ms, 3),
-              "measured": "one untimed one-stream launch over all rows (isolated from RotatE)",
+              "measured": ground_how,
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
+    if ground_ms != ground_ms:  # nan
+        ground = None
     if args.feature == "RotatE":
         # per launch: n_rot launches of nq / n_rot rows each on the main stream
         ach = rotate_flops / (base_ms * 1e-3) / 1e12
@@ -361,7 +386,7 @@ def main():
                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(x_bytes / (base_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                             "alg_bytes": x_bytes}
-        dominant = roof if base_ms >= ground_ms else ground
+        dominant = roof if not (ground_ms > base_ms) else ground
     else:
         dominant = ground
     out = {
@@ -390,7 +415,7 @@ def main():
         "roofline_grounding": ground,
     }
     out.update(extra)
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and not args.profile_only and world == 1:
         out["cpu_baseline"] = cpu_baseline(graph.data_path, model, rows, threads)
         with contextlib.redirect_stdout(sys.stderr):
             out["reference_pytorch"] = reference_pytorch_baseline(model, graph, test_set, dev, args.feature)
