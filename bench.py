@@ -249,7 +249,7 @@ def main():
     nodes_ms = float(np.mean([e["start"].elapsed_time(e["base"]) for e in evs]))
     base_ms = float(np.mean([e["base"].elapsed_time(e["ground"]) for e in evs]))
     tail_ms = float(np.mean([e["ground"].elapsed_time(e["end"]) for e in evs]))
-    overlapped = args.feature == "RotatE" and model.overlap_chunks > 1
+    overlapped = args.feature == "RotatE" and model.overlap
     n_rot = model.overlap_chunks if overlapped else 1  # RotatE launches per step
     # the grounding + scoring kernels alone (one untimed one-stream launch), for their roofline
     if not args.profile_only:

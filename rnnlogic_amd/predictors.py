@@ -398,6 +398,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # scoring pass starts as soon as its RotatE rows are written
         # (DESIGN.md "Stream overlap").  1 disables the overlap.
         self.overlap_chunks = int(os.environ.get("RNNL_OVERLAP_CHUNKS", "2"))
+        self.overlap = os.environ.get("RNNL_OVERLAP", "1") != "0"
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -546,7 +547,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        if self.entity_feature == "RotatE" and self.overlap_chunks > 1 and nq >= 2 * self.overlap_chunks:
+        if self.entity_feature == "RotatE" and self.overlap and nq >= 2 * self.overlap_chunks:
             self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec)
             del keep
             return (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device), n_cand) \
