@@ -261,6 +261,15 @@ int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *
                       int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
                       size_t workspace_bytes, void *stream);
 
+/* ------------------------------------------------------ training batches --
+ * Device-side TrainDataset rows (reference src/data.py:201-219, the target
+ * part): out (n_rows x width, f32, row-major) = multi-hot of the value list
+ * of row_keys[i] in a CSR map (keys ascending, offs n_keys + 1, vals int32).
+ * A key not in the map gives a zero row.  With keys = r * |E| + h and the
+ * hr2o lists this is TrainDataset's `target`. */
+int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
+                   const int64_t *row_keys, int32_t n_rows, int32_t width, float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

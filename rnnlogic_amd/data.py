@@ -190,6 +190,64 @@ class TrainDataset(Dataset):
         return all_h, all_r, all_t, target, torch.LongTensor(edges_to_remove)
 
 
+class DeviceTrainBatches(object):
+    """TrainDataset rows built on the device: item `idx`
+    equals `train_set[idx]` — (all_h, all_r, all_t, target, edges_to_remove),
+    reference src/data.py:201-219 — as tensors on `device`.  The dense
+    multi-hot target comes from rnnl_multi_hot over a CSR of hr2o (keys
+    r * |E| + h, built once); the row's own relation-local edge id
+    (relation2ht2index) from a sorted key table of all train edges.  Follows
+    `train_set.batches`, so a make_batches() reshuffle is seen."""
+
+    def __init__(self, train_set, device):
+        self.train_set = train_set
+        self.device = torch.device(device)
+        g = train_set.graph
+        E = g.entity_size
+        keys = np.fromiter(g.hr2o.keys(), dtype=np.int64, count=len(g.hr2o))
+        order = np.argsort(keys, kind="stable")
+        lists = list(g.hr2o.values())
+        lens = np.asarray([len(lists[i]) for i in order], dtype=np.int64)
+        offs = np.zeros(len(order) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        vals = np.fromiter((t for i in order for t in lists[i]), dtype=np.int32, count=int(offs[-1]))
+        self.keys = torch.from_numpy(keys[order]).to(self.device)
+        self.offs = torch.from_numpy(offs).to(self.device)
+        self.vals = torch.from_numpy(vals).to(self.device)
+        # relation-local edge ids: key (r * |E| + t) * |E| + h -> id, sorted
+        ek, ev = [], []
+        for r, m in enumerate(g.relation2ht2index):
+            if m:
+                ht = np.fromiter(m.keys(), dtype=np.int64, count=len(m))
+                ek.append(r * E * E + ht)
+                ev.append(np.fromiter(m.values(), dtype=np.int64, count=len(m)))
+        ek = np.concatenate(ek) if ek else np.zeros(0, np.int64)
+        ev = np.concatenate(ev) if ev else np.zeros(0, np.int64)
+        o = np.argsort(ek, kind="stable")
+        self.edge_keys = torch.from_numpy(ek[o]).to(self.device)
+        self.edge_ids = torch.from_numpy(ev[o]).to(self.device)
+
+    def __len__(self):
+        return len(self.train_set)
+
+    def __getitem__(self, idx):
+        g = self.train_set.graph
+        E = g.entity_size
+        hrt = torch.tensor(self.train_set.batches[idx], dtype=torch.int64).view(-1, 3).to(self.device,
+                                                                                        non_blocking=True)
+        all_h, all_r, all_t = hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
+        B = all_h.numel()
+        target = torch.empty((B, E), dtype=torch.float32, device=self.device)
+        row_keys = (all_r * E + all_h).contiguous()
+        _native.call("rnnl_multi_hot", self.keys.data_ptr(), self.offs.data_ptr(), self.vals.data_ptr(),
+                     self.keys.numel(), row_keys.data_ptr(), B, E, target.data_ptr(),
+                     torch.cuda.current_stream(self.device).cuda_stream)
+        ekey = (all_r * E + all_t) * E + all_h
+        pos = torch.searchsorted(self.edge_keys, ekey).clamp(max=max(self.edge_keys.numel() - 1, 0))
+        etr = self.edge_ids[pos]
+        return all_h, all_r, all_t, target, etr
+
+
 class _EvalDataset(Dataset):
     facts_attr = None
     filter_attr = None

@@ -22,6 +22,20 @@ from torch import nn
 from torch.utils import data as torch_data
 
 from . import comm
+from .data import DeviceTrainBatches
+
+
+class _SizedIter(object):
+    """len() + iteration over fn(index) for the sampler's indices."""
+
+    def __init__(self, sampler, fn):
+        self.sampler, self.fn = sampler, fn
+
+    def __len__(self):
+        return len(self.sampler)
+
+    def __iter__(self):
+        return (self.fn(i) for i in self.sampler)
 
 
 class TrainerPredictor(object):
@@ -57,10 +71,20 @@ class TrainerPredictor(object):
         self.test_set = test_set
         self.optimizer = optimizer
         self.scheduler = scheduler
+        self.device_batches = True  # GPU: training batches built on the device (f3)
 
     # ------------------------------------------------------------------ train
     def _loader(self, dataset):
+        """(sampler, iterable of batches).  On a GPU the training batches are
+        built on the device (data.DeviceTrainBatches, same tensors as
+        TrainDataset.__getitem__) in the sampler's order; otherwise the
+        reference's DataLoader."""
         sampler = torch_data.DistributedSampler(dataset, self.world_size, self.rank)
+        if self.device.type == "cuda" and dataset is self.train_set and self.device_batches:
+            if getattr(self, "_dev_batches", None) is None:
+                self._dev_batches = DeviceTrainBatches(self.train_set, self.device)
+            dev = self._dev_batches
+            return sampler, _SizedIter(sampler, lambda i: [x.unsqueeze(0) for x in dev[i]])
         return sampler, torch_data.DataLoader(dataset, 1, sampler=sampler, num_workers=self.num_worker)
 
     def train(self, batch_per_epoch, smoothing, print_every):

@@ -117,3 +117,24 @@ def test_trainer_end_to_end_umls(dev):
     solver.train(batch_per_epoch=8, smoothing=0.2, print_every=4)
     mrr1 = solver.evaluate("valid", expectation=True)
     assert 0.0 < mrr1 <= 1.0
+
+
+@pytest.mark.parametrize("data", ["umls", "FB15k-237"])
+def test_device_train_batches_match_dataset(data, dev):
+    """data.DeviceTrainBatches (multi-hot target by rnnl_multi_hot, edge ids by
+    a device key lookup) returns exactly TrainDataset.__getitem__'s tensors
+    (reference src/data.py:201-219), before and after a reshuffle."""
+    import random
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import DeviceTrainBatches, KnowledgeGraph, TrainDataset
+    random.seed(3)
+    graph = KnowledgeGraph(datasets.materialize(data))
+    ts = TrainDataset(graph, 32)
+    db = DeviceTrainBatches(ts, dev)
+    for rnd in range(2):
+        for idx in list(range(0, len(ts), max(1, len(ts) // 40)))[:40]:
+            want = ts[idx]
+            got = db[idx]
+            for w, g in zip(want, got):
+                np.testing.assert_array_equal(g.cpu().numpy(), w.numpy())
+        ts.make_batches()

@@ -117,3 +117,23 @@ def test_grounding_api_matches_golden_counts(fixtures):
             b, e = np.nonzero(x)
             got.append(np.stack([np.full_like(b, i), b, e, x[b, e]], 1))
         np.testing.assert_array_equal(np.concatenate(got), c["coo"].astype(np.int64))
+
+
+def test_device_train_batches_tables():
+    """The key tables behind data.DeviceTrainBatches (built on the host,
+    uploaded once): hr2o CSR and the relation-local edge id map."""
+    import numpy as np
+    import torch
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import DeviceTrainBatches, KnowledgeGraph, TrainDataset
+    graph = KnowledgeGraph(datasets.materialize("umls"))
+    db = DeviceTrainBatches(TrainDataset(graph, 32), torch.device("cpu"))
+    keys, offs, vals = db.keys.numpy(), db.offs.numpy(), db.vals.numpy()
+    assert (np.diff(keys) > 0).all() and len(offs) == len(keys) + 1
+    E = graph.entity_size
+    for h, r, t in graph.train_facts[::97]:
+        i = np.searchsorted(keys, r * E + h)
+        assert keys[i] == r * E + h
+        assert list(vals[offs[i]:offs[i + 1]]) == graph.hr2o[graph.encode_hr(h, r)]
+        j = np.searchsorted(db.edge_keys.numpy(), (r * E + t) * E + h)
+        assert db.edge_ids.numpy()[j] == graph.relation2ht2index[r][graph.encode_ht(h, t)]
