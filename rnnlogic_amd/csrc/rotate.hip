@@ -330,6 +330,10 @@ __global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restri
                                                            int accumulate, unsigned long long *clk) {
   const int64_t Ep = ent_pad(E);
   int et, qt;
+#ifdef RNNL_ROT_LDS_PAD  // diagnostic: cap the blocks per CU through LDS
+  __shared__ volatile char pad[RNNL_ROT_LDS_PAD];
+  if (threadIdx.x == 0) pad[0] = 0;
+#endif
   if (!xcd_tile((int)(Ep / RB), (nq + DQ - 1) / DQ, et, qt)) return;
   ClockStamp cs;
   cs.begin(clk);
