@@ -43,6 +43,7 @@ extern "C" {
 
 typedef struct rnnl_graph_s *rnnl_graph;
 typedef struct rnnl_rules_s *rnnl_rules;
+typedef struct rnnl_miner_s *rnnl_miner;
 
 const char *rnnl_last_error(void);
 int rnnl_version(void);
@@ -269,6 +270,25 @@ int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *
  * hr2o lists this is TrainDataset's `target`. */
 int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
                    const int64_t *row_keys, int32_t n_rows, int32_t width, float *out, void *stream);
+
+/* ---------------------------------------------------------- rule mining --
+ * The reference miner's RuleMiner::search (miner/rnnlogic.cpp:505-589 with
+ * KnowledgeGraph::rule_search :350-382) on the GPU: for every train triple
+ * (h, r, t), every relation path of length <= max_length (1..3) from h to t
+ * with the triple's own edge removed gives the rule r <- path; the pool is the
+ * set over all triples minus r <- r.
+ *   rnnl_miner_create: host triples (n x 3 int32, train-file order); R < 2^15.
+ *   rnnl_rule_search: table = device scratch of table_cap (power of two)
+ *     uint64 slots; rules_out receives the distinct rules as keys
+ *     head<<47 | len<<45 | b1<<30 | b2<<15 | b3 (numeric order == the
+ *     reference's order); counters (4 x uint64, device): [1] != 0 if the table
+ *     was too small (retry larger), [2] = number of rules (may exceed out_cap:
+ *     retry with a larger rules_out). */
+int rnnl_miner_create(const int32_t *hrt, int64_t n_triples, int32_t n_entities, int32_t n_relations,
+                      rnnl_miner *out);
+int rnnl_miner_destroy(rnnl_miner m);
+int rnnl_rule_search(rnnl_miner m, int32_t max_length, uint64_t *table, int64_t table_cap, uint64_t *rules_out,
+                     int64_t out_cap, uint64_t *counters, void *stream);
 
 #ifdef __cplusplus
 }

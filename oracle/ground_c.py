@@ -158,5 +158,29 @@ class RefMiner:
             os.close(saved)
         return sec, n.value
 
+    def rule_search(self, max_length, threads=1, cap=1 << 26):
+        """RuleMiner::search (rnnlogic.cpp:505-589) over all train triples:
+        (rules [(head, body tuple)] in the reference's order, seconds)."""
+        out = np.empty(cap, np.int32)
+        sec = ctypes.c_double(0.0)
+        self.lib.ref_rule_search.restype = ctypes.c_longlong
+        import sys
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            n = self.lib.ref_rule_search(_P(self.kg), int(max_length), int(threads), _ptr(out),
+                                         ctypes.c_longlong(cap), ctypes.byref(sec))
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+        assert n >= 0, "cap too small"
+        rules, k = [], 0
+        while k < n:
+            hd, ln = int(out[k]), int(out[k + 1])
+            rules.append((hd, tuple(int(x) for x in out[k + 2:k + 2 + ln])))
+            k += 2 + ln
+        return rules, sec.value
+
     def close(self):
         self.lib.ref_kg_free(_P(self.kg))

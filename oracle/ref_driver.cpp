@@ -2,7 +2,7 @@
 //
 // Thin C-ABI shim over the *reference* C++ miner, compiled from the reference
 // sources where they lie (/root/reference/miner/rnnlogic.cpp) by oracle/Makefile
-// into oracle/_ref/libref_miner.so.  It exposes exactly two things:
+// into oracle/_ref/libref_miner.so.  It exposes exactly three things:
 //
 //   * ref_rule_destination — KnowledgeGraph::rule_destination
 //     (reference miner/rnnlogic.cpp:412-442): per-(query, rule) path counts with
@@ -10,6 +10,8 @@
 //   * ref_out_test_timed — ReasoningPredictor::out_test (rnnlogic.cpp:1262-1406):
 //     the miner's multi-threaded grounding over (a prefix of) the test split.
 //     Used only by bench.py's cpu_baseline leg (kind "reference").
+//   * ref_rule_search — RuleMiner::search (rnnlogic.cpp:505-589): the rule
+//     pool the GPU miner (rnnl_rule_search) must reproduce; tests/ only.
 //
 // Nothing here re-implements the algorithm; it only marshals plain arrays into
 // the reference's own classes.
@@ -104,6 +106,34 @@ double ref_out_test_timed(void *kgp, const int *rules_flat, int n_rules, int thr
   if (out_len) *out_len = static_cast<long long>(data.size());
   delete[] rel2rules;
   return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// RuleMiner::search (reference miner/rnnlogic.cpp:505-589, rule_search at
+// :350-382) over ALL train triples (portion 1) with `threads` pthreads.  The
+// mined pool is written flat as (head, len, body...) in the reference's own
+// order (per head relation, std::set<Rule> order).  Returns the number of ints
+// written, or -(needed) if cap is too small; *seconds gets the search time.
+long long ref_rule_search(void *kgp, int max_length, int threads, int *out_flat, long long cap, double *seconds) {
+  KG *kg = static_cast<KG *>(kgp);
+  RuleMiner rm;
+  rm.init_knowledge_graph(kg);
+  auto t0 = std::chrono::steady_clock::now();
+  rm.search(max_length, 1.0, threads);
+  auto t1 = std::chrono::steady_clock::now();
+  if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+  std::vector<Rule> *rel2rules = rm.get_logic_rules();
+  long long n = 0;
+  for (int r = 0; r < kg->get_relation_size(); ++r)
+    for (const Rule &rule : rel2rules[r]) n += 2 + rule.type;
+  if (n > cap) return -n;
+  long long k = 0;
+  for (int r = 0; r < kg->get_relation_size(); ++r)
+    for (const Rule &rule : rel2rules[r]) {
+      out_flat[k++] = rule.r_head;
+      out_flat[k++] = rule.type;
+      for (int b : rule.r_body) out_flat[k++] = b;
+    }
+  return n;
 }
 
 }  // extern "C"

@@ -21,6 +21,7 @@ Reference anchors (file:line in /root/reference):
   func_to_node_pna      src/layers.py:89-126
   mlp                   src/layers.py:35-51
   rotate_forward        src/embedding.py:28-70
+  rule_search_pool      miner/rnnlogic.cpp:350-382, 505-589 (the miner's rule search)
   rank_metrics          src/trainer.py:189-238
 """
 import json
@@ -227,6 +228,39 @@ def rotate_forward(eemb, remb, gamma, dim, h, r):
     dim_ = im[:, None, :] - eemb[None, :, dim:]
     dist = np.sqrt(dre * dre + dim_ * dim_).sum(-1, dtype=np.float32)
     return (np.float32(gamma) - dist).astype(np.float32)
+
+
+def rule_search_pool(g, max_length):
+    """RuleMiner::search (miner/rnnlogic.cpp:505-589) with the DFS of
+    KnowledgeGraph::rule_search (:350-382): for every train triple (h, r, t),
+    every relation path of length <= max_length from h that reaches t (a walk
+    stops at t), the triple's own edge skipped at every hop, is the rule
+    r <- path; r <- r is dropped (:532-539).  Returns [(head, body tuple)] per
+    head in std::set<Rule> order (length, then body).  Pure Python: small
+    graphs only."""
+    adj = {}
+    for h, r, t in g.train_facts:
+        adj.setdefault(h, []).append((r, t))
+    pool = [set() for _ in range(g.relation_size)]
+
+    def dfs(e, goal, path, head, removed):
+        if e == goal:
+            pool[head].add(tuple(path))
+            return
+        if len(path) == max_length:
+            return
+        for rel, nxt in adj.get(e, ()):
+            if (e, rel, nxt) == removed:
+                continue
+            dfs(nxt, goal, path + [rel], head, removed)
+
+    for h, r, t in g.train_facts:
+        found = set()
+        pool_r, pool[r] = pool[r], found
+        dfs(h, t, [], r, (h, r, t))
+        found.discard((r,))  # the per-triple set loses r <- r before the merge
+        pool[r] = pool_r | found
+    return [(hd, b) for hd in range(g.relation_size) for b in sorted(pool[hd], key=lambda x: (len(x), x))]
 
 
 class Rules:

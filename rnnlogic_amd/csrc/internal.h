@@ -23,6 +23,15 @@ struct GraphDev {
   const int32_t *edge_dst = nullptr;
 };
 
+// Rule miner graph (mine.hip): out-edges grouped by source, in-edges grouped
+// by target with sources ascending, and the train triples themselves.
+struct MinerDev {
+  int32_t E = 0, R = 0, n = 0;
+  const int32_t *out_off = nullptr, *out_dst = nullptr, *out_rel = nullptr;  // E + 1, n, n
+  const int32_t *in_off = nullptr, *in_src = nullptr, *in_rel = nullptr;     // E + 1, n, n
+  const int32_t *th = nullptr, *tr = nullptr, *tt = nullptr;                 // n
+};
+
 // Rule bodies as one prefix trie per head relation.  Node ids are global;
 // the nodes of one head are contiguous, numbered breadth-first, so the
 // children of a node are contiguous too.  Node 0 of a head is its root

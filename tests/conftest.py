@@ -52,7 +52,21 @@ class Fixture:
         return datasets.rotate_path(self.cfg["data"], int(emb.split(":")[1]))
 
 
-ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("_", "train_", "pred_")))
+ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN)
+                   if f.endswith(".npz") and not f.startswith(("_", "train_", "pred_", "rules_")))
+# reference miner rule pools (tools/make_golden_rules.py)
+RULE_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("rules_") and f.endswith(".npz"))
+
+
+def golden_rules(case):
+    """[(head, body tuple)] of a tests/golden/rules_*.npz pool, reference order."""
+    flat = np.load(os.path.join(GOLDEN, case + ".npz"))["flat"].astype(np.int64)
+    rules, k = [], 0
+    while k < len(flat):
+        hd, ln = int(flat[k]), int(flat[k + 1])
+        rules.append((hd, tuple(int(x) for x in flat[k + 2:k + 2 + ln])))
+        k += 2 + ln
+    return rules
 # training-path fixtures (tools/make_golden_train.py)
 TRAIN_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("train_") and f.endswith(".npz"))
 TRAIN_SPECS = {  # dataset, PredictorPlus kwargs, RotatE dir — mirrors tools/make_golden_train.py CASES

@@ -147,3 +147,13 @@ def test_reference_torch_forward(case, fixtures):
         fin = np.isfinite(c["score"])
         np.testing.assert_array_equal(np.isfinite(score), fin)
         np.testing.assert_allclose(score[fin], c["score"][fin], atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("data", ["umls", "kinship"])
+def test_rule_search_restatement_vs_reference_pool(data):
+    """The Python restatement of the miner's rule search equals the reference
+    miner's own pool (tests/golden/rules_*_L2.npz, tools/make_golden_rules.py)."""
+    from conftest import golden_rules
+    from rnnlogic_amd import datasets
+    g = ref.Graph(datasets.materialize(data))
+    assert ref.rule_search_pool(g, 2) == golden_rules("rules_%s_L2" % data)
