@@ -65,6 +65,7 @@ struct MineSmem {
 __device__ __forceinline__ void global_insert(uint64_t key, unsigned long long *table, int64_t cap,
                                               unsigned long long *flags) {
   uint64_t h = key_hash(key) & (uint64_t)(cap - 1);
+  if (__hip_atomic_load(&flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // already too small
   for (int p = 0; p < GPROBE; ++p) {
     const unsigned long long v = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v == key) return;
@@ -135,7 +136,11 @@ __global__ __launch_bounds__(MB) void mine_kernel(MinerDev m, int L, unsigned lo
 #pragma unroll 1
   while (true) {
     __syncthreads();
-    if (tid == 0) S.q = (int)atomicAdd(&flags[0], 1ull);
+    if (tid == 0) {
+      // a full set ends the search early: the caller retries with a larger table
+      const bool full = __hip_atomic_load(&flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      S.q = full ? m.n : (int)atomicAdd(&flags[0], 1ull);
+    }
     __syncthreads();
     const int q = S.q;
     if (q >= m.n) break;

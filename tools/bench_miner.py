@@ -27,6 +27,7 @@ def main():
         with contextlib.redirect_stdout(io.StringIO()):
             g = KnowledgeGraph(datasets.materialize(data))
         m = RuleMiner(g, dev)
+        print("mining %s L=%s ..." % (data, L), flush=True)
         m.search(int(L))  # warm-up (and table sizing)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
