@@ -38,6 +38,10 @@ constexpr int BS = 256;      // threads per workgroup (scoring kernels)
 #endif
 constexpr int GBS = RNNL_GBS;  // threads per grounding workgroup
 constexpr int GNW = GBS / 64;  // its waves
+#ifndef RNNL_EPT
+#define RNNL_EPT 1
+#endif
+constexpr int EPT = RNNL_EPT;  // phase-A edges per lane per pass
 #ifndef RNNL_HBITS
 #define RNNL_HBITS 12
 #endif
@@ -385,18 +389,33 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
         __syncthreads();
         PSTAMP(4);
         const int nit = min(GBS, NI - ib);
-        for (int eb = 0; eb < NE; eb += GBS) {
-          const int j = eb + tid;
-          if (j < NE) {
-            const int it = upper_idx(S.edge_off, nit, j);
-            const int tt = p.g.col[S.it_beg[it] + (j - S.edge_off[it])];
-            const int fl = S.it_flags[it];
-            if (!((fl & 4) && tt == rm_dst)) {
-              const int child = S.it_child[it];
-              const uint32_t c = S.it_c[it];
-              if (fl & 1) emit_contrib(S, sl, p.pcap, tt, child, c);
-              if (fl & 2) {
-                if (!hash_add(S, (child - root) * E + tt, c)) emit_frontier(S, sl, nxt, p.fcap, child, tt, c);
+        // EPT edges per lane per pass: their binary searches and col loads are
+        // independent, so EPT loads are in flight before the first is used
+        for (int eb = 0; eb < NE; eb += GBS * EPT) {
+          int ev_it[EPT], ev_t[EPT];
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) {
+            const int j = eb + k * GBS + tid;
+            ev_it[k] = -1;
+            if (j < NE) {
+              const int it = upper_idx(S.edge_off, nit, j);
+              ev_it[k] = it;
+              ev_t[k] = p.g.col[S.it_beg[it] + (j - S.edge_off[it])];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) {
+            const int it = ev_it[k];
+            if (it >= 0) {
+              const int tt = ev_t[k];
+              const int fl = S.it_flags[it];
+              if (!((fl & 4) && tt == rm_dst)) {
+                const int child = S.it_child[it];
+                const uint32_t c = S.it_c[it];
+                if (fl & 1) emit_contrib(S, sl, p.pcap, tt, child, c);
+                if (fl & 2) {
+                  if (!hash_add(S, (child - root) * E + tt, c)) emit_frontier(S, sl, nxt, p.fcap, child, tt, c);
+                }
               }
             }
           }
