@@ -389,6 +389,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self.RotatE = RotatE(embedding_path)
         self._native_rules = {}
         self._node_cache = {}
+        self._tok_cache = {}
         self._ws = {}
         self._ws_chunks = {}
         self._side = {}
@@ -417,6 +418,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             nn.init.kaiming_uniform_(self.rule_emb, a=math.sqrt(5), mode="fan_in")
         self._native_rules = {}
         self._node_cache = {}
+        self._tok_cache = {}
 
     def encode_rules(self, rule_features):
         """LSTM/GRU/RNN output at each rule's last token (predictors.py:201-208)."""
@@ -449,11 +451,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                                         for k in range(L)]).contiguous()
         w_ih, w_hh, b_ih, b_hh = cat("weight_ih"), cat("weight_hh"), cat("bias_ih"), cat("bias_hh")
         vocab = self.vocab_emb.weight.detach().float().contiguous()
-        key = (self._device_index(device), "tok")
-        tok = self._node_cache.get(key)
+        # rule tokens depend only on the rule set: cached across invalidate_cache()
+        # (a pageable host->device copy per forward costs 1-20 ms depending on the host)
+        key = self._device_index(device)
+        tok = self._tok_cache.get(key)
         if tok is None:
-            tok = self.rule_features.to(device=device, dtype=torch.int32).contiguous()
-            self._node_cache[key] = tok
+            tok = self.rule_features.to(dtype=torch.int32).contiguous().to(device)
+            self._tok_cache[key] = tok
         out = torch.empty((self.num_rules, self.hidden_dim), dtype=torch.float32, device=device)
         _native.call("rnnl_lstm_encode", vocab.data_ptr(), w_ih.data_ptr(), w_hh.data_ptr(), b_ih.data_ptr(),
                      b_hh.data_ptr(), L, self.hidden_dim, tok.data_ptr(), self.num_rules, tok.size(1),
