@@ -153,11 +153,14 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
 int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, const int64_t *all_h,
                               const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries,
                               int32_t *n_cand, void *workspace, size_t workspace_bytes, int32_t capacity_scale,
-                              void *stream);
+                              int32_t workgroups, void *stream);
 int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p, const int64_t *all_h,
                              const int64_t *all_r, int32_t n_queries, float *score, uint8_t *mask, int32_t *n_cand,
                              uint64_t *digest, void *workspace, size_t workspace_bytes, int32_t capacity_scale,
-                             void *stream);
+                             int32_t workgroups, void *stream);
+/* workgroups: cap on the persistent workgroups of the launch (0 = the full
+ * default occupancy); a smaller grid leaves room on the CUs for a kernel on
+ * another stream (the RotatE overlap). */
 /* After a forward: RNNL_OK, or RNNL_ERR_OVERFLOW if any query exceeded the
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */

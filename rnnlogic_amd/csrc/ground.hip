@@ -1512,11 +1512,14 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
 }
 
 // Kernel sequences shared by the one-call forward and its two halves.
-static void launch_ground(const KParams &p, int agg, hipStream_t st) {
+// `grid` caps the persistent workgroups (0: one per workspace slot, the
+// default occupancy); a smaller grid leaves CUs to a concurrent kernel.
+static void launch_ground(const KParams &p, int agg, hipStream_t st, int grid = 0) {
+  const unsigned g = (unsigned)(grid > 0 ? std::min(grid, p.nslots) : p.nslots);
   if (agg == RNNL_AGG_SUM)
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(g), dim3(GBS), 0, st, p);
   else
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(p.nslots), dim3(GBS), 0, st, p);
+    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(g), dim3(GBS), 0, st, p);
 }
 
 static void set_score_params(KParams &p, const rnnl_predictor_params *pp, float *score, uint8_t *mask,
@@ -1538,7 +1541,7 @@ static void set_score_params(KParams &p, const rnnl_predictor_params *pp, float 
   p.digest = digest;
 }
 
-static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st) {
+static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int grid = 0) {
   const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
@@ -1546,7 +1549,8 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st) {
     // staged path while the largest head's leaves fit the LDS budget
     const int64_t base_lds = (int64_t)(WL<RNNL_AGG_SUM>::N + 128) * 4;
     const int64_t stage = sum_stage_bytes(r->d.max_leaves, r->d.max_head_nodes);
-    const unsigned sgrid = (unsigned)std::min<int64_t>((nq + QCHUNK - 1) / QCHUNK, (int64_t)NUM_CU * RNNL_SCORE_WG_PER_CU);
+    const unsigned sgrid = (unsigned)std::min<int64_t>(
+        (nq + QCHUNK - 1) / QCHUNK, grid > 0 ? (int64_t)grid : (int64_t)NUM_CU * RNNL_SCORE_WG_PER_CU);
 #ifndef RNNL_STAGE_LIMIT
 #define RNNL_STAGE_LIMIT 0  // staging measured slower (lower occupancy); kept for A/B
 #endif
@@ -1592,7 +1596,7 @@ int rnnl_predictorplus_forward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_
 
 int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, const int64_t *all_h,
                               const int64_t *all_r, const int64_t *etr, int32_t nq, int32_t *n_cand, void *ws,
-                              size_t ws_bytes, int32_t scale, void *stream) {
+                              size_t ws_bytes, int32_t scale, int32_t workgroups, void *stream) {
   if (aggregator != RNNL_AGG_SUM && aggregator != RNNL_AGG_PNA) {
     set_error("rnnl_predictorplus_ground: bad aggregator");
     return RNNL_ERR_INVALID;
@@ -1605,14 +1609,15 @@ int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, co
   RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
   if (nq == 0) return RNNL_OK;
   p.agg = aggregator;
-  launch_ground(p, aggregator, st);
+  launch_ground(p, aggregator, st, workgroups);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
 
 int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
                              const int64_t *all_r, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
-                             uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, void *stream) {
+                             uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t workgroups,
+                             void *stream) {
   if (bad_params(pp, score) || !n_cand) {
     set_error("rnnl_predictorplus_score: bad arguments");
     return RNNL_ERR_INVALID;
@@ -1625,7 +1630,7 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
   set_score_params(p, pp, score, mask, digest);
   hipStream_t st = (hipStream_t)stream;
   RNNL_HIP_CHECK(hipMemsetAsync(p.ws + 4 * H_DEQUEUE2, 0, 4, st));  // the scoring dequeue counter
-  launch_score(p, r, st);
+  launch_score(p, r, st, workgroups);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

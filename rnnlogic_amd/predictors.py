@@ -394,12 +394,17 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._ws_chunks = {}
         self._side = {}
         self.capacity_scale = 1
-        # RotatE base score: rows are split into this many chunks; the grounding
-        # runs on a side stream beside the RotatE kernel and each chunk's
-        # scoring pass starts as soon as its RotatE rows are written
-        # (DESIGN.md "Stream overlap").  1 disables the overlap.
-        self.overlap_chunks = int(os.environ.get("RNNL_OVERLAP_CHUNKS", "2"))
+        # RotatE base score: the grounding runs on a side stream beside the
+        # RotatE kernel; rows may be split into chunks so that each chunk's
+        # scoring pass starts as soon as its RotatE rows are written (DESIGN.md
+        # "Stream overlap": 2 chunks measured 2-3 % faster than 1 but with an
+        # occasional one-step stall early in a process; 1 chunk is stable).
+        self.overlap_chunks = int(os.environ.get("RNNL_OVERLAP_CHUNKS", "1"))
         self.overlap = os.environ.get("RNNL_OVERLAP", "1") != "0"
+        # persistent workgroups of the side-stream kernels (0 = full occupancy):
+        # fewer leave RotatE its waves (it needs ~6 per SIMD to reach its floor)
+        self.overlap_ground_wg = int(os.environ.get("RNNL_OVERLAP_GROUND_WG", "0"))
+        self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "0"))
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -625,7 +630,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 lo, hi = bounds[k], bounds[k + 1]
                 _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h[lo:].data_ptr(),
                              all_r[lo:].data_ptr(), etr[lo:].data_ptr() if etr is not None else None, hi - lo,
-                             n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, side_g.cuda_stream)
+                             n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_ground_wg,
+                             side_g.cuda_stream)
                 ev_g.append(torch.cuda.Event())
                 ev_g[-1].record(side_g)
             for k in range(K):
@@ -641,10 +647,14 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
                              all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None, n_cand[lo:].data_ptr(),
                              digest[lo:].data_ptr() if digest is not None else None, wss[k].data_ptr(),
-                             wss[k].numel(), scale, side_s.cuda_stream)
+                             wss[k].numel(), scale, self.overlap_score_wg, side_s.cuda_stream)
             main.wait_stream(side_s)
             main.wait_stream(side_g)
             rec("end")
+            # the host waits for the result anyway: drain the side streams too,
+            # so no cross-stream wait is left pending into the next call
+            side_g.synchronize()
+            side_s.synchronize()
             rcs = [_native.lib().rnnl_forward_status(ws.data_ptr(), main.cuda_stream) for ws in wss]
             bad = [rc for rc in rcs if rc != _native.RNNL_OK]
             if bad and all(rc == _native.RNNL_ERR_OVERFLOW for rc in bad) and self.capacity_scale < 64:
