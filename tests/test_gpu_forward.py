@@ -144,21 +144,22 @@ def test_stream_overlap_is_bit_identical(case, dev):
     h = torch.from_numpy(test[:, 0]).to(dev)
     r = torch.from_numpy(test[:, 1]).to(dev)
     outs = []
-    for chunks in (1, 4, 7):
-        model.overlap_chunks = chunks
+    for chunks in (0, 1, 4, 7):  # 0: one stream, no overlap
+        model.overlap = chunks > 0
+        model.overlap_chunks = max(chunks, 1)
         dig = torch.zeros(len(h), dtype=torch.int64, device=dev)
         with torch.no_grad():
             score, mask, n = model.forward_rows(h, r, None, return_ncand=True, digest=dig)
         torch.cuda.synchronize()
         outs.append((score.cpu().numpy(), mask.cpu().numpy(), n.cpu().numpy(), dig.cpu().numpy()))
-    model.overlap_chunks = 4
+    model.overlap, model.overlap_chunks = True, 1
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             np.testing.assert_array_equal(a, b)
     g, orc = oracle_for(fx)
     want_d, want_n = orc.digests(test[:, 0], test[:, 1])
-    np.testing.assert_array_equal(outs[1][2], want_n)
-    np.testing.assert_array_equal(outs[1][3].view(np.uint64), want_d)
+    np.testing.assert_array_equal(outs[0][2], want_n)
+    np.testing.assert_array_equal(outs[0][3].view(np.uint64), want_d)
 
 
 @pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "umls_emb_pna_rotate", "kinship_lstm_sum_none"])
