@@ -324,7 +324,10 @@ __global__ void rotate_hr_kernel(const float *__restrict__ eemb, const float2 *_
   }
 }
 
-__global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restrict__ ptab,
+#ifndef RNNL_ROT_WAVES
+#define RNNL_ROT_WAVES 1
+#endif
+__global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAVES, 8))) void rotate_direct_kernel(const float *__restrict__ ptab,
                                                            const float *__restrict__ hr, int D, float gamma,
                                                            int nq, int E, float *__restrict__ score,
                                                            int accumulate, unsigned long long *clk) {

@@ -602,6 +602,16 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self._ws_chunks[key] = ws
         return ws
 
+    def _overlap_events(self, device, K):
+        """K (grounding, RotatE) event pairs, created once and re-recorded each
+        call (creating HIP events per call is not free)."""
+        key = (self._device_index(device), "ev")
+        evs = self._side.get(key)
+        if evs is None or len(evs[0]) < K:
+            evs = ([torch.cuda.Event() for _ in range(K)], [torch.cuda.Event() for _ in range(K)])
+            self._side[key] = evs
+        return evs
+
     def _side_streams(self, device):
         key = self._device_index(device)
         if key not in self._side:
@@ -628,20 +638,18 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             side_g.wait_stream(main)  # inputs, node aggregates, workspaces
             side_s.wait_stream(main)
             rec("base")
-            ev_g, ev_r = [], []
+            ev_g, ev_r = self._overlap_events(device, K)
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
                 _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h[lo:].data_ptr(),
                              all_r[lo:].data_ptr(), etr[lo:].data_ptr() if etr is not None else None, hi - lo,
                              n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_ground_wg,
                              side_g.cuda_stream)
-                ev_g.append(torch.cuda.Event())
-                ev_g[-1].record(side_g)
+                ev_g[k].record(side_g)
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
                 self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=False)
-                ev_r.append(torch.cuda.Event())
-                ev_r[-1].record(main)
+                ev_r[k].record(main)
             rec("ground")
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
