@@ -157,10 +157,17 @@ int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, co
 int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p, const int64_t *all_h,
                              const int64_t *all_r, int32_t n_queries, float *score, uint8_t *mask, int32_t *n_cand,
                              uint64_t *digest, void *workspace, size_t workspace_bytes, int32_t capacity_scale,
-                             int32_t workgroups, void *stream);
+                             int32_t workgroups, int32_t deferred, void *stream);
 /* workgroups: cap on the persistent workgroups of the launch (0 = the full
  * default occupancy); a smaller grid leaves room on the CUs for a kernel on
- * another stream (the RotatE overlap). */
+ * another stream (the RotatE overlap).
+ * deferred (sum aggregator): the score pass writes each candidate's
+ * score_model output into the workspace instead of adding it into `score`
+ * (it then neither reads nor writes `score`, so it can run beside
+ * rnnl_rotate_score); rnnl_predictorplus_apply adds the outputs into the
+ * finished base score and sets mask (same fp32 sums as the direct pass). */
+int rnnl_predictorplus_apply(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
+                             int32_t feature, float *score, uint8_t *mask, int32_t n_entities, void *stream);
 /* After a forward: RNNL_OK, or RNNL_ERR_OVERFLOW if any query exceeded the
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */

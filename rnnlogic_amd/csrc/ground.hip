@@ -113,6 +113,7 @@ struct KParams {
   unsigned char *slots;
   int64_t *q_base;   // per query: first pool index of its run
   float *q_scale;    // per query: PNA mean log-degree
+  float *cand_out;   // deferred scoring: score_model output per candidate record (nullable)
   int4 *cand;        // per pool index: candidate record (entity, bucket start, bucket length, 0)
                      // (the first n_cand entries of a query's run)
   int2 *bent;        // bucket entries: (trie node, path count bits)
@@ -165,7 +166,7 @@ __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, in
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
-  int64_t off_qbase, off_qscale, off_cand, off_bent, off_slots, total;
+  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -185,6 +186,8 @@ static Layout make_layout(int64_t nq, int64_t scale) {
   o += 16 * L.pool_cap;
   L.off_bent = o = align256(o);
   o += 8 * L.pool_cap;
+  L.off_cout = o = align256(o);
+  o += 4 * L.pool_cap;
   L.off_slots = o = align256(o);
   o += L.nslots * slot_bytes(L.fcap, L.pcap);
   L.total = o;
@@ -1183,7 +1186,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
 #ifdef RNNL_DIAG_NOSCORE
         const float base = 0.f;
 #else
-        const float base = p.feature == RNNL_FEATURE_NONE ? 0.f : p.score[idx];
+        const float base = (p.feature == RNNL_FEATURE_NONE || p.cand_out) ? 0.f : p.score[idx];
 #endif
 #ifdef RNNL_DIAG_NOENTRIES  // diagnostic build: no bucket-entry walk
         for (int d = 0; d < 16; ++d) f[d] = (float)(cr.z * d);
@@ -1206,6 +1209,10 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
         if (out == 1234.5f) p.score[idx] = base;
         continue;
 #endif
+        if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
+          p.cand_out[qb + s2] = out;
+          continue;
+        }
         p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + base;
         if (p.mask) p.mask[idx] = 1;
       }
@@ -1213,6 +1220,25 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
         __syncthreads();
         if (tid == 0) p.digest[q] = s_dig;
       }
+    }
+  }
+}
+
+
+// Deferred scoring, second half: score[q][t] = out + score[q][t] (the same
+// fp32 sum as the direct path, operands commuted) and mask[q][t] = 1 for every
+// candidate record, once the base score (RotatE) is in place.  One workgroup
+// per query (grid-stride).
+__global__ __launch_bounds__(BS) void apply_kernel(KParams p) {
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    const int nc = p.n_cand[q];
+    if (nc <= 0) continue;
+    const int64_t qb = p.q_base[q];
+    for (int s = threadIdx.x; s < nc; s += BS) {
+      const int64_t idx = (int64_t)q * p.g.E + p.cand[qb + s].x;
+      const float out = p.cand_out[qb + s];
+      p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + p.score[idx];
+      if (p.mask) p.mask[idx] = 1;
     }
   }
 }
@@ -1617,7 +1643,7 @@ int rnnl_predictorplus_ground(rnnl_graph g, rnnl_rules r, int32_t aggregator, co
 int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const int64_t *all_h,
                              const int64_t *all_r, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
                              uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t workgroups,
-                             void *stream) {
+                             int32_t deferred, void *stream) {
   if (bad_params(pp, score) || !n_cand) {
     set_error("rnnl_predictorplus_score: bad arguments");
     return RNNL_ERR_INVALID;
@@ -1628,9 +1654,41 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
     return rc;
   if (nq == 0) return RNNL_OK;
   set_score_params(p, pp, score, mask, digest);
+  if (deferred) {
+    if (pp->aggregator != RNNL_AGG_SUM) {
+      set_error("rnnl_predictorplus_score: deferred scoring supports the sum aggregator only");
+      return RNNL_ERR_INVALID;
+    }
+    p.cand_out = reinterpret_cast<float *>(static_cast<unsigned char *>(ws) + make_layout(nq, scale).off_cout);
+  }
   hipStream_t st = (hipStream_t)stream;
   RNNL_HIP_CHECK(hipMemsetAsync(p.ws + 4 * H_DEQUEUE2, 0, 4, st));  // the scoring dequeue counter
   launch_score(p, r, st, workgroups);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_apply(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand, int32_t feature,
+                             float *score, uint8_t *mask, int32_t n_entities, void *stream) {
+  if (!ws || nq < 0 || scale < 1 || !n_cand || !score || n_entities <= 0) {
+    set_error("rnnl_predictorplus_apply: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  const Layout Ly = make_layout(nq, scale);
+  unsigned char *base = static_cast<unsigned char *>(ws);
+  KParams p{};
+  p.nq = nq;
+  p.g.E = n_entities;
+  p.feature = feature;
+  p.n_cand = const_cast<int32_t *>(n_cand);
+  p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
+  p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
+  p.cand_out = reinterpret_cast<float *>(base + Ly.off_cout);
+  p.score = score;
+  p.mask = mask;
+  hipLaunchKernelGGL(apply_kernel, dim3((unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8)), dim3(BS), 0,
+                     (hipStream_t)stream, p);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -408,6 +408,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # ~18 ms, well inside the RotatE launch.
         self.overlap_ground_wg = int(os.environ.get("RNNL_OVERLAP_GROUND_WG", "256"))
         self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "0"))
+        # sum aggregator: the scoring pass also runs beside RotatE, writing its
+        # per-candidate outputs to the workspace; a short apply pass adds them
+        # into the finished RotatE rows (rnnl_predictorplus_apply)
+        self.overlap_deferred = os.environ.get("RNNL_OVERLAP_DEFERRED", "1") != "0"
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -632,6 +636,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         K = self.overlap_chunks
         bounds = [nq * k // K for k in range(K + 1)]
         agg = params.aggregator
+        deferred = self.overlap_deferred and agg == _native.AGG_SUM
         while True:
             scale = self.capacity_scale
             wss = [self._chunk_workspace(device, k, bounds[k + 1] - bounds[k], scale) for k in range(K)]
@@ -645,20 +650,31 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                              all_r[lo:].data_ptr(), etr[lo:].data_ptr() if etr is not None else None, hi - lo,
                              n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_ground_wg,
                              side_g.cuda_stream)
+                if deferred:  # the score pass does not touch `score`: it runs beside RotatE too
+                    _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
+                                 all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None,
+                                 n_cand[lo:].data_ptr(), digest[lo:].data_ptr() if digest is not None else None,
+                                 wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_score_wg, 1,
+                                 side_g.cuda_stream)
                 ev_g[k].record(side_g)
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
                 self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=False)
                 ev_r[k].record(main)
             rec("ground")
-            for k in range(K):
+            for k in range(K if deferred else 0):
+                lo, hi = bounds[k], bounds[k + 1]
+                main.wait_event(ev_g[k])
+                _native.call("rnnl_predictorplus_apply", wss[k].data_ptr(), hi - lo, scale, n_cand[lo:].data_ptr(),
+                             params.feature, score[lo:].data_ptr(), None, self.num_entities, main.cuda_stream)
+            for k in range(0 if deferred else K):
                 lo, hi = bounds[k], bounds[k + 1]
                 side_s.wait_event(ev_g[k])
                 side_s.wait_event(ev_r[k])
                 _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
                              all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None, n_cand[lo:].data_ptr(),
                              digest[lo:].data_ptr() if digest is not None else None, wss[k].data_ptr(),
-                             wss[k].numel(), scale, self.overlap_score_wg, side_s.cuda_stream)
+                             wss[k].numel(), scale, self.overlap_score_wg, 0, side_s.cuda_stream)
             main.wait_stream(side_s)
             main.wait_stream(side_g)
             rec("end")
