@@ -131,20 +131,20 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 
 __device__ __forceinline__ uint32_t hash32(uint32_t k) { return k * 2654435761u; }
 
-// Per-slot scratch: two frontier buffers (node | entity | count planes of
-// fcap entries each) then the contribution planes.  Buffer pointers are
-// computed, not indexed from an array: a runtime index into a pointer array
-// would put the array in scratch memory.
+// Per-slot scratch: two frontier buffers and the contribution list, each an
+// array of 12-B entries (a, b, count) — one contiguous run per list, so a
+// query touches a few compact address ranges (frontier: a = trie node,
+// b = entity; contribution: a = entity, b = trie node).
+struct Ent {
+  int32_t a, b;
+  uint32_t c;
+};
+
 struct Slot {
-  int32_t *f0;
+  Ent *f0;
   int64_t fcap;
-  int32_t *ct, *cn;
-  uint32_t *cc;
-  __device__ __forceinline__ int32_t *fn(int k) const { return f0 + (int64_t)(3 * k) * fcap; }
-  __device__ __forceinline__ int32_t *fv(int k) const { return f0 + (int64_t)(3 * k + 1) * fcap; }
-  __device__ __forceinline__ uint32_t *fc(int k) const {
-    return reinterpret_cast<uint32_t *>(f0 + (int64_t)(3 * k + 2) * fcap);
-  }
+  Ent *ct;
+  __device__ __forceinline__ Ent *f(int k) const { return f0 + (int64_t)k * fcap; }
 };
 
 __host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) { return 2 * fcap * 12 + pcap * 12; }
@@ -152,14 +152,9 @@ __host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) { retu
 __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, int64_t pcap) {
   unsigned char *b = base + (int64_t)slot * slot_bytes(fcap, pcap);
   Slot s;
-  s.f0 = reinterpret_cast<int32_t *>(b);
+  s.f0 = reinterpret_cast<Ent *>(b);
   s.fcap = fcap;
-  b += 2 * fcap * 12;
-  s.ct = reinterpret_cast<int32_t *>(b);
-  b += pcap * 4;
-  s.cn = reinterpret_cast<int32_t *>(b);
-  b += pcap * 4;
-  s.cc = reinterpret_cast<uint32_t *>(b);
+  s.ct = reinterpret_cast<Ent *>(b + 2 * fcap * 12);
   return s;
 }
 
@@ -280,9 +275,7 @@ struct __align__(16) Smem {
 __device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pcap, int t, int node, uint32_t c) {
   const int pos = atomicAdd(&S.np, 1);
   if (pos < pcap) {
-    sl.ct[pos] = t;
-    sl.cn[pos] = node;
-    sl.cc[pos] = c;
+    sl.ct[pos] = Ent{t, node, c};
   } else {
     S.ovf = 1;
   }
@@ -292,9 +285,7 @@ __device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, 
                                               uint32_t c) {
   const int pos = atomicAdd(&S.nd, 1);
   if (pos < fcap) {
-    sl.fn(buf)[pos] = node;
-    sl.fv(buf)[pos] = v;
-    sl.fc(buf)[pos] = c;
+    sl.f(buf)[pos] = Ent{node, v, c};
   } else {
     S.ovf = 1;
   }
@@ -341,9 +332,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
   const int E = p.g.E, R = p.g.R;
   const int depth = p.rl.head_depth[r];
   if (tid == 0) {
-    sl.fn(0)[0] = root;
-    sl.fv(0)[0] = h;
-    sl.fc(0)[0] = 1u;
+    sl.f(0)[0] = Ent{root, h, 1u};
     if (p.rl.node_nrules[root] > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
   }
   wg_sync_global();
@@ -356,9 +345,10 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       const int ne = min(GBS, n_prev - cb);
       int nch = 0;
       if (tid < ne) {
-        const int node = sl.fn(cur)[cb + tid];
-        S.ent_v[tid] = sl.fv(cur)[cb + tid];
-        S.ent_c[tid] = sl.fc(cur)[cb + tid];
+        const Ent fe = sl.f(cur)[cb + tid];
+        const int node = fe.a;
+        S.ent_v[tid] = fe.b;
+        S.ent_c[tid] = fe.c;
         S.ent_fch[tid] = p.rl.node_child[node];
         nch = p.rl.node_nchild[node];
       }
@@ -469,19 +459,18 @@ __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
   return total;
 }
 
-// One entity window [lo, lo + WIN) whose contributions are wt/wn/wc[beg, end):
+// One entity window [lo, lo + WIN) whose contributions are w[beg, end):
 // candidate records for it are written at pool indices cbase + [0, nc) and
 // its buckets at pool indices qbase + beg + [0, end - beg).  degree_only (PNA
 // sweep 1) accumulates sum log(degree) instead.  Returns nc.
 __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, int beg, int end, int64_t cbase,
                            bool degree_only) {
   const int tid = threadIdx.x;
-  const int32_t *wt = sl.fn(0), *wn = sl.fv(0);
-  const uint32_t *wc = sl.fc(0);
+  const Ent *w = sl.f(0);  // window-sorted contributions: a = entity, b = node, c = count
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
   for (int i = tid; i < WIN; i += GBS) S.u.b.map[i] = 0;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) S.u.b.map[wt[i] - lo] = 1;  // mark present entities
+  for (int i = beg + tid; i < end; i += GBS) S.u.b.map[w[i].a - lo] = 1;  // mark present entities
   __syncthreads();
   for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = S.u.b.map[i];
   __syncthreads();
@@ -500,8 +489,8 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
     for (int i = beg + tid; i < end; i += GBS)
-      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[wt[i] - lo]]),
-                wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
+      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[w[i].a - lo]]),
+                w[i].c * (uint32_t)p.rl.node_nrules[w[i].b]);
     __syncthreads();
     for (int s2 = tid; s2 < nc; s2 += GBS) {
       const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
@@ -510,7 +499,7 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
     __syncthreads();
     return nc;
   }
-  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.b.cnt[S.u.b.map[wt[i] - lo]], 1);  // bucket sizes
+  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.b.cnt[S.u.b.map[w[i].a - lo]], 1);  // bucket sizes
   __syncthreads();
   for (int i = tid; i < WIN; i += GBS) S.u.b.off[i] = S.u.b.cnt[i];
   __syncthreads();
@@ -525,9 +514,9 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   __syncthreads();
   PSTAMP(1);
   for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
-    const int s2 = S.u.b.map[wt[i] - lo];
+    const int s2 = S.u.b.map[w[i].a - lo];
     const int64_t pos = qb + beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
-    p.bent[pos] = make_int2(wn[i], (int)wc[i]);
+    p.bent[pos] = make_int2(w[i].b, (int)w[i].c);
   }
   __syncthreads();
   PSTAMP(2);
@@ -554,14 +543,13 @@ __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
 __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int end, int64_t cbase,
                          bool degree_only) {
   const int tid = threadIdx.x;
-  const int32_t *wt = sl.fn(0), *wn = sl.fv(0);
-  const uint32_t *wc = sl.fc(0);
+  const Ent *w = sl.f(0);  // window-sorted contributions: a = entity, b = node, c = count
   for (int i = tid; i < HB; i += GBS) {
     S.u.c.key[i] = EMPTY;
     S.u.c.cnt[i] = 0;
   }
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, wt[i], true)], 1);
+  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, w[i].a, true)], 1);
   __syncthreads();
   // one scan of (bucket size << 12 | occupied): bucket offsets and candidate ids
   constexpr int PER = HB / GBS;
@@ -589,8 +577,8 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int
     for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
     __syncthreads();
     for (int i = beg + tid; i < end; i += GBS)
-      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, wt[i], false)]),
-                wc[i] * (uint32_t)p.rl.node_nrules[wn[i]]);
+      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, w[i].a, false)]),
+                w[i].c * (uint32_t)p.rl.node_nrules[w[i].b]);
     __syncthreads();
     for (int i = tid; i < HB; i += GBS) {
       if (S.u.c.key[i] != EMPTY) {
@@ -612,9 +600,9 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int
   for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
   __syncthreads();
   for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
-    const int sl2 = hb_slot(S, wt[i], false);
+    const int sl2 = hb_slot(S, w[i].a, false);
     const int64_t pos = qb + beg + S.u.c.off[sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
-    p.bent[pos] = make_int2(wn[i], (int)wc[i]);
+    p.bent[pos] = make_int2(w[i].b, (int)w[i].c);
   }
   __syncthreads();
   return nc;
@@ -628,7 +616,7 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
   if (!sorted) {
     for (int i = tid; i < nwin; i += GBS) S.whist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < P; i += GBS) atomicAdd(&S.whist[sl.ct[i] >> WBITS], 1);
+    for (int i = tid; i < P; i += GBS) atomicAdd(&S.whist[sl.ct[i].a >> WBITS], 1);
     __syncthreads();
     if (tid == 0) {
       int acc = 0;
@@ -642,11 +630,10 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
     }
     __syncthreads();
     for (int i = tid; i < P; i += GBS) {
-      const int t = sl.ct[i];
+      const Ent ce = sl.ct[i];
+      const int t = ce.a;
       const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
-      sl.fn(0)[pos] = t;
-      sl.fv(0)[pos] = sl.cn[i];
-      sl.fc(0)[pos] = sl.cc[i];
+      sl.f(0)[pos] = ce;
     }
     wg_sync_global();
   }
