@@ -232,6 +232,14 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   rs->head_root = head_root;
   rs->d.max_leaves = max_leaves;
   rs->d.max_head_nodes = max_head_nodes;
+  std::vector<int32_t> node_info(4 * node_rel.size());
+  for (size_t n = 0; n < node_rel.size(); ++n) {
+    node_info[4 * n] = node_rel[n];
+    node_info[4 * n + 1] = node_child[n];
+    node_info[4 * n + 2] = node_nchild[n];
+    node_info[4 * n + 3] = node_nrules[n];
+  }
+  const int32_t *node_info_dev = nullptr;
   int rc = RNNL_OK;
   if ((rc = upload(head_root, &rs->mem[0], &rs->d.head_root)) ||
       (rc = upload(head_depth, &rs->mem[1], &rs->d.head_depth)) ||
@@ -245,10 +253,12 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
       (rc = upload(node_fp, &rs->mem[9], &rs->d.node_fp)) ||
       (rc = upload(head_leaf_ptr, &rs->mem[10], &rs->d.head_leaf_ptr)) ||
       (rc = upload(head_leaf_node, &rs->mem[11], &rs->d.head_leaf_node)) ||
-      (rc = upload(node_leaf, &rs->mem[12], &rs->d.node_leaf))) {
+      (rc = upload(node_leaf, &rs->mem[12], &rs->d.node_leaf)) ||
+      (rc = upload(node_info, &rs->mem[13], &node_info_dev))) {
     rnnl_rules_destroy(rs);
     return rc;
   }
+  rs->d.node_info = reinterpret_cast<const int4 *>(node_info_dev);
   *out = rs;
   return RNNL_OK;
 }

@@ -333,7 +333,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
   const int depth = p.rl.head_depth[r];
   if (tid == 0) {
     sl.f(0)[0] = Ent{root, h, 1u};
-    if (p.rl.node_nrules[root] > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
+    if (p.rl.node_info[root].w > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
   }
   wg_sync_global();
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
@@ -349,8 +349,9 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
         const int node = fe.a;
         S.ent_v[tid] = fe.b;
         S.ent_c[tid] = fe.c;
-        S.ent_fch[tid] = p.rl.node_child[node];
-        nch = p.rl.node_nchild[node];
+        const int4 ni = p.rl.node_info[node];
+        S.ent_fch[tid] = ni.y;
+        nch = ni.z;
       }
       int NI;
       const int ioff = block_scan(nch, S.ws, NI);
@@ -363,7 +364,8 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
         if (k < NI) {
           const int ent = upper_idx(S.item_off, ne, k);
           const int child = S.ent_fch[ent] + (k - S.item_off[ent]);
-          const int rel = p.rl.node_rel[child];
+          const int4 ci = p.rl.node_info[child];
+          const int rel = ci.x;
           const int v = S.ent_v[ent];
           const int64_t o = (int64_t)v * R + rel;
           const int beg = p.g.off[o];
@@ -373,7 +375,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
           S.it_c[tid] = S.ent_c[ent];
           // bit 0: leaf (rules end here), bit 1: inner (has children),
           // bit 2: this hop may traverse the query's own edge (data.py:143-146)
-          S.it_flags[tid] = (p.rl.node_nrules[child] > 0 ? 1 : 0) | (p.rl.node_nchild[child] > 0 ? 2 : 0) |
+          S.it_flags[tid] = (ci.w > 0 ? 1 : 0) | (ci.z > 0 ? 2 : 0) |
                             (rel == r && v == rm_src ? 4 : 0);
         }
         int NE;

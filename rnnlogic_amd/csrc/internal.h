@@ -53,6 +53,8 @@ struct RulesDev {
   const int32_t *head_leaf_ptr = nullptr;   // R + 1
   const int32_t *head_leaf_node = nullptr;  // leaf node ids, head-major, ascending node id
   const int32_t *node_leaf = nullptr;       // n_nodes: local leaf index within its head, -1 if none
+  // the grounding walk's per-node fields in one 16-B load: (rel, first child, nchild, nrules)
+  const int4 *node_info = nullptr;
 };
 
 // Node-weight records (bytes per node); see rnnl_node_weights.
