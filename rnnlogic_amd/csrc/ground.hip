@@ -542,10 +542,10 @@ __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
   return -1;  // unreachable: at most HB_LOAD < HB distinct keys
 }
 
-__device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int end, int64_t cbase,
+__device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int end, int64_t cbase,
                          bool degree_only) {
+  // w: contributions (a = entity, b = node, c = count), window-sorted or raw
   const int tid = threadIdx.x;
-  const Ent *w = sl.f(0);  // window-sorted contributions: a = entity, b = node, c = count
   for (int i = tid; i < HB; i += GBS) {
     S.u.c.key[i] = EMPTY;
     S.u.c.cnt[i] = 0;
@@ -614,6 +614,9 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Slot &sl, int beg, int
 // (free during phase B), then window_pass over every non-empty window.
 __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P, bool degree_only, bool sorted) {
   const int tid = threadIdx.x;
+  // all contributions fit one hash pass: no window sort (it exists only to
+  // bound the hash load) — one read of the raw list instead of a sorted copy
+  if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only) : 0;
   const int nwin = (p.g.E + WIN - 1) >> WBITS;
   if (!sorted) {
     for (int i = tid; i < nwin; i += GBS) S.whist[i] = 0;
@@ -651,7 +654,7 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
     }
     int w2 = w + 1;
     while (w2 < nwin && S.wbeg[w2 + 1] - beg <= HB_LOAD) ++w2;
-    if (S.wbeg[w2] > beg) ncand += hash_pass(p, S, sl, beg, S.wbeg[w2], S.qbase + ncand, degree_only);
+    if (S.wbeg[w2] > beg) ncand += hash_pass(p, S, sl.f(0), beg, S.wbeg[w2], S.qbase + ncand, degree_only);
     w = w2;
   }
   return ncand;
