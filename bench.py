@@ -172,13 +172,19 @@ def isolated_ground_ms(model, graph, h, r, dev):
 
 
 def algorithmic_work(model, graph, rows, threads):
-    """Exact per-rule work counts of the SURVEY §8(d) formula from the C oracle:
-    F (frontier expansions), T (edge traversals), P ((rule, dest) pairs)."""
-    from oracle import ground_c
-    cg = ground_c.CGraph(graph.entity_size, graph.relation_size, graph._train)
-    orc = ground_c.Oracle(cg, model.rules, graph.relation_size)
-    _, ncand, work = orc.digests(rows[:, 0], rows[:, 1], threads=threads, work=True)
-    return work.sum(0), int(ncand.sum())
+    """Exact per-rule work counts of the SURVEY §8(d) formula: F (frontier
+    expansions), T (edge traversals), P ((rule, dest) pairs) and C
+    (candidates) of this workload, from tests/golden/fb15k237_work.json (made by
+    tools/make_work_counts.py with the C oracle; a prefix is re-derived by
+    tests/test_oracle_c.py).  The file must describe exactly these rows."""
+    import hashlib
+    with open(os.path.join(REPO, "tests", "golden", "fb15k237_work.json")) as f:
+        w = json.load(f)
+    dig = hashlib.sha256(np.ascontiguousarray(rows[:, :2], dtype=np.int64).tobytes()).hexdigest()
+    if w["rows_sha256"] != dig or w["rules"] != model.num_rules:
+        raise RuntimeError("tests/golden/fb15k237_work.json does not describe this workload: "
+                           "rerun tools/make_work_counts.py")
+    return (w["F"], w["T"], w["P"]), w["C"]
 
 
 def main():

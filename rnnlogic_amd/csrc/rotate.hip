@@ -327,6 +327,15 @@ __global__ void rotate_hr_kernel(const float *__restrict__ eemb, const float2 *_
 #ifndef RNNL_ROT_WAVES
 #define RNNL_ROT_WAVES 1
 #endif
+#ifndef RNNL_ROT_ACC_LDS
+#define RNNL_ROT_ACC_LDS 0
+#endif
+#ifndef RNNL_ROT_QW
+#define RNNL_ROT_QW 1
+#endif
+constexpr int ROT_QW = RNNL_ROT_QW;    // query groups per block (divides RB / 64)
+constexpr int ROT_RE = RB / ROT_QW;    // entities per block
+static_assert(ROT_RE % 64 == 0 && 256 % ROT_RE == 0, "whole waves per query group; ent_pad divisible");
 __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAVES, 8))) void rotate_direct_kernel(const float *__restrict__ ptab,
                                                            const float *__restrict__ hr, int D, float gamma,
                                                            int nq, int E, float *__restrict__ score,
@@ -337,19 +346,37 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
   __shared__ volatile char pad[RNNL_ROT_LDS_PAD];
   if (threadIdx.x == 0) pad[0] = 0;
 #endif
-  if (!xcd_tile((int)(Ep / RB), (nq + DQ - 1) / DQ, et, qt)) return;
+  const int ngroups = (nq + DQ - 1) / DQ;
+  if (!xcd_tile((int)(Ep / ROT_RE), (ngroups + ROT_QW - 1) / ROT_QW, et, qt)) return;
+  // ROT_QW query groups per block, one per wave row, over the same ROT_RE
+  // entities (their entity-plane loads meet in L1)
+  qt = __builtin_amdgcn_readfirstlane(qt * ROT_QW + (int)threadIdx.x / ROT_RE);  // wave-uniform: SGPR h o r operands
+  if (qt >= ngroups) return;  // wave-uniform; the kernel has no barrier
   ClockStamp cs;
   cs.begin(clk);
-  const int e = et * RB + threadIdx.x;  // < Ep: the table is padded
+  const int e = et * ROT_RE + (int)threadIdx.x % ROT_RE;  // < Ep: the table is padded
   const int q0 = qt * DQ;
   const float *hp = hr + (int64_t)qt * D * 2 * DQ;
   const float *ap = ptab + e;
   // software pipeline: the sqrt of dim d runs one dim later than its
   // squared distance (a VALU result feeding v_sqrt directly costs ~6 more
   // cycles per term; tools/micro/valu_rates.hip "direct pipelined")
+#if RNNL_ROT_ACC_LDS
+  // row totals live in LDS (each lane its own column: no barrier), which
+  // frees DQ VGPRs so RotatE keeps its occupancy beside the side-stream
+  // grounding waves
+  __shared__ float s_acc[DQ][RB];
+  float sq[DQ];
+#pragma unroll
+  for (int k = 0; k < DQ; ++k) {
+    s_acc[k][threadIdx.x] = 0.f;
+    sq[k] = 0.f;
+  }
+#else
   float acc[DQ], sq[DQ];
 #pragma unroll
   for (int k = 0; k < DQ; ++k) acc[k] = sq[k] = 0.f;
+#endif
   // entity values: LCH dims at a time, loaded one LCH-block ahead (fixed
   // register slots per dim, so the prefetch never waits on a rotation)
   float va[LCH], vb[LCH], na[LCH], nb[LCH];
@@ -392,8 +419,22 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
       }
     }
 #pragma unroll
-    for (int k = 0; k < DQ; ++k) acc[k] += part[k];
+    for (int k = 0; k < DQ; ++k) {
+#if RNNL_ROT_ACC_LDS
+      s_acc[k][threadIdx.x] += part[k];
+#else
+      acc[k] += part[k];
+#endif
+    }
+#if RNNL_ROT_ACC_LDS
+    asm volatile("" ::: "memory");  // keeps LICM from promoting the columns back into VGPRs
+#endif
   }
+#if RNNL_ROT_ACC_LDS
+  float acc[DQ];
+#pragma unroll
+  for (int k = 0; k < DQ; ++k) acc[k] = s_acc[k][threadIdx.x];
+#endif
 #pragma unroll
   for (int k = 0; k < DQ; ++k) acc[k] += __builtin_amdgcn_sqrtf(sq[k]);  // v_sqrt_f32 (1 ulp)
   cs.end(clk);
@@ -590,7 +631,7 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
     hipLaunchKernelGGL(rotate_hr_kernel, dim3(grid_for(nhr)), dim3(256), 0, (hipStream_t)stream, eemb,
                        (const float2 *)rtab, D, all_h, all_r, nq, (float *)workspace);
     RNNL_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(rotate_direct_kernel, dim3(xcd_grid(ent_pad(E) / RB, (nq + DQ - 1) / DQ)), dim3(RB), 0,
+    hipLaunchKernelGGL(rotate_direct_kernel, dim3(xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW)), dim3(RB), 0,
                        (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E, score,
                        accumulate, g_clk);
   } else {

@@ -101,3 +101,24 @@ def test_c_oracle_digest_consistency(fixtures):
         for a, b, c in zip(tt.tolist(), ss.tolist(), ff.tolist()):
             acc = (acc + ground_c.mix64(a ^ ground_c.mix64(b ^ ground_c.mix64(c)))) & 0xFFFFFFFFFFFFFFFF
         assert int(d[i]) == acc and n[i] == len(tt)
+
+
+def test_bench_work_counts_fixture():
+    """tests/golden/fb15k237_work.json (bench.py's algorithmic-bytes input)
+    describes the bench rows, and its first 2000 queries re-derive from the C
+    oracle."""
+    import importlib.util
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("make_work_counts", os.path.join(root, "tools", "make_work_counts.py"))
+    mwc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mwc)
+    with open(os.path.join(root, "tests", "golden", "fb15k237_work.json")) as f:
+        w = json.load(f)
+    graph, model, rows = mwc.workload()
+    assert w["queries"] == len(rows) and w["rules"] == model.num_rules
+    assert w["rows_sha256"] == mwc.rows_digest(rows)
+    pre = w["prefix"]
+    work, ncand = mwc.work_counts(graph, model, rows[:pre["queries"]], threads=os.cpu_count() or 1)
+    assert [int(x) for x in work.sum(0)] == [pre["F"], pre["T"], pre["P"]]
+    assert int(ncand.sum()) == pre["C"]
