@@ -1261,31 +1261,47 @@ __global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
 }
 
 // ---------------------------------------------------------------- node weights
-__global__ void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, int ld, int agg,
-                                    unsigned char *__restrict__ out) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = (int)(gid >> 4), d = (int)(gid & 15);
-  if (n >= rl.n_nodes) return;
-  float s1 = 0.f, s2 = 0.f, mn = __builtin_huge_valf(), mx = -__builtin_huge_valf();
-  for (int k = rl.node_rule_ptr[n]; k < rl.node_rule_ptr[n + 1]; ++k) {
-    const float x = emb[(int64_t)rl.node_rules[k] * ld + d];
-    s1 += x;
-    s2 += x * x;
-    mn = fminf(mn, x);
-    mx = fmaxf(mx, x);
-  }
+// Grid-stride over (node, dim) pairs; the table-wide max |s1| (the SUM table's
+// shift) is reduced per thread, per wave and per block before one atomic per
+// block (one atomic per lane on a single word serialised at ~0.5 ms).
+__global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, int ld,
+                                                          int agg, unsigned char *__restrict__ out) {
   const double sc = (double)(1 << kFixShift);
-  if (agg == RNNL_AGG_SUM) {
-    // f32 sum for now; node_fix_kernel turns it into int32 fixed point
-    reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = s1;
-    atomicMax(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStrideSum), __float_as_uint(fabsf(s1)));
-  } else {
-    long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStridePna);
-    rec[d] = llrint((double)s1 * sc);
-    rec[16 + d] = llrint((double)s2 * sc);
-    float *fr = reinterpret_cast<float *>(rec + 32);
-    fr[d] = mn;
-    fr[16 + d] = mx;
+  const int64_t total = (int64_t)rl.n_nodes * 16;
+  unsigned int m = 0;
+  for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+       gid += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(gid >> 4), d = (int)(gid & 15);
+    float s1 = 0.f, s2 = 0.f, mn = __builtin_huge_valf(), mx = -__builtin_huge_valf();
+    for (int k = rl.node_rule_ptr[n]; k < rl.node_rule_ptr[n + 1]; ++k) {
+      const float x = emb[(int64_t)rl.node_rules[k] * ld + d];
+      s1 += x;
+      s2 += x * x;
+      mn = fminf(mn, x);
+      mx = fmaxf(mx, x);
+    }
+    if (agg == RNNL_AGG_SUM) {
+      // f32 sum for now; node_fix_kernel turns it into int32 fixed point
+      reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = s1;
+      m = max(m, __float_as_uint(fabsf(s1)));
+    } else {
+      long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStridePna);
+      rec[d] = llrint((double)s1 * sc);
+      rec[16 + d] = llrint((double)s2 * sc);
+      float *fr = reinterpret_cast<float *>(rec + 32);
+      fr[d] = mn;
+      fr[16 + d] = mx;
+    }
+  }
+  if (agg != RNNL_AGG_SUM) return;  // uniform across the grid
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+  __shared__ unsigned int s_m[4];
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+    if (m) atomicMax(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStrideSum), m);
   }
 }
 
@@ -1354,12 +1370,16 @@ __host__ __device__ inline int64_t lin_trailer_off(int n_nodes) { return ((int64
 
 __global__ void lin_node_kernel(RulesDev rl, const float *__restrict__ w, unsigned char *__restrict__ out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= rl.n_nodes) return;
+  const bool valid = n < rl.n_nodes;
   double s = 0.0;
-  for (int k = rl.node_rule_ptr[n]; k < rl.node_rule_ptr[n + 1]; ++k) s += (double)w[rl.node_rules[k]];
+  const int k0 = valid ? rl.node_rule_ptr[n] : 0, k1 = valid ? rl.node_rule_ptr[n + 1] : 0;
+  for (int k = k0; k < k1; ++k) s += (double)w[rl.node_rules[k]];
   const float f = (float)s;
-  reinterpret_cast<float *>(out)[n] = f;
-  atomicMax(reinterpret_cast<unsigned int *>(out + lin_trailer_off(rl.n_nodes)), __float_as_uint(fabsf(f)));
+  if (valid) reinterpret_cast<float *>(out)[n] = f;
+  unsigned int m = __float_as_uint(fabsf(f));  // wave max, then one atomic per wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(reinterpret_cast<unsigned int *>(out + lin_trailer_off(rl.n_nodes)), m);
 }
 
 __global__ void lin_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
@@ -1457,8 +1477,8 @@ int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, v
     RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * kStrideSum, 0, 8, (hipStream_t)stream));
   if (n == 0) return RNNL_OK;
   const int bs = 256;
-  hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, (hipStream_t)stream,
-                     r->d, emb, ld, agg, out);
+  hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 2048)), dim3(bs), 0,
+                     (hipStream_t)stream, r->d, emb, ld, agg, out);
   if (agg == RNNL_AGG_SUM)
     hipLaunchKernelGGL(node_fix_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 4096)), dim3(bs), 0,
                        (hipStream_t)stream, r->d.n_nodes, out);
