@@ -307,20 +307,30 @@ constexpr int DCH = 32;   // dims per partial sum
 #endif
 constexpr int LCH = RNNL_LCH;  // dims per entity-value prefetch block (divides DCH)
 
-// hr[g][d][0..15 | 16..31] = (re | im) of (h o r)_d for queries 16 g + k
-__global__ void rotate_hr_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D,
-                                 const int64_t *__restrict__ all_h, const int64_t *__restrict__ all_r, int nq,
-                                 float *__restrict__ hr) {
-  const int64_t n = (int64_t)((nq + DQ - 1) / DQ) * D * DQ;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int k = (int)(i % DQ);
-    const int64_t gd = i / DQ;
-    const int d = (int)(gd % D);
-    const int q = (int)(gd / D) * DQ + k;
+// hr[g][d][0..DQ-1 | DQ..2DQ-1] = (re | im) of (h o r)_d for queries DQ g + k.
+// One block per (query group, 64 dims): entity rows read coalesced along d,
+// the group's 64 x 2DQ slab transposed in LDS and written contiguously.
+__global__ __launch_bounds__(256) void rotate_hr_kernel(const float *__restrict__ eemb,
+                                                        const float2 *__restrict__ rtab, int D,
+                                                        const int64_t *__restrict__ all_h,
+                                                        const int64_t *__restrict__ all_r, int nq,
+                                                        float *__restrict__ hr) {
+  __shared__ float s_re[64][DQ + 1], s_im[64][DQ + 1];
+  const int g = blockIdx.x, d0 = blockIdx.y * 64;
+  const int dl = threadIdx.x & 63, nd = min(64, D - d0);
+  for (int k = threadIdx.x >> 6; k < DQ; k += 4) {
+    const int q = g * DQ + k;
     float re = 0.f, im = 0.f;
-    if (q < nq) rotate_head(eemb + all_h[q] * 2 * (int64_t)D, rtab + all_r[q] * (int64_t)D, D, d, re, im);
-    hr[gd * 2 * DQ + k] = re;
-    hr[gd * 2 * DQ + DQ + k] = im;
+    if (q < nq && dl < nd)
+      rotate_head(eemb + all_h[q] * 2 * (int64_t)D, rtab + all_r[q] * (int64_t)D, D, d0 + dl, re, im);
+    s_re[dl][k] = re;
+    s_im[dl][k] = im;
+  }
+  __syncthreads();
+  float *out = hr + ((int64_t)g * D + d0) * 2 * DQ;
+  for (int j = threadIdx.x; j < nd * 2 * DQ; j += 256) {
+    const int d = j / (2 * DQ), w = j % (2 * DQ);
+    out[j] = w < DQ ? s_re[d][w] : s_im[d][w - DQ];
   }
 }
 
@@ -627,11 +637,12 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
       set_error("rnnl_rotate_score: workspace too small (see rnnl_rotate_workspace_size)");
       return RNNL_ERR_INVALID;
     }
-    const int64_t nhr = (int64_t)((nq + DQ - 1) / DQ) * D * DQ;
-    hipLaunchKernelGGL(rotate_hr_kernel, dim3(grid_for(nhr)), dim3(256), 0, (hipStream_t)stream, eemb,
+    hipLaunchKernelGGL(rotate_hr_kernel, dim3((unsigned)((nq + DQ - 1) / DQ), (unsigned)((D + 63) / 64)), dim3(256), 0,
+                       (hipStream_t)stream, eemb,
                        (const float2 *)rtab, D, all_h, all_r, nq, (float *)workspace);
     RNNL_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(rotate_direct_kernel, dim3(xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW)), dim3(RB), 0,
+    hipLaunchKernelGGL(rotate_direct_kernel,
+                       dim3(xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW)), dim3(RB), 0,
                        (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E, score,
                        accumulate, g_clk);
   } else {
