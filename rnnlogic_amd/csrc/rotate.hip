@@ -340,6 +340,9 @@ __global__ __launch_bounds__(256) void rotate_hr_kernel(const float *__restrict_
 #ifndef RNNL_ROT_ACC_LDS
 #define RNNL_ROT_ACC_LDS 0
 #endif
+#ifndef RNNL_ROT_PRIO
+#define RNNL_ROT_PRIO 0
+#endif
 #ifndef RNNL_ROT_QW
 #define RNNL_ROT_QW 1
 #endif
@@ -362,6 +365,12 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
   // entities (their entity-plane loads meet in L1)
   qt = __builtin_amdgcn_readfirstlane(qt * ROT_QW + (int)threadIdx.x / ROT_RE);  // wave-uniform: SGPR h o r operands
   if (qt >= ngroups) return;  // wave-uniform; the kernel has no barrier
+#if RNNL_ROT_PRIO
+  // diagnostic: wave priority above the side-stream grounding / scoring waves
+  // sharing the SIMDs (RotatE then runs near its alone time but
+  // starves the side streams)
+  __builtin_amdgcn_s_setprio(RNNL_ROT_PRIO);
+#endif
   ClockStamp cs;
   cs.begin(clk);
   const int e = et * ROT_RE + (int)threadIdx.x % ROT_RE;  // < Ep: the table is padded
