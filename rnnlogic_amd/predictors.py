@@ -252,6 +252,10 @@ class Predictor(_HipGrounding, torch.nn.Module):
         relations): (score (n, |E|) f32, mask (n, |E|) bool[, n_cand])."""
         device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
         nq, E = all_h.numel(), self.num_entities
+        if nq == 0:  # no rows: empty outputs, no launch
+            out = (torch.empty((0, E), dtype=torch.float32, device=device),
+                   torch.empty((0, E), dtype=torch.bool, device=device))
+            return out + (torch.empty(0, dtype=torch.int32, device=device),) if return_ncand else out
         g, nr = self.graph.device_graph(device), self.native_rules(device)
         node_w = self.node_weights(device)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -552,6 +556,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         all_r = all_r.to(torch.int64).contiguous()
         etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
         nq = all_h.numel()
+        if nq == 0:  # no rows: empty outputs, no launch
+            out = (torch.empty((0, self.num_entities), dtype=torch.float32, device=device),
+                   torch.empty((0, self.num_entities), dtype=torch.bool, device=device))
+            return out + (torch.empty(0, dtype=torch.int32, device=device),) if return_ncand else out
         g = self.graph.device_graph(device)
         nr = self.native_rules(device)
         rec = (lambda k: events.setdefault(k, torch.cuda.Event(enable_timing=True)).record()) \
