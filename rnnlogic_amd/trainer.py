@@ -22,11 +22,14 @@ from torch import nn
 from torch.utils import data as torch_data
 
 from . import comm
-from .data import DeviceTrainBatches
+from .data import DeviceTrainBatches, Iterator
 
 
 class _SizedIter(object):
-    """len() + iteration over fn(index) for the sampler's indices."""
+    """len() + iteration over fn(index) for the sampler's indices.  Starting an
+    iteration draws one int64 from the global torch RNG, as a DataLoader
+    iterator does for its base seed, so a seeded run (e.g. run_rnnlogic.py)
+    consumes the RNG exactly as the reference's DataLoader path does."""
 
     def __init__(self, sampler, fn):
         self.sampler, self.fn = sampler, fn
@@ -35,6 +38,7 @@ class _SizedIter(object):
         return len(self.sampler)
 
     def __iter__(self):
+        torch.empty((), dtype=torch.int64).random_()
         return (self.fn(i) for i in self.sampler)
 
 
@@ -274,3 +278,231 @@ class TrainerPredictor(object):
             torch.save({"model": self.model.state_dict(), "optimizer": self.optimizer.state_dict()},
                        os.path.expanduser(checkpoint))
         comm.synchronize()
+
+
+class _RuleTable(object):
+    """A RuleDataset laid out once for the device: every formatted rule
+    [head, body..., END] right-padded with its PAD token into an (N, Lmax)
+    int64 tensor, its weight (N,) and its length (host).  A training batch is
+    then an index gather + a slice to the batch's longest rule, the same
+    tensors RuleDataset.collate_fn builds (data.py:321-342) without a Python
+    pass over the batch."""
+
+    def __init__(self, rule_set, device):
+        seqs = [item[0] for item in rule_set.rules]
+        pads = [int(item[1]) for item in rule_set.rules]
+        self.lens = torch.tensor([len(s) for s in seqs], dtype=torch.long)
+        L = int(self.lens.max()) if len(seqs) else 1
+        seq = torch.tensor(pads, dtype=torch.long).unsqueeze(1).repeat(1, L)
+        for k, s in enumerate(seqs):
+            seq[k, :len(s)] = torch.tensor(s, dtype=torch.long)
+        pad = torch.tensor(pads, dtype=torch.long).unsqueeze(1)
+        # inputs drop each rule's END (collate_fn: item[0][:-1]), targets its head
+        self.inputs = torch.where(seq == rule_set.ending_idx, pad, seq)[:, :-1].contiguous().to(device)
+        self.target = seq[:, 1:].contiguous().to(device)
+        self.pad = pad.squeeze(1).to(device)
+        self.weight = torch.tensor([float(item[-1]) for item in rule_set.rules], device=device)
+        self.device = device
+
+    def batch(self, idx):
+        """idx: CPU int64 (n,) -> (inputs, target, mask, weight) on the device."""
+        T = int(self.lens[idx].max()) - 1
+        i = idx.to(self.device, non_blocking=True)
+        target = self.target[i, :T]
+        return self.inputs[i, :T], target, target != self.pad[i].unsqueeze(1), self.weight[i]
+
+
+class TrainerGenerator(object):
+    """Trainer of the rule generator (reference src/trainer.py:291-485):
+    train / log_probability / next_relation_log_probability / beam_search /
+    sample / load / save, same arguments and outputs.
+
+    How it differs from the reference (not what it computes):
+      * train() draws the batch order from the reference's own shuffled
+        DataLoader (same RandomSampler, same global-RNG draws, so a seeded run
+        sees the same batches) but gathers each batch from a device-resident
+        padded rule table, and sums the logged loss on the device (one host
+        sync per print, not per step);
+      * beam_search() advances every relation's beam in one batched LSTM step
+        per rule position, feeding only the new token from the parent's cached
+        (h, c) (the LSTM is causal, so this equals re-running the prefix as
+        next_relation_log_probability does) and ranks candidates with a stable
+        descending sort in float64 — the reference's sorted(..., reverse=True)
+        over Python-float sums of the same float32 log-probabilities;
+      * sample() draws all relations' sequences in one batch per position.
+    """
+
+    def __init__(self, model, gpu):
+        self.model = model
+        self.device = torch.device("cpu") if gpu is None else torch.device(gpu)
+        model.to(self.device)
+
+    def train(self, rule_set, num_epoch=10000, lr=1e-3, print_every=100, batch_size=512):
+        """trainer.py:303-338."""
+        if comm.get_rank() == 0:
+            logging.info(">>>>> Generator: Training")
+        model = self.model
+        model.train()
+        table = _RuleTable(rule_set, self.device)
+        # indices only: the reference's DataLoader(rule_set, batch_size, shuffle=True) RNG use
+        order = torch_data.DataLoader(range(len(rule_set)), batch_size, shuffle=True)
+        iterator = Iterator(order)
+        optimizer = torch.optim.Adam(model.parameters(), lr=lr)
+        total_loss = torch.zeros((), dtype=torch.float64, device=self.device)
+        for epoch in range(num_epoch):
+            inputs, target, mask, weight = table.batch(next(iterator))
+            hidden = self.zero_state(inputs.size(0))
+            loss = model.loss(inputs, target, mask, weight, hidden)
+            loss.backward()
+            optimizer.step()
+            optimizer.zero_grad()
+            total_loss += loss.detach().double()
+            if (epoch + 1) % print_every == 0:
+                if comm.get_rank() == 0:
+                    logging.info("{} {} {:.6f}".format(epoch + 1, num_epoch, total_loss.item() / print_every))
+                total_loss.zero_()
+
+    def zero_state(self, batch_size):
+        shape = (self.model.num_layers, batch_size, self.model.hidden_dim)
+        h0 = torch.zeros(*shape, device=self.device)
+        return (h0, h0)
+
+    @torch.no_grad()
+    def log_probability(self, rules):
+        """Σ_t log p(token_t | prefix) of each [head, body...] rule, END
+        included (trainer.py:344-370)."""
+        if rules == []:
+            return []
+        model = self.model
+        model.eval()
+        L = max(len(r) for r in rules) + 1
+        seq = torch.full((len(rules), L), model.padding_idx, dtype=torch.long)
+        for k, r in enumerate(rules):
+            seq[k, :len(r)] = torch.tensor(r, dtype=torch.long)
+            seq[k, len(r)] = model.ending_idx
+        seq = seq.to(self.device)
+        inputs, target = seq[:, :-1], seq[:, 1:]
+        mask = target != model.padding_idx
+        logits, _ = model(inputs, inputs[:, 0], self.zero_state(len(rules)))
+        logp = torch.log_softmax(logits, -1)
+        picked = logp.gather(-1, torch.where(mask, target, torch.zeros_like(target)).unsqueeze(-1)).squeeze(-1)
+        return (picked * mask).sum(-1).cpu().numpy().tolist()
+
+    @torch.no_grad()
+    def next_relation_log_probability(self, seq, temperature):
+        """log_softmax(logits / T) of the token after seq (trainer.py:372-382)."""
+        model = self.model
+        model.eval()
+        inputs = torch.tensor([seq], dtype=torch.long, device=self.device)
+        logits, _ = model(inputs, inputs[:, 0], self.zero_state(1))
+        return torch.log_softmax(logits[0, -1, :] / temperature, dim=-1).cpu().numpy().tolist()
+
+    @torch.no_grad()
+    def beam_search(self, num_samples, max_len, temperature=0.2):
+        """Per head relation, the num_samples best-scoring rules of length
+        ≤ max_len, [head, body..., score] (trainer.py:384-411).  Beams of all
+        relations advance together: rows (relation, beam slot)."""
+        if comm.get_rank() == 0:
+            logging.info(">>>>> Generator: Rule generation with beam search")
+        model = self.model
+        model.eval()
+        dev = self.device
+        R, S, V, END = model.num_relations, num_samples, model.label_size, model.ending_idx
+        steps = max_len + 1
+        # live beams: tokens (R, s, k+1), score f64 (R, s), valid (R, s), LSTM state per row
+        tokens = torch.arange(R, device=dev).view(R, 1, 1)
+        score = torch.zeros(R, 1, dtype=torch.float64, device=dev)
+        valid = torch.ones(R, 1, dtype=torch.bool, device=dev)
+        head = torch.arange(R, device=dev)
+        logits, hidden = model(tokens.view(R, 1), head, self.zero_state(R))
+        found_tok = torch.zeros(R, 0, steps + 1, dtype=torch.long, device=dev)
+        found_score = torch.zeros(R, 0, dtype=torch.float64, device=dev)
+        neg = torch.tensor(float("-inf"), dtype=torch.float64, device=dev)
+        for k in range(steps):
+            s = score.size(1)
+            logp = torch.log_softmax(logits.view(R, s, V) / temperature, dim=-1).double()
+            cand = torch.where(valid.unsqueeze(-1), score.unsqueeze(-1) + logp, neg)  # (R, s, V)
+            # rules closed by END at this step, appended after the earlier ones (stable order)
+            pad = steps + 1 - (k + 2)
+            end_tok = torch.cat([tokens, torch.full((R, s, 1), END, dtype=torch.long, device=dev),
+                                 torch.full((R, s, pad), END, dtype=torch.long, device=dev)], dim=2)
+            all_tok = torch.cat([found_tok, end_tok], dim=1)
+            all_score = torch.cat([found_score, cand[:, :, END]], dim=1)
+            n_found = torch.cat([found_score > neg, valid], dim=1).sum(1)
+            keep = min(S, all_score.size(1))
+            srt, order = torch.sort(all_score, dim=1, descending=True, stable=True)
+            found_score = srt[:, :keep]
+            found_tok = all_tok.gather(1, order[:, :keep, None].expand(-1, -1, steps + 1))
+            found_score = torch.where(torch.arange(keep, device=dev) < n_found.unsqueeze(1), found_score, neg)
+            if k + 1 == steps:
+                break
+            # extend every live beam by each relation token (END excluded), keep the best S
+            ext = cand[:, :, :END].reshape(R, s * END)
+            n_live = valid.sum(1) * END
+            keep = min(S, s * END)
+            srt, order = torch.sort(ext, dim=1, descending=True, stable=True)
+            score = srt[:, :keep]
+            valid = torch.arange(keep, device=dev) < n_live.unsqueeze(1)
+            parent, tok = order[:, :keep] // END, order[:, :keep] % END
+            tokens = torch.cat([tokens.gather(1, parent[:, :, None].expand(-1, -1, k + 1)), tok.unsqueeze(-1)], 2)
+            rows = (parent + torch.arange(R, device=dev).unsqueeze(1) * s).reshape(-1)
+            hidden = tuple(x[:, rows] for x in hidden)
+            logits, hidden = model(tok.reshape(-1, 1), head.repeat_interleave(keep), hidden)
+        all_rules = []
+        tok_host = found_tok.cpu().tolist()
+        score_host = found_score.cpu().tolist()
+        for r in range(R):
+            for t, sc in zip(tok_host[r], score_host[r]):
+                if sc == float("-inf"):
+                    continue
+                all_rules.append(t[:t.index(END)] + [sc])
+        return all_rules
+
+    @torch.no_grad()
+    def sample(self, num_samples, max_len, temperature=1.0):
+        """num_samples sequences per head relation drawn from the generator,
+        deduplicated per relation, [head, body..., Σ log p] (trainer.py:413-465).
+        All relations are drawn together (one multinomial per position)."""
+        if comm.get_rank() == 0:
+            logging.info(">>>>> Generator: Rule generation with sampling")
+        model = self.model
+        model.eval()
+        dev = self.device
+        R, END = model.num_relations, model.ending_idx
+        N = R * num_samples
+        head = torch.arange(R, device=dev).repeat_interleave(num_samples)
+        rules = torch.full((N, max_len + 1), END, dtype=torch.long, device=dev)
+        rules[:, 0] = head
+        logp_sum = torch.zeros(N, max_len + 1, device=dev)
+        hidden = self.zero_state(N)
+        for pst in range(max_len):
+            logits, hidden = model(rules[:, pst:pst + 1], head, hidden)
+            logits = logits.squeeze(1) / temperature
+            draw = torch.multinomial(torch.softmax(logits, dim=-1), 1)
+            lp = torch.log_softmax(logits, dim=-1).gather(1, draw).squeeze(-1)
+            live = rules[:, pst] != END
+            rules[:, pst + 1] = torch.where(live, draw.squeeze(-1), rules[:, pst + 1])
+            logp_sum[:, pst + 1] = torch.where(live, lp, logp_sum[:, pst + 1])
+        length = (rules != END).sum(-1) - 1
+        total = logp_sum.sum(-1)
+        rules, length, total = rules.cpu().tolist(), length.cpu().tolist(), total.cpu().tolist()
+        all_rules = []
+        for r in range(R):
+            seen = dict()
+            for k in range(r * num_samples, (r + 1) * num_samples):
+                seen.setdefault(tuple(rules[k][:1 + length[k]] + [total[k]]), None)
+            all_rules += [list(x) for x in seen]
+        return all_rules
+
+    def load(self, checkpoint):
+        """trainer.py:467-475."""
+        if comm.get_rank() == 0:
+            logging.info("Load checkpoint from %s" % checkpoint)
+        state = torch.load(os.path.expanduser(checkpoint), map_location=self.device, weights_only=True)
+        self.model.load_state_dict(state["model"])
+
+    def save(self, checkpoint):
+        """trainer.py:477-485."""
+        if comm.get_rank() == 0:
+            logging.info("Save checkpoint to %s" % checkpoint)
+        torch.save({"model": self.model.state_dict()}, os.path.expanduser(checkpoint))

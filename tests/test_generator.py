@@ -1,0 +1,128 @@
+"""Rule generator + TrainerGenerator (reference src/generators.py:3-37,
+src/trainer.py:291-485) against the reference's own run of the
+run_rnnlogic.py sequence on UMLS (tests/golden/em_umls.npz, made by
+tools/make_golden_em.py).
+
+CPU: seeded init identical; generator pre-training (losses, weights, global
+RNG probes — the batch order comes from the same DataLoader draws);
+log_probability, next_relation_log_probability, beam_search.
+GPU: the same on cuda:0, then one EM iteration through the package (the
+Predictor on the HIP path): predictor losses, MRRs, H scores, posterior, the
+M-step's generator losses and final log-probabilities.
+
+Tolerances: the generator and the EM Predictor train in fp32 with a few
+dozen Adam steps, so weights and losses are compared at 2e-5 (abs, plus 1e-6
+for the reference's 6-decimal log lines); RNG probes, rules and mined-rule
+pools are exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import em_chain
+
+W_TOL = 2e-5
+
+
+def _close(a, b, tol):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = float(np.abs(a - b).max()) if a.size else 0.0
+    assert err <= tol, "max |err| %g > %g" % (err, tol)
+    return err
+
+
+def _check_states(got, want, tol):
+    assert sorted(got) == sorted(want)
+    for k in want:
+        _close(got[k], want[k], tol)
+
+
+def _check_generator_part(z, got):
+    _check_states(got["gen_init"], em_chain.state(z, "gen_init"), 0.0)
+    _close(got["pre_train/loss"], z["pre_train/loss"], W_TOL + 1e-6)
+    assert np.array_equal(got["probe/pre_train"], z["probe/pre_train"])
+    _check_states(got["gen_pre"], em_chain.state(z, "gen_pre"), W_TOL)
+    _close(got["pre/log_prob"], z["pre/log_prob"], 1e-4)
+    _close(got["pre/next_logp"], z["pre/next_logp"], 1e-4)
+    import json
+    em_chain.check_beam(got["pre/beam"], json.loads(str(z["pre/beam"])), 1e-4)
+    assert np.array_equal(got["probe/beam"], z["probe/beam"])
+
+
+def test_generator_chain_cpu():
+    z, got = em_chain.run(torch.device("cpu"))
+    _check_generator_part(z, got)
+
+
+def test_generator_state_dict_names():
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph
+    from rnnlogic_amd.generators import Generator
+    z, cfg = em_chain.fixture()
+    g = Generator(KnowledgeGraph(datasets.materialize("umls")), **cfg["gen"])
+    want = em_chain.state(z, "gen_init")
+    assert {k: tuple(v.shape) for k, v in g.state_dict().items()} == {k: v.shape for k, v in want.items()}
+
+
+def test_rule_dataset_and_table_match_collate():
+    """_RuleTable.batch gives the tensors RuleDataset.collate_fn gives."""
+    from rnnlogic_amd.data import RuleDataset
+    from rnnlogic_amd.trainer import _RuleTable
+    rules = [[3, 1, 2, 0.5], [4, 7, -1.25], [1, 2, 3, 4, 2.0], [5, 0.0]]
+    ds = RuleDataset(10, rules)
+    table = _RuleTable(ds, torch.device("cpu"))
+    for idx in ([0, 1, 2, 3], [1, 3], [2], [3, 0]):
+        want = RuleDataset.collate_fn([ds[i] for i in idx])
+        got = table.batch(torch.tensor(idx))
+        for a, b in zip(got, want):
+            assert torch.equal(a, b), (idx, a, b)
+
+
+def test_sample_shapes_and_dedupe_cpu():
+    """sample() is not pinned (device RNG streams differ from the reference);
+    check its output contract: [head, body..., log p], body ≤ max_len, one
+    entry per distinct sequence and head, log p = the generator's own
+    log_probability of the rule."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph
+    from rnnlogic_amd.generators import Generator
+    from rnnlogic_amd.trainer import TrainerGenerator
+    torch.manual_seed(0)
+    g = Generator(KnowledgeGraph(datasets.materialize("umls")), num_layers=1, embedding_dim=16, hidden_dim=16)
+    solver = TrainerGenerator(g, gpu=None)
+    out = solver.sample(20, 3)
+    seen = set()
+    for rule in out:
+        body = rule[1:-1]
+        assert 0 <= rule[0] < g.num_relations and len(body) <= 3
+        assert all(0 <= x < g.num_relations for x in body)
+        assert tuple(rule) not in seen
+        seen.add(tuple(rule))
+    # a sequence closed by END before max_len carries END's log p, as log_probability does
+    closed = [r for r in out if len(r) - 2 < 3][:50]
+    assert closed
+    lp = solver.log_probability([list(r[:-1]) for r in closed])
+    _close([r[-1] for r in closed], lp, 1e-4)
+
+
+@pytest.mark.gpu
+def test_em_iteration_gpu():
+    """run_rnnlogic.py:45-91 on cuda:0 through the package vs the reference run."""
+    z, got = em_chain.run(torch.device("cuda:0"), em=True)
+    _check_generator_part(z, got)
+    _check_states(got["pred_init"], em_chain.state(z, "pred_init"), 0.0)
+    _close(got["em/train_loss"], z["em/train_loss"], W_TOL + 1e-6)
+    assert np.array_equal(got["probe/em_train"], z["probe/em_train"])
+    _check_states(got["pred_trained"], em_chain.state(z, "pred_trained"), W_TOL)
+    print("EM: valid MRR %.9f (ref %.9f), test MRR %.9f (ref %.9f)" % (
+        got["em/valid_mrr"], z["em/valid_mrr"], got["em/test_mrr"], z["em/test_mrr"]))
+    _close(got["em/valid_mrr"], z["em/valid_mrr"], 1e-4)
+    _close(got["em/test_mrr"], z["em/test_mrr"], 1e-4)
+    _close(got["em/H"], z["em/H"], 1e-5)
+    _close(got["em/posterior"], z["em/posterior"], 1e-5)
+    assert np.array_equal(got["probe/em_H"], z["probe/em_H"])
+    _close(got["m_step/loss"], z["m_step/loss"], W_TOL + 1e-6)
+    assert np.array_equal(got["probe/m_step"], z["probe/m_step"])
+    _close(got["m_step/log_prob"], z["m_step/log_prob"], 1e-4)
+    _check_states(got["gen_m"], em_chain.state(z, "gen_m"), W_TOL)
