@@ -93,7 +93,27 @@ def time_forward(fn, reps):
     return (time.perf_counter() - t0) / reps
 
 
-def cpu_baseline(path, model, rows, threads, budget_s=20.0):
+def host_cores():
+    """The host's CPU count (nproc), the CPUs this process may run on (its
+    affinity mask) and the cgroup CPU quota, if any; `usable` = the smallest."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"nproc": nproc, "affinity": affinity, "cgroup_quota": quota, "usable": usable}
+
+
+def cpu_baseline(path, model, rows, threads, cores, budget_s=20.0):
     """The reference's own C++ path counter (miner/rnnlogic.cpp rule_destination
     via ReasoningPredictor::out_test, compiled from the reference sources into
     oracle/_ref) on the host cores, over a bounded prefix of the test split."""
@@ -114,8 +134,10 @@ def cpu_baseline(path, model, rows, threads, budget_s=20.0):
     finally:
         miner.close()
     return {"value": round(sample / sec, 1), "unit": "queries/s", "cores": threads, "kind": "reference",
+            "host": cores,
             "sample": "first %d FB15k-237 test triples, grounding only (ReasoningPredictor::out_test, "
-                      "%d pthreads), %.1f s" % (sample, threads, sec)}
+                      "%d pthreads = the CPUs this process may use; host nproc %d), %.1f s"
+                      % (sample, threads, cores["nproc"], sec)}
 
 
 def reference_pytorch_baseline(model, graph, test_set, dev, feature, budget_s=15.0):
@@ -194,7 +216,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--feature", default="RotatE", choices=["RotatE", "bias"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the CPU baseline (default: every core this process may run on)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed steps (no extra lines, baselines or clock probe): the command the "
                          "committed rocprofv3 summaries profile, so every launch of a kernel has the same shape")
@@ -349,7 +372,8 @@ def main():
         return
 
     E = graph.entity_size
-    threads = args.cpu_threads
+    cores = host_cores()
+    threads = args.cpu_threads or cores["usable"]
     (F, T, P), C = algorithmic_work(model, graph, rows, threads)
     # ALG_BYTES = 12 F + 12 T + 8 P + 4 B|E| + X
     ground_bytes = 12 * F + 12 * T + 8 * P + 4 * nq * E
@@ -426,7 +450,7 @@ def main():
     }
     out.update(extra)
     if not args.no_cpu_baseline and not args.profile_only and world == 1:
-        out["cpu_baseline"] = cpu_baseline(graph.data_path, model, rows, threads)
+        out["cpu_baseline"] = cpu_baseline(graph.data_path, model, rows, threads, cores)
         with contextlib.redirect_stdout(sys.stderr):
             out["reference_pytorch"] = reference_pytorch_baseline(model, graph, test_set, dev, args.feature)
     print(json.dumps(out), flush=True)
