@@ -14,9 +14,15 @@ tables are absent from the reference mount, so both are seeded synthetic
 Timed region per step: rule embeddings (LSTM over all rules) + node
 aggregates, the RotatE base-score kernel and the fused grounding/aggregation/
 MLP kernel over all rows, and the overflow status check — inputs already in
-HBM.  N ranks (torchrun, one per GPU) each run the full split: per-rank work
-is fixed ("scaling": "weak"); there is no collective in the timed region
-(queries are independent; DESIGN.md "Multi-GPU").
+HBM.  N ranks (torchrun, one per GPU) split the test batches with the
+reference evaluate()'s DistributedSampler(test_set, N, rank) (shuffled with
+seed 0, padded by repeating batches so every rank holds the same count;
+src/trainer.py:150), the KG replicated on every GPU: the total work is fixed
+("scaling": "strong") and `value` counts each of the split's 40,932 queries
+once (the sampler's padding duplicates are extra work, not extra queries).
+There is no collective in the timed region (queries are independent;
+DESIGN.md "Multi-GPU").  At N > 1 a secondary line `weak_replicated` times
+every rank on the whole split.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--feature RotatE|bias]
 """
@@ -65,6 +71,17 @@ def build_workload(feature):
     rows = np.asarray([x for b in test_set.batches for x in b], dtype=np.int64)
     model.train_set = train_set  # for the train-mode line (not a module attribute of the reference)
     return graph, test_set, model, rows
+
+
+def shard_rows(test_set, world, rank):
+    """Rows of this rank's batches under the reference evaluate()'s sampler:
+    DistributedSampler(test_set, world, rank) — shuffle with seed 0, epoch 0,
+    padded by repeating indices so len % world == 0 (src/trainer.py:150).
+    Returns (rows (n, 3) int64, batch indices)."""
+    from torch.utils import data as torch_data
+    idx = list(iter(torch_data.DistributedSampler(test_set, world, rank)))
+    rows = np.asarray([x for i in idx for x in test_set.batches[i]], dtype=np.int64).reshape(-1, 3)
+    return rows, idx
 
 
 def train_rows(train_set, n_rows):
@@ -226,6 +243,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d: launch N>1 with torch.distributed.run "
+                         "--nproc-per-node N" % (args.gpus, world))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -236,10 +256,12 @@ def main():
         dist.barrier()
 
     with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
-        graph, test_set, model, rows = build_workload(args.feature)
+        graph, test_set, model, all_rows = build_workload(args.feature)
     model = model.to(dev).eval()
-    h = torch.from_numpy(rows[:, 0]).to(dev)
-    r = torch.from_numpy(rows[:, 1]).to(dev)
+    n_split = len(all_rows)
+    rows, shard = (all_rows, list(range(len(test_set)))) if world == 1 else shard_rows(test_set, world, rank)
+    h = torch.from_numpy(np.ascontiguousarray(rows[:, 0])).to(dev)
+    r = torch.from_numpy(np.ascontiguousarray(rows[:, 1])).to(dev)
     nq = len(rows)
     torch.cuda.synchronize(dev)
 
@@ -266,6 +288,40 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    rows_per_rank = [nq]
+    if world > 1:
+        cnt = torch.tensor([nq], dtype=torch.int64, device=dev)
+        parts = [torch.empty_like(cnt) for _ in range(world)]
+        dist.all_gather(parts, cnt)
+        rows_per_rank = [int(x.item()) for x in parts]
+
+    # secondary at N > 1: every rank on the whole split (replicated, weak scaling)
+    weak = None
+    if world > 1 and not args.profile_only:
+        ah = torch.from_numpy(np.ascontiguousarray(all_rows[:, 0])).to(dev)
+        ar = torch.from_numpy(np.ascontiguousarray(all_rows[:, 1])).to(dev)
+
+        def full_step():
+            model.invalidate_cache()
+            with torch.no_grad():
+                return model.forward_rows(ah, ar, None)
+        full_step()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            full_step()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tw = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        weak = {"queries_per_s": round(n_split * args.steps * world / float(tw.item()), 1),
+                "ms_per_step": round(float(tw.item()) / args.steps * 1e3, 3), "rows_per_rank": n_split,
+                "scaling": "weak",
+                "note": "every rank runs the whole test split (replicated work; value counts world x rows)"}
+        del ah, ar
 
     # per-kernel device time (HIP events on the launch stream).  With the
     # RotatE feature the forward overlaps: the grounding runs on a side stream
@@ -285,7 +341,9 @@ def main():
     overlapped = args.feature == "RotatE" and model.overlap
     n_rot = model.overlap_chunks if overlapped else 1  # RotatE launches per step
     # the grounding + scoring kernels alone (one untimed one-stream launch), for their roofline
-    if not args.profile_only:
+    if world > 1:  # the work-count fixture describes the whole split, not a shard
+        ground_ms, ground_how = None, None
+    elif not args.profile_only:
         ground_ms, ground_how = isolated_ground_ms(model, graph, h, r, dev), \
             "one untimed one-stream launch over all rows (isolated from RotatE)"
     elif args.feature != "RotatE":
@@ -374,7 +432,7 @@ def main():
     E = graph.entity_size
     cores = host_cores()
     threads = args.cpu_threads or cores["usable"]
-    (F, T, P), C = algorithmic_work(model, graph, rows, threads)
+    (F, T, P), C = algorithmic_work(model, graph, all_rows, threads)
     # ALG_BYTES = 12 F + 12 T + 8 P + 4 B|E| + X
     ground_bytes = 12 * F + 12 * T + 8 * P + 4 * nq * E
     D = model.RotatE.emb_dim if args.feature == "RotatE" else 0
@@ -425,22 +483,25 @@ def main():
         dominant = ground
     out = {
         "metric": METRIC,
-        "value": round(nq * args.steps * world / elapsed, 1),
+        "value": round(n_split * args.steps / elapsed, 1),
         "unit": "queries/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
-        "config": {"workload": "FB15k-237 test split per rank: %d batches, %d queries; PredictorPlus(lstm,3,16,sum)"
+        "config": {"workload": "FB15k-237 test split: %d batches, %d queries, sharded over %d rank(s) by the "
+                               "reference evaluate()'s DistributedSampler; PredictorPlus(lstm,3,16,sum)"
                                " + %s; rnnlogic_rules.txt (%d rules, L<=3); seeded synthetic train graph%s"
-                               % (len(test_set), nq, "RotatE(D=1000,gamma=9)" if args.feature == "RotatE" else "bias",
+                               % (len(test_set), n_split, world,
+                                  "RotatE(D=1000,gamma=9)" if args.feature == "RotatE" else "bias",
                                   model.num_rules, " and RotatE tables" if args.feature == "RotatE" else ""),
-                   "batch_size": 32, "parallelism": "dp%d (queries sharded, KG replicated)" % world},
+                   "batch_size": 32, "parallelism": "dp%d (test batches sharded, KG replicated)" % world,
+                   "rows_per_rank": rows_per_rank, "batches_per_rank": len(shard)},
         "roofline": dominant,
         "kernels_ms": {"rule_encoder+node_weights": round(nodes_ms, 3), "base_score": round(base_ms, 3),
                        "tail_after_base": round(tail_ms, 3), "ground+score_isolated": round(ground_ms, 3)},
@@ -449,6 +510,8 @@ def main():
         "roofline_grounding": ground,
     }
     out.update(extra)
+    if weak is not None:
+        out["weak_replicated"] = weak
     if not args.no_cpu_baseline and not args.profile_only and world == 1:
         out["cpu_baseline"] = cpu_baseline(graph.data_path, model, rows, threads, cores)
         with contextlib.redirect_stdout(sys.stderr):

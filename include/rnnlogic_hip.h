@@ -281,6 +281,14 @@ int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *
 int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
                    const int64_t *row_keys, int32_t n_rows, int32_t width, float *out, void *stream);
 
+/* Evaluation filter rows (reference ValidDataset / TestDataset.__getitem__,
+ * src/data.py:250-255 and 287-291): out (n_rows x width, u8 0/1) is 1 except
+ * at the values listed for row_keys[i] — with the hr2oo / hr2ooo lists, the
+ * reference's `flag` (true = a ranked competitor). Same map layout as
+ * rnnl_multi_hot. */
+int rnnl_filter_flags(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
+                      const int64_t *row_keys, int32_t n_rows, int32_t width, uint8_t *out, void *stream);
+
 /* ---------------------------------------------------------- rule mining --
  * The reference miner's RuleMiner::search (miner/rnnlogic.cpp:505-589 with
  * KnowledgeGraph::rule_search :350-382) on the GPU: for every train triple

@@ -7,7 +7,10 @@ a node); a gloo group is kept beside it for CPU tensors, as in the reference
 (comm.py:50-65).  reduce/stack/cat take a tensor or a nested dict/list/tuple of
 tensors and return the same structure: every leaf of one dtype travels in one
 flat buffer, so a call costs one collective per dtype (cat: two, the second
-after a size exchange), not one per leaf.
+after a size exchange), not one per leaf.  bool leaves travel as uint8 (RCCL
+has no bool) and come back as bool, as in the reference (comm.py:162-172).
+`dst` (reduce) leaves the result on that rank only (dist.reduce); stack and
+cat accept `dst` and return the gathered result on every rank.
 """
 import multiprocessing
 import os
@@ -93,26 +96,41 @@ def _by_dtype(leaves):
     return groups
 
 
-def reduce(obj, op="sum"):
-    """All-reduce every tensor of `obj` (comm.py:136-175); op "sum" or "mean"."""
+_OPS = {"sum": dist.ReduceOp.SUM, "mean": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN,
+        "max": dist.ReduceOp.MAX, "product": dist.ReduceOp.PRODUCT}
+
+
+def _wire(t):
+    """The tensor as sent: bool -> uint8 (no bool in RCCL)."""
+    return t.to(torch.uint8) if t.dtype == torch.bool else t
+
+
+def reduce(obj, op="sum", dst=None):
+    """Reduce every tensor of `obj` over the ranks (comm.py:136-175); op is
+    "sum", "mean", "min", "max" or "product".  With dst the result is valid
+    on that rank only."""
+    if op not in _OPS:
+        raise ValueError("Unknown reduction `%s`" % op)
     world = get_world_size()
     if world == 1:
         return obj
     leaves = _leaves(obj, [])
     result = [None] * len(leaves)
     for dtype, idx in _by_dtype(leaves).items():
-        flat = torch.cat([leaves[i].reshape(-1) for i in idx])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=get_group(flat.device))
+        flat = torch.cat([_wire(leaves[i]).reshape(-1) for i in idx])
+        group = get_group(flat.device)
+        if dst is None:
+            dist.all_reduce(flat, op=_OPS[op], group=group)
+        else:
+            dist.reduce(flat, dst=dst, op=_OPS[op], group=group)
         if op == "mean":
             flat = flat / world
-        elif op != "sum":
-            raise ValueError("Unknown reduction `%s`" % op)
         for i, part in zip(idx, flat.split([leaves[i].numel() for i in idx])):
-            result[i] = part.view_as(leaves[i])
+            result[i] = part.view(leaves[i].shape).to(dtype)
     return _rebuild(obj, iter(result))
 
 
-def stack(obj):
+def stack(obj, dst=None):
     """All-gather every tensor of `obj` and stack along a new dim 0
     (comm.py:178-211); every rank must pass equal shapes."""
     world = get_world_size()
@@ -121,16 +139,16 @@ def stack(obj):
     leaves = _leaves(obj, [])
     result = [None] * len(leaves)
     for dtype, idx in _by_dtype(leaves).items():
-        flat = torch.cat([leaves[i].reshape(-1) for i in idx])
+        flat = torch.cat([_wire(leaves[i]).reshape(-1) for i in idx])
         parts = [torch.empty_like(flat) for _ in range(world)]
         dist.all_gather(parts, flat, group=get_group(flat.device))
         gathered = torch.stack(parts)
         for i, part in zip(idx, gathered.split([leaves[i].numel() for i in idx], dim=1)):
-            result[i] = part.reshape((world,) + tuple(leaves[i].shape))
+            result[i] = part.reshape((world,) + tuple(leaves[i].shape)).to(dtype)
     return _rebuild(obj, iter(result))
 
 
-def cat(obj):
+def cat(obj, dst=None):
     """All-gather every tensor of `obj` and concatenate along dim 0
     (comm.py:214-256); dim 0 may differ across ranks (sizes are exchanged
     first, payloads padded to the largest rank)."""
@@ -148,7 +166,7 @@ def cat(obj):
         all_sizes = torch.stack(all_sizes).cpu()          # (world, n_leaves)
         totals = all_sizes.sum(1)
         cap = int(totals.max())
-        flat = torch.cat([leaves[i].reshape(-1) for i in idx])
+        flat = torch.cat([_wire(leaves[i]).reshape(-1) for i in idx])
         padded = torch.zeros(cap, dtype=flat.dtype, device=device)
         padded[:flat.numel()] = flat
         gathered = [torch.empty_like(padded) for _ in range(world)]
@@ -160,5 +178,5 @@ def cat(obj):
                 pieces[j].append(part)
         for j, i in enumerate(idx):
             tail = tuple(leaves[i].shape[1:])
-            result[i] = torch.cat(pieces[j]).view((-1,) + tail)
+            result[i] = torch.cat(pieces[j]).view((-1,) + tail).to(dtype)
     return _rebuild(obj, iter(result))

@@ -190,6 +190,38 @@ class TrainDataset(Dataset):
         return all_h, all_r, all_t, target, torch.LongTensor(edges_to_remove)
 
 
+class _DeviceLists(object):
+    """A {key: [values]} map (hr2o / hr2oo / hr2ooo, keys r * |E| + h) laid out
+    once on the device as a CSR with ascending keys — the input of
+    rnnl_multi_hot / rnnl_filter_flags."""
+
+    def __init__(self, lists, device):
+        keys = np.fromiter(lists.keys(), dtype=np.int64, count=len(lists))
+        order = np.argsort(keys, kind="stable")
+        vals_l = list(lists.values())
+        lens = np.asarray([len(vals_l[i]) for i in order], dtype=np.int64)
+        offs = np.zeros(len(order) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        vals = np.fromiter((t for i in order for t in vals_l[i]), dtype=np.int32, count=int(offs[-1]))
+        self.device = device
+        self.keys = torch.from_numpy(keys[order]).to(device)
+        self.offs = torch.from_numpy(offs).to(device)
+        self.vals = torch.from_numpy(vals).to(device)
+
+    def rows(self, fn, row_keys, width, out):
+        _native.call(fn, self.keys.data_ptr(), self.offs.data_ptr(), self.vals.data_ptr(), self.keys.numel(),
+                     row_keys.data_ptr(), row_keys.numel(), width, out.data_ptr(),
+                     torch.cuda.current_stream(self.device).cuda_stream)
+        return out
+
+
+def _batch_rows(batches, indices, device):
+    """(all_h, all_r, all_t) of the concatenated batches[indices], on device."""
+    flat = [x for i in indices for x in batches[i]]
+    hrt = torch.tensor(flat, dtype=torch.int64).view(-1, 3).to(device, non_blocking=True)
+    return hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
+
+
 class DeviceTrainBatches(object):
     """TrainDataset rows built on the device: item `idx`
     equals `train_set[idx]` — (all_h, all_r, all_t, target, edges_to_remove),
@@ -204,16 +236,7 @@ class DeviceTrainBatches(object):
         self.device = torch.device(device)
         g = train_set.graph
         E = g.entity_size
-        keys = np.fromiter(g.hr2o.keys(), dtype=np.int64, count=len(g.hr2o))
-        order = np.argsort(keys, kind="stable")
-        lists = list(g.hr2o.values())
-        lens = np.asarray([len(lists[i]) for i in order], dtype=np.int64)
-        offs = np.zeros(len(order) + 1, dtype=np.int64)
-        np.cumsum(lens, out=offs[1:])
-        vals = np.fromiter((t for i in order for t in lists[i]), dtype=np.int32, count=int(offs[-1]))
-        self.keys = torch.from_numpy(keys[order]).to(self.device)
-        self.offs = torch.from_numpy(offs).to(self.device)
-        self.vals = torch.from_numpy(vals).to(self.device)
+        self.hr2o = _DeviceLists(g.hr2o, self.device)
         # relation-local edge ids: key (r * |E| + t) * |E| + h -> id, sorted
         ek, ev = [], []
         for r, m in enumerate(g.relation2ht2index):
@@ -233,19 +256,41 @@ class DeviceTrainBatches(object):
     def __getitem__(self, idx):
         g = self.train_set.graph
         E = g.entity_size
-        hrt = torch.tensor(self.train_set.batches[idx], dtype=torch.int64).view(-1, 3).to(self.device,
-                                                                                        non_blocking=True)
-        all_h, all_r, all_t = hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
+        all_h, all_r, all_t = _batch_rows(self.train_set.batches, [idx], self.device)
         B = all_h.numel()
         target = torch.empty((B, E), dtype=torch.float32, device=self.device)
-        row_keys = (all_r * E + all_h).contiguous()
-        _native.call("rnnl_multi_hot", self.keys.data_ptr(), self.offs.data_ptr(), self.vals.data_ptr(),
-                     self.keys.numel(), row_keys.data_ptr(), B, E, target.data_ptr(),
-                     torch.cuda.current_stream(self.device).cuda_stream)
+        self.hr2o.rows("rnnl_multi_hot", (all_r * E + all_h).contiguous(), E, target)
         ekey = (all_r * E + all_t) * E + all_h
         pos = torch.searchsorted(self.edge_keys, ekey).clamp(max=max(self.edge_keys.numel() - 1, 0))
         etr = self.edge_ids[pos]
         return all_h, all_r, all_t, target, etr
+
+
+class DeviceEvalBatches(object):
+    """ValidDataset / TestDataset rows built on the device:
+    item `idx` equals `eval_set[idx]` — (all_h, all_r, all_t, flag), reference
+    src/data.py:250-255 / 287-291 — with the filter row from
+    rnnl_filter_flags over a CSR of hr2oo / hr2ooo.  `rows(indices)` gives
+    the concatenation of many batches with one launch."""
+
+    def __init__(self, eval_set, device):
+        self.eval_set = eval_set
+        self.device = torch.device(device)
+        self.lists = _DeviceLists(getattr(eval_set.graph, eval_set.filter_attr), self.device)
+
+    def __len__(self):
+        return len(self.eval_set)
+
+    def rows(self, indices):
+        E = self.eval_set.graph.entity_size
+        all_h, all_r, all_t = _batch_rows(self.eval_set.batches, indices, self.device)
+        flag = torch.empty((all_h.numel(), E), dtype=torch.bool, device=self.device)
+        if all_h.numel():
+            self.lists.rows("rnnl_filter_flags", (all_r * E + all_h).contiguous(), E, flag.view(torch.uint8))
+        return all_h, all_r, all_t, flag
+
+    def __getitem__(self, idx):
+        return self.rows([idx])
 
 
 class _EvalDataset(Dataset):

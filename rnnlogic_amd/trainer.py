@@ -16,13 +16,14 @@ import logging
 import os
 from itertools import islice
 
+import numpy as np
 import torch
 from torch import distributed as dist
 from torch import nn
 from torch.utils import data as torch_data
 
 from . import comm
-from .data import DeviceTrainBatches, Iterator
+from .data import DeviceEvalBatches, DeviceTrainBatches, Iterator
 
 
 class _SizedIter(object):
@@ -187,31 +188,43 @@ class TrainerPredictor(object):
     @staticmethod
     def rank_metrics(ranks, expectation=True):
         """trainer.py:207-238 on an (N, 5) [h, r, t, L, H] list: metrics over the
-        unique (h, r, t), divided by N (the sampler's padding included)."""
-        query2LH = dict()
-        for h, r, t, L, H in ranks:
-            query2LH[(h, r, t)] = (L, H)
-        hit1, hit3, hit10, mr, mrr = 0.0, 0.0, 0.0, 0.0, 0.0
-        for (L, H) in query2LH.values():
-            if expectation:
-                for rank in range(L, H):
-                    if rank <= 1:
-                        hit1 += 1.0 / (H - L)
-                    if rank <= 3:
-                        hit3 += 1.0 / (H - L)
-                    if rank <= 10:
-                        hit10 += 1.0 / (H - L)
-                    mr += rank / (H - L)
-                    mrr += 1.0 / rank / (H - L)
-            else:
-                rank = H - 1
-                hit1 += rank <= 1
-                hit3 += rank <= 3
-                hit10 += rank <= 10
-                mr += rank
-                mrr += 1.0 / rank
-        n = len(ranks)
-        return dict(Data=len(query2LH), Hit1=hit1 / n, Hit3=hit3 / n, Hit10=hit10 / n, MR=mr / n, MRR=mrr / n)
+        unique (h, r, t) (a later row of the same triple replaces an earlier
+        one, as the reference's dict does), divided by N (the sampler's padding
+        included).  The expectation over ranks L..H-1 is in closed form
+        instead of the reference's loop over every rank: per query, with
+        n = H - L, Hit@k = #{rank <= k} / n, MR = (L + H - 1) / 2 and
+        MRR = (Harm(H - 1) - Harm(L - 1)) / n in float64 (a direct sum for
+        n <= 256, prefix harmonic numbers beyond)."""
+        a = np.asarray(ranks, dtype=np.int64).reshape(-1, 5)
+        n_rows = len(a)
+        if n_rows == 0:
+            return dict(Data=0, Hit1=0.0, Hit3=0.0, Hit10=0.0, MR=0.0, MRR=0.0)
+        # last occurrence of each (h, r, t)
+        _, first_rev = np.unique(a[::-1, :3], axis=0, return_index=True)
+        q = a[::-1][first_rev]
+        L, H = q[:, 3].astype(np.int64), q[:, 4].astype(np.int64)
+        if not expectation:
+            rank = (H - 1).astype(np.float64)
+            hit = lambda k: float((rank <= k).sum())  # noqa: E731
+            m = dict(Hit1=hit(1), Hit3=hit(3), Hit10=hit(10), MR=float(rank.sum()), MRR=float((1.0 / rank).sum()))
+        else:
+            n = (H - L).astype(np.float64)
+            hit = lambda k: float((np.clip(np.minimum(k, H - 1) - L + 1, 0, None) / n).sum())  # noqa: E731
+            mr = float(((L + H - 1) / 2.0).sum())
+            inv = np.zeros(len(q), dtype=np.float64)
+            short = (H - L) <= 256
+            if short.any():
+                Ls, Hs = L[short], H[short]
+                k = np.arange(256, dtype=np.int64)
+                rk = Ls[:, None] + k[None, :]
+                inv[short] = np.where(rk < Hs[:, None], 1.0 / rk, 0.0).sum(1)
+            if (~short).any():
+                harm = np.concatenate([[0.0], np.cumsum(1.0 / np.arange(1, int(H.max()), dtype=np.float64))])
+                inv[~short] = harm[H[~short] - 1] - harm[L[~short] - 1]
+            m = dict(Hit1=hit(1), Hit3=hit(3), Hit10=hit(10), MR=mr, MRR=float((inv / n).sum()))
+        out = {k: v / n_rows for k, v in m.items()}
+        out["Data"] = len(q)
+        return out
 
     @torch.no_grad()
     def evaluate(self, split, expectation=True):
@@ -219,30 +232,33 @@ class TrainerPredictor(object):
         if comm.get_rank() == 0:
             logging.info(">>>>> Predictor: Evaluating on {}".format(split))
         test_set = getattr(self, "%s_set" % split)
-        _, dataloader = self._loader(test_set)
         model = self.model
         model.eval()
         E = test_set.graph.entity_size
-        hs, rs, ts, flags = [], [], [], []
-        for batch in dataloader:
-            all_h, all_r, all_t, flag = [x.squeeze(0) for x in batch]
-            hs.append(all_h)
-            rs.append(all_r)
-            ts.append(all_t)
-            flags.append(flag)
+        dev = self.device
         ranks = torch.zeros((0, 5), dtype=torch.long)
-        if hs:
-            all_h, all_r, all_t = torch.cat(hs), torch.cat(rs), torch.cat(ts)
-            dev = self.device
-            all_h, all_r, all_t = all_h.to(dev), all_r.to(dev), all_t.to(dev)
-            if hasattr(model, "forward_rows") and dev.type == "cuda":
+        if dev.type == "cuda" and hasattr(model, "forward_rows"):
+            # the rank's sampler batches at once: rows + filter flags built on
+            # the device (rnnl_filter_flags), one forward over all rows
+            sampler = torch_data.DistributedSampler(test_set, self.world_size, self.rank)
+            torch.empty((), dtype=torch.int64).random_()  # the reference DataLoader's base-seed draw
+            if not hasattr(self, "_dev_eval"):
+                self._dev_eval = {}
+            key = id(test_set)
+            if key not in self._dev_eval:
+                self._dev_eval[key] = DeviceEvalBatches(test_set, dev)
+            all_h, all_r, all_t, flag = self._dev_eval[key].rows(list(iter(sampler)))
+            if all_h.numel():
                 logits, mask = model.forward_rows(all_h, all_r, None)
-            else:  # per batch, as the reference (e.g. Predictor)
-                out = [model(h.to(dev), r.to(dev), None) for h, r in zip(hs, rs)]
-                logits, mask = torch.cat([o[0] for o in out]), torch.cat([o[1] for o in out])
-            flag = torch.cat(flags).to(dev)
-            L, H = self.filtered_ranks(logits, mask, flag, all_t, E)
-            ranks = torch.stack([all_h, all_r, all_t, L, H], 1).to(torch.long)
+                L, H = self.filtered_ranks(logits, mask, flag, all_t, E)
+                ranks = torch.stack([all_h, all_r, all_t, L, H], 1).to(torch.long)
+        else:  # per batch, as the reference (CPU, or a model without forward_rows)
+            _, dataloader = self._loader(test_set)
+            for batch in dataloader:
+                all_h, all_r, all_t, flag = [x.squeeze(0).to(dev) for x in batch]
+                logits, mask = model(all_h, all_r, None)
+                L, H = self.filtered_ranks(logits, mask, flag, all_t, E)
+                ranks = torch.cat([ranks.to(dev), torch.stack([all_h, all_r, all_t, L, H], 1).to(torch.long)])
         if self.world_size > 1:
             ranks = comm.cat(ranks.to(self.device))
         m = self.rank_metrics(ranks.cpu().numpy().tolist(), expectation)

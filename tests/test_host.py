@@ -128,7 +128,7 @@ def test_device_train_batches_tables():
     from rnnlogic_amd.data import DeviceTrainBatches, KnowledgeGraph, TrainDataset
     graph = KnowledgeGraph(datasets.materialize("umls"))
     db = DeviceTrainBatches(TrainDataset(graph, 32), torch.device("cpu"))
-    keys, offs, vals = db.keys.numpy(), db.offs.numpy(), db.vals.numpy()
+    keys, offs, vals = db.hr2o.keys.numpy(), db.hr2o.offs.numpy(), db.hr2o.vals.numpy()
     assert (np.diff(keys) > 0).all() and len(offs) == len(keys) + 1
     E = graph.entity_size
     for h, r, t in graph.train_facts[::97]:
@@ -137,3 +137,20 @@ def test_device_train_batches_tables():
         assert list(vals[offs[i]:offs[i + 1]]) == graph.hr2o[graph.encode_hr(h, r)]
         j = np.searchsorted(db.edge_keys.numpy(), (r * E + t) * E + h)
         assert db.edge_ids.numpy()[j] == graph.relation2ht2index[r][graph.encode_ht(h, t)]
+
+
+def test_device_eval_batches_tables():
+    """The filter lists behind data.DeviceEvalBatches (hr2oo for valid, hr2ooo
+    for test; reference src/data.py:250-255, 287-291) as an ascending-key CSR."""
+    import numpy as np
+    import torch
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import DeviceEvalBatches, KnowledgeGraph, TestDataset, ValidDataset
+    graph = KnowledgeGraph(datasets.materialize("umls"))
+    for ds, lists in ((ValidDataset(graph, 32), graph.hr2oo), (TestDataset(graph, 32), graph.hr2ooo)):
+        db = DeviceEvalBatches(ds, torch.device("cpu"))
+        keys, offs, vals = db.lists.keys.numpy(), db.lists.offs.numpy(), db.lists.vals.numpy()
+        assert (np.diff(keys) > 0).all() and len(keys) == len(lists)
+        for k, v in list(lists.items())[::13]:
+            i = np.searchsorted(keys, k)
+            assert keys[i] == k and list(vals[offs[i]:offs[i + 1]]) == v

@@ -88,6 +88,20 @@ def _worker(rank, world, port, out_dir):
     ct = comm.cat(x)
     res["cat_a"] = ct["a"].tolist()
     res["cat_b"] = ct["b"][0].tolist()
+    # the other reductions, a dst reduce, and bool leaves (sent as uint8, returned as bool)
+    v = torch.tensor([rank + 1.0, 5.0 - rank])
+    res["min"] = comm.reduce(v.clone(), "min").tolist()
+    res["max"] = comm.reduce(v.clone(), "max").tolist()
+    res["product"] = comm.reduce(v.clone(), "product").tolist()
+    res["mean"] = comm.reduce(v.clone(), "mean").tolist()
+    res["dst"] = comm.reduce(v.clone(), "sum", dst=0).tolist()
+    b = torch.tensor([rank == 0, True, False])
+    rb = comm.reduce({"b": b}, "max")["b"]
+    res["bool_reduce"] = (str(rb.dtype), rb.tolist())
+    sb = comm.stack(b, dst=1)
+    res["bool_stack"] = (str(sb.dtype), sb.tolist())
+    cb = comm.cat([b[:rank + 1]])[0]
+    res["bool_cat"] = (str(cb.dtype), cb.tolist())
     # sharded evaluate
     fx, train_set, valid_set, test_set = _setup()
     solver = TrainerPredictor(GoldenScores(fx), train_set, valid_set, test_set, None, gpus=None)
@@ -106,6 +120,12 @@ def test_gloo_world2_comm_and_sharded_evaluate(tmp_path):
         assert res[r]["stack"] == [[1.0] * 3, [2.0] * 3]
         assert res[r]["cat_a"] == [1.0] * 3 + [2.0] * 3
         assert res[r]["cat_b"] == [0, 1] + [0, 1, 2]
+        assert res[r]["min"] == [1.0, 4.0] and res[r]["max"] == [2.0, 5.0]
+        assert res[r]["product"] == [2.0, 20.0] and res[r]["mean"] == [1.5, 4.5]
+        assert res[r]["bool_reduce"] == ("torch.bool", [True, True, False])
+        assert res[r]["bool_stack"] == ("torch.bool", [[True, True, False], [False, True, False]])
+        assert res[r]["bool_cat"] == ("torch.bool", [True, False, True])
+    assert res[0]["dst"] == [3.0, 9.0]
     # both ranks agree; the gathered ranks (padding duplicates included) give
     # the reference's formula over the padded shard union
     assert res[0]["mrr"] == res[1]["mrr"]
@@ -124,3 +144,54 @@ def test_gloo_world2_comm_and_sharded_evaluate(tmp_path):
     assert abs(res[0]["mrr"] - want) < 1e-12
     if len(test_set) % world == 0:
         assert abs(res[0]["mrr"] - float(fx.z["eval/mrr"])) < 1e-12
+
+
+def _loop_metrics(ranks, expectation):
+    """The reference's own loop (trainer.py:207-238), for the closed form."""
+    query2LH = dict()
+    for h, r, t, L, H in ranks:
+        query2LH[(h, r, t)] = (L, H)
+    hit1, hit3, hit10, mr, mrr = 0.0, 0.0, 0.0, 0.0, 0.0
+    for (L, H) in query2LH.values():
+        if expectation:
+            for rank in range(L, H):
+                if rank <= 1:
+                    hit1 += 1.0 / (H - L)
+                if rank <= 3:
+                    hit3 += 1.0 / (H - L)
+                if rank <= 10:
+                    hit10 += 1.0 / (H - L)
+                mr += rank / (H - L)
+                mrr += 1.0 / rank / (H - L)
+        else:
+            rank = H - 1
+            hit1 += rank <= 1
+            hit3 += rank <= 3
+            hit10 += rank <= 10
+            mr += rank
+            mrr += 1.0 / rank
+    n = len(ranks)
+    return dict(Data=len(query2LH), Hit1=hit1 / n, Hit3=hit3 / n, Hit10=hit10 / n, MR=mr / n, MRR=mrr / n)
+
+
+@pytest.mark.parametrize("expectation", [True, False])
+def test_closed_form_metrics_match_the_loop(expectation):
+    """rank_metrics' closed form (Hit@k counts, MR mean, harmonic-number MRR)
+    equals the reference loop to 1e-12 on ragged (L, H) ranges — short and
+    |E|-long ranges, duplicate (h, r, t) rows whose later (L, H) wins — and on
+    the UMLS fixture's ranks."""
+    from rnnlogic_amd.trainer import TrainerPredictor
+    rng = np.random.default_rng(0)
+    E = 40943
+    rows = []
+    for i in range(3000):
+        L = int(rng.integers(1, 200)) if i % 3 else int(rng.integers(1, E))
+        H = L + 1 + (int(rng.integers(0, 5)) if i % 2 else int(rng.integers(0, E + 1 - L)))
+        rows.append([int(rng.integers(0, 50)), int(rng.integers(0, 4)), int(rng.integers(0, 50)), L, H])
+    rows.append([1, 1, 1, 1, E + 1])  # target not a candidate
+    got = TrainerPredictor.rank_metrics(rows, expectation)
+    want = _loop_metrics(rows, expectation)
+    assert got["Data"] == want["Data"]
+    for k in ("Hit1", "Hit3", "Hit10", "MR", "MRR"):
+        assert abs(got[k] - want[k]) <= 1e-12 * max(1.0, abs(want[k])), (k, got[k], want[k])
+    assert TrainerPredictor.rank_metrics([], expectation)["Data"] == 0
