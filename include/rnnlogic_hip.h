@@ -34,6 +34,8 @@ extern "C" {
 #define RNNL_ERR_OVERFLOW 3  /* workspace capacity exceeded: retry with a larger workspace */
 #define RNNL_ERR_NOMEM 4
 #define RNNL_ERR_INTERNAL 5  /* kernel self-check failed (message names the query) */
+#define RNNL_ERR_RANGE 6     /* integer range: a path count / PNA degree reached 2^32, or the rule
+                                aggregates are non-finite or too large for the fixed-point tables */
 
 #define RNNL_AGG_SUM 0       /* FuncToNodeSum   (reference src/layers.py:53-77)  */
 #define RNNL_AGG_PNA 1       /* FuncToNode, pna (reference src/layers.py:79-126) */
@@ -199,6 +201,14 @@ int rnnl_debug_profile(void *dev_counters);
  * 100 MHz real-time ticks) of every block into dev_counters (2 x uint64); the
  * ratio x 0.1 GHz is the effective shader clock under that kernel's load. */
 int rnnl_debug_clock(void *dev_counters);
+
+/* Test hook: lower the per-slot frontier / contribution capacities and the
+ * per-query bucket-pool entries of the grounding workspace (at
+ * capacity_scale 1; all three <= 0 restores the defaults), so that a test can
+ * force RNNL_ERR_OVERFLOW and the host's doubled-capacity_scale retry.
+ * Affects the sizes computed by later rnnl_forward_workspace_size / launches
+ * in this process. */
+int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t pool_per_query);
 
 /* ------------------------------------------------------- EM Predictor --
  * The EM loop's rule-weight predictor (reference src/predictors.py:17-119,

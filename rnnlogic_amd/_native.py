@@ -13,7 +13,8 @@ LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
 # diagnostic A/B builds (tools/*_variants.sh) may be selected with RNNL_LIB
 LIB_PATH = os.environ.get("RNNL_LIB") or LIB_PATH
 
-RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL = 0, 1, 2, 3, 4, 5
+RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL, RNNL_ERR_RANGE = \
+    0, 1, 2, 3, 4, 5, 6
 AGG_SUM, AGG_PNA = 0, 1
 FEATURE_ADD, FEATURE_NONE = 0, 1
 ROTATE_DIRECT, ROTATE_MFMA = 0, 1
@@ -57,6 +58,7 @@ SIGNATURES = [
     ("rnnl_predictor_rule_stats", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_debug_clock", ctypes.c_int, [_P]),
+    ("rnnl_debug_capacity", ctypes.c_int, [_I64, _I64, _I64]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
     ("rnnl_rotate_table_sizes", ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P]),

@@ -67,6 +67,10 @@ constexpr int EMPTY = -1;
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
 enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5 };
+// H_ERRBITS: 4 watchdog, 8 a path count or PNA degree reached 2^32 (the u32
+// sums would wrap), 16 the node-weight table is out of its fixed-point range
+// (a non-finite aggregate, or |sum| >= 2^30).  8 and 16 -> RNNL_ERR_RANGE.
+enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16 };
 constexpr int HDR_WORDS_BYTES = 256;
 
 // Packed MLP weights (written by pack_weights_kernel behind the header).
@@ -166,12 +170,16 @@ struct Layout {
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 
+// Base capacities (entries at capacity_scale 1); rnnl_debug_capacity lowers
+// them so tests can force the overflow -> retry path.
+static int64_t g_fcap_base = FCAP_BASE, g_pcap_base = PCAP_BASE, g_pool_per_query = POOL_PER_QUERY;
+
 static Layout make_layout(int64_t nq, int64_t scale) {
   Layout L;
   L.nslots = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)NUM_CU * WG_PER_CU));
-  L.fcap = FCAP_BASE * scale;
-  L.pcap = PCAP_BASE * scale;
-  L.pool_cap = std::max<int64_t>(POOL_PER_QUERY * scale * std::max<int64_t>(nq, 1), L.pcap);
+  L.fcap = g_fcap_base * scale;
+  L.pcap = g_pcap_base * scale;
+  L.pool_cap = std::max<int64_t>(g_pool_per_query * scale * std::max<int64_t>(nq, 1), L.pcap);
   int64_t o = HDR_BYTES;
   L.off_qbase = o = align256(o);
   o += 8 * std::max<int64_t>(nq, 1);
@@ -298,7 +306,8 @@ __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
   for (int probe = 0; probe < 64; ++probe) {
     const int k = atomicCAS(&S.u.a.key[h], EMPTY, key);
     if (k == EMPTY || k == key) {
-      atomicAdd(&S.u.a.val[h], c);
+      const uint32_t old = atomicAdd(&S.u.a.val[h], c);
+      if (old + c < old) atomicOr(&S.err, ERR_COUNT_WIDTH);  // carry out of the u32 path count
       return true;
     }
     h = (h + 1) & (HCAP - 1);
@@ -311,7 +320,7 @@ __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
 // then flags S.err.  Guarantees every wave reaches the kernel exit.
 constexpr unsigned long long kWatchdogTicks = 200000000ull;  // 2 s
 __device__ __forceinline__ bool watchdog(Smem &S) {
-  if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - S.t0 > kWatchdogTicks) S.err |= 4;
+  if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - S.t0 > kWatchdogTicks) atomicOr(&S.err, ERR_WATCHDOG);
   __syncthreads();
   return S.err != 0;
 }
@@ -439,6 +448,13 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
 }
 
 // ---------------------------------------------------------------- phase B
+// PNA degree += count x rules at the node (u32 in LDS), carry-checked.
+__device__ __forceinline__ void degree_add(Smem &S, uint32_t *cell, uint32_t c, int nrules) {
+  const uint64_t v = (uint64_t)c * (uint32_t)nrules;
+  const uint32_t old = atomicAdd(cell, (uint32_t)v);
+  if ((v >> 32) || old + (uint32_t)v < old) atomicOr(&S.err, ERR_COUNT_WIDTH);
+}
+
 // Exclusive scan of WIN ints in place (PER consecutive per thread); returns the total.
 __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
   constexpr int PER = WIN / GBS;
@@ -491,8 +507,8 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
     for (int i = beg + tid; i < end; i += GBS)
-      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[w[i].a - lo]]),
-                w[i].c * (uint32_t)p.rl.node_nrules[w[i].b]);
+      degree_add(S, reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[w[i].a - lo]]), w[i].c,
+                 p.rl.node_nrules[w[i].b]);
     __syncthreads();
     for (int s2 = tid; s2 < nc; s2 += GBS) {
       const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
@@ -579,8 +595,8 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
     for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
     __syncthreads();
     for (int i = beg + tid; i < end; i += GBS)
-      atomicAdd(reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, w[i].a, false)]),
-                w[i].c * (uint32_t)p.rl.node_nrules[w[i].b]);
+      degree_add(S, reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, w[i].a, false)]), w[i].c,
+                 p.rl.node_nrules[w[i].b]);
     __syncthreads();
     for (int i = tid; i < HB; i += GBS) {
       if (S.u.c.key[i] != EMPTY) {
@@ -760,7 +776,10 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
       }
     }
     const int ncand = candidates_phase(p, S, sl, P, false, sorted);
-    if (tid == 0) {
+    __syncthreads();  // S.err: a PNA degree may have hit 2^32 in phase B
+    if (tid == 0 && S.err) {
+      flag_error(p, hdr, S, q);
+    } else if (tid == 0) {
       p.n_cand[q] = ncand;
       p.q_base[q] = S.qbase;
       if (p.prof) {
@@ -785,6 +804,16 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
 }
 
 // ---------------------------------------------------------------- K2: scoring
+// Scoring kernels: a node table flagged by fix_shift / node_weights_kernel
+// fails the launch (ERR_NODE_RANGE) instead of scoring with it.
+__device__ __forceinline__ void check_node_table(const KParams &p, const unsigned int *trailer) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && trailer[2]) {
+    unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+    atomicOr(&hdr[H_ERRBITS], (unsigned)ERR_NODE_RANGE);
+    atomicOr(&hdr[H_STATUS], 2u);
+  }
+}
+
 template <int AGG>
 __device__ __forceinline__ float score_one(const KParams &p, const float *__restrict__ wl, const float *relb,
                                            int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
@@ -909,6 +938,8 @@ __global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__res
   __shared__ unsigned long long s_dig;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  check_node_table(p, reinterpret_cast<const unsigned int *>(
+                          p.node_w + (int64_t)p.rl.n_nodes * (AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna)));
   for (int i = tid; i < L::N; i += BS) {
     float v = 0.f;
     if (i < L::ADDB) v = W[W_ADDW + i];
@@ -1117,6 +1148,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
     s_w[i] = v;
   }
   if (tid == 0) s_r = -1;
+  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum));
   const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
   const float inv_scale = ldexpf(1.f, -shift);
 #pragma unroll 1
@@ -1286,8 +1318,11 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
       m = max(m, __float_as_uint(fabsf(s1)));
     } else {
       long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStridePna);
-      rec[d] = llrint((double)s1 * sc);
-      rec[16 + d] = llrint((double)s2 * sc);
+      // |x| * 2^28 must stay well inside int64 (and be finite): else flag the table
+      const bool ok = fabs((double)s1) < 0x1p30 && fabs((double)s2) < 0x1p30 && !isnan(mn) && !isnan(mx);
+      if (!ok) atomicOr(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStridePna) + 2, 1u);
+      rec[d] = ok ? llrint((double)s1 * sc) : 0;
+      rec[16 + d] = ok ? llrint((double)s2 * sc) : 0;
       float *fr = reinterpret_cast<float *>(rec + 32);
       fr[d] = mn;
       fr[16 + d] = mx;
@@ -1342,18 +1377,33 @@ __global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent
 // |fix| < 2^30 for the largest |sum|, so a candidate's int64 sum of
 // count x fix is exact (deterministic in any entry order) with ~2^-30
 // relative resolution.  Trailer: u32 max|x| bits, i32 shift.
+// Table-wide shift from the max |sum| bits in trailer[0]; trailer[2] = 1 when
+// the table cannot be represented (a non-finite sum — its |x| bits are >=
+// those of +inf — or |sum| >= 2^30, which would need a negative shift): the
+// records are zeroed and the scoring kernels report ERR_NODE_RANGE.
+__device__ __forceinline__ int fix_shift(unsigned int *trailer, bool &bad) {
+  const unsigned int bits = trailer[0];
+  int e = 0;
+  bad = bits >= 0x7f800000u;
+  if (!bad && bits) frexpf(__uint_as_float(bits), &e);  // max < 2^e
+  bad = bad || e > 30;
+  const int shift = bad ? 0 : min(30 - e, 60);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    trailer[1] = (unsigned)shift;
+    trailer[2] = bad ? 1u : 0u;
+  }
+  return shift;
+}
+
 __global__ void node_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
   unsigned int *trailer = reinterpret_cast<unsigned int *>(out + (int64_t)n_nodes * kStrideSum);
-  const float mx = __uint_as_float(trailer[0]);
-  int e = 0;
-  if (mx > 0.f) frexpf(mx, &e);  // mx < 2^e
-  const int shift = min(max(30 - e, 0), 60);
-  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = (unsigned)shift;
-  const float sc = ldexpf(1.f, min(shift, 120));
+  bool bad;
+  const int shift = fix_shift(trailer, bad);
+  const float sc = ldexpf(1.f, shift);
   const int64_t n = (int64_t)n_nodes * 16;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float *f = reinterpret_cast<float *>(out) + i;
-    reinterpret_cast<int *>(out)[i] = (int)rintf(*f * sc);
+    reinterpret_cast<int *>(out)[i] = bad ? 0 : (int)rintf(*f * sc);
   }
 }
 
@@ -1384,17 +1434,15 @@ __global__ void lin_node_kernel(RulesDev rl, const float *__restrict__ w, unsign
 
 __global__ void lin_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
   unsigned int *trailer = reinterpret_cast<unsigned int *>(out + lin_trailer_off(n_nodes));
-  const float mx = __uint_as_float(trailer[0]);
-  int e = 0;
-  if (mx > 0.f) frexpf(mx, &e);  // mx < 2^e
-  const int shift = min(max(30 - e, 0), 60);
-  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = (unsigned)shift;
-  const float sc = ldexpf(1.f, min(shift, 120));
+  bool bad;
+  const int shift = fix_shift(trailer, bad);
+  const float sc = ldexpf(1.f, shift);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_nodes; i += gridDim.x * blockDim.x) {
     const float f = reinterpret_cast<float *>(out)[i];
-    reinterpret_cast<int *>(out)[i] = (int)rintf(f * sc);
+    reinterpret_cast<int *>(out)[i] = bad ? 0 : (int)rintf(f * sc);
   }
 }
+
 
 // One workgroup per query (grid-stride), one lane per candidate: the
 // candidate's exact sum, added into the pre-filled bias row (entity_feature
@@ -1403,6 +1451,8 @@ __global__ __launch_bounds__(BS) void score_linear_kernel(KParams p, const int *
   const int shift = (int)reinterpret_cast<const unsigned int *>(reinterpret_cast<const unsigned char *>(fix) +
                                                                 lin_trailer_off(p.rl.n_nodes))[1];
   const double inv = ldexp(1.0, -shift);
+  check_node_table(p, reinterpret_cast<const unsigned int *>(reinterpret_cast<const unsigned char *>(fix) +
+                                                             lin_trailer_off(p.rl.n_nodes)));
   for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
     const int nc = p.n_cand[q];
     if (nc <= 0) continue;
@@ -1473,8 +1523,8 @@ int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, v
   }
   const int64_t n = (int64_t)r->d.n_nodes * 16;
   unsigned char *out = static_cast<unsigned char *>(node_w);
-  if (agg == RNNL_AGG_SUM)
-    RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * kStrideSum, 0, 8, (hipStream_t)stream));
+  RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna), 0, 16,
+                                (hipStream_t)stream));
   if (n == 0) return RNNL_OK;
   const int bs = 256;
   hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 2048)), dim3(bs), 0,
@@ -1775,7 +1825,7 @@ int rnnl_linear_node_weights(rnnl_rules r, const float *rule_weights, int32_t n_
   }
   unsigned char *out = static_cast<unsigned char *>(node_w);
   hipStream_t st = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipMemsetAsync(out + lin_trailer_off(r->d.n_nodes), 0, 8, st));
+  RNNL_HIP_CHECK(hipMemsetAsync(out + lin_trailer_off(r->d.n_nodes), 0, 16, st));
   const int n = r->d.n_nodes;
   if (n == 0) return RNNL_OK;
   hipLaunchKernelGGL(lin_node_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, r->d, rule_weights, out);
@@ -1836,12 +1886,39 @@ int rnnl_debug_profile(void *dev_counters) {
   return RNNL_OK;
 }
 
+int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t pool_per_query) {
+  if (frontier_base <= 0 && contrib_base <= 0 && pool_per_query <= 0) {  // restore the defaults
+    g_fcap_base = FCAP_BASE;
+    g_pcap_base = PCAP_BASE;
+    g_pool_per_query = POOL_PER_QUERY;
+    return RNNL_OK;
+  }
+  if (frontier_base < 256 || contrib_base < 256 || frontier_base < contrib_base || pool_per_query < 1 ||
+      frontier_base > FCAP_BASE || contrib_base > PCAP_BASE || pool_per_query > POOL_PER_QUERY) {
+    set_error("rnnl_debug_capacity: need 256 <= contrib <= frontier <= defaults, 1 <= pool <= default");
+    return RNNL_ERR_INVALID;
+  }
+  g_fcap_base = frontier_base;
+  g_pcap_base = contrib_base;
+  g_pool_per_query = pool_per_query;
+  return RNNL_OK;
+}
+
 int rnnl_forward_status(void *ws, void *stream) {
   unsigned int st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
   RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
   if (st[H_STATUS] & 2u) {
-    set_error("rnnl_predictorplus_forward: internal error bits 0x" + std::to_string(st[H_ERRBITS]) +
+    const unsigned bits = st[H_ERRBITS];
+    if (bits & (ERR_COUNT_WIDTH | ERR_NODE_RANGE) && !(bits & ERR_WATCHDOG)) {
+      std::string msg = "rnnl_predictorplus_forward:";
+      if (bits & ERR_COUNT_WIDTH)
+        msg += " a path count or PNA degree reached 2^32 (query " + std::to_string(st[H_ERRQ]) + ");";
+      if (bits & ERR_NODE_RANGE) msg += " rule-embedding / rule-weight aggregates are non-finite or >= 2^30;";
+      set_error(msg);
+      return RNNL_ERR_RANGE;
+    }
+    set_error("rnnl_predictorplus_forward: internal error bits 0x" + std::to_string(bits) +
               " (4: watchdog) at query " + std::to_string(st[H_ERRQ]));
     return RNNL_ERR_INTERNAL;
   }

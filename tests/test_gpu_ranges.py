@@ -1,0 +1,162 @@
+"""Integer / fixed-point range guards and the workspace-overflow retry of the
+HIP forward.
+
+* Path counts are u32 in the grounding kernel's LDS hash (the reference counts
+  in int64, src/data.py:139-171).  A graph with parallel edges whose path
+  count reaches 2^32 must fail loudly (RNNL_ERR_RANGE), and one just below
+  (255^4 paths, above 2^31) must match the oracle.
+* Rule-embedding / rule-weight aggregates that are non-finite or too large
+  for the fixed-point node tables fail loudly instead of converting.
+* A forward whose workspace is too small (capacities lowered with
+  rnnl_debug_capacity) reports RNNL_ERR_OVERFLOW, the host retries with a
+  doubled capacity_scale, and the result is bit-identical to a forward with
+  the default capacities.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_np as ref
+from rnnlogic_amd import _native, datasets
+from rnnlogic_amd.data import KnowledgeGraph
+from rnnlogic_amd.predictors import Predictor, PredictorPlus
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def chain_graph(tmp_path, mult):
+    """e0 =r1=> e1 =r1=> e2 =r1=> e3 =r1=> e4 with `mult` parallel edges per
+    hop (duplicate train lines are separate edges, as in the reference),
+    e4 -r1-> e5, plus the query relation r0 (e0 -r0-> e5); rules r0 <- r1^4
+    and r0 <- r1^5, so the depth-4 trie node is inner and its path count
+    (mult^4 at e4) is summed in the grounding hash."""
+    d = tmp_path / ("chain%d" % mult)
+    d.mkdir()
+    ents = ["e%d" % i for i in range(6)]
+    (d / "entities.dict").write_text("".join("%d\t%s\n" % (i, e) for i, e in enumerate(ents)))
+    (d / "relations.dict").write_text("0\tr0\n1\tr1\n")
+    lines = []
+    for k in range(4):
+        lines += ["e%d\tr1\te%d\n" % (k, k + 1)] * mult
+    lines.append("e4\tr1\te5\n")
+    lines.append("e0\tr0\te5\n")
+    (d / "train.txt").write_text("".join(lines))
+    (d / "valid.txt").write_text("e1\tr0\te5\n")
+    (d / "test.txt").write_text("e0\tr0\te5\n")
+    rules = d / "rules.txt"
+    rules.write_text("0 1 1 1 1\n0 1 1 1 1 1\n")
+    return str(d), str(rules)
+
+
+def _emb_model(graph, rule_path, dev, aggregator="sum"):
+    torch.manual_seed(0)
+    model = PredictorPlus(graph, type="emb", entity_feature="bias", aggregator=aggregator)
+    model.set_rules(rule_path)
+    return model.to(dev).eval()
+
+
+def test_path_count_at_2_32_fails_loudly(tmp_path, dev):
+    path, rules = chain_graph(tmp_path, 256)  # 256^4 = 2^32 paths e0 -> e4
+    model = _emb_model(KnowledgeGraph(path), rules, dev)
+    h = torch.tensor([0], device=dev)
+    r = torch.tensor([0], device=dev)
+    with pytest.raises(_native.NativeError) as ei:
+        with torch.no_grad():
+            model(h, r, None)
+    assert ei.value.code == _native.RNNL_ERR_RANGE, str(ei.value)
+
+
+@pytest.mark.parametrize("aggregator", ["sum", "pna"])
+def test_path_count_above_2_31_matches_oracle(tmp_path, dev, aggregator):
+    path, rules = chain_graph(tmp_path, 255)  # 255^4 = 4.23e9 paths: above 2^31, below 2^32
+    graph = KnowledgeGraph(path)
+    model = _emb_model(graph, rules, dev, aggregator)
+    with torch.no_grad():
+        model.bias.normal_()
+        score, mask = model(torch.tensor([0], device=dev), torch.tensor([0], device=dev), None)
+    g = ref.Graph(path)
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    want, wmask = ref.predictorplus_forward(sd, dict(type="emb", aggregator=aggregator, entity_feature="bias"), g,
+                                           ref.Rules(rules, g.relation_size), np.asarray([0]), np.asarray([0]), None)
+    assert np.array_equal(mask.cpu().numpy(), wmask)
+    np.testing.assert_allclose(score.cpu().numpy(), want, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf"), 2.0 ** 31])
+@pytest.mark.parametrize("aggregator", ["sum", "pna"])
+def test_node_table_out_of_range_fails_loudly(bad, aggregator, dev):
+    path = datasets.materialize("umls")
+    graph = KnowledgeGraph(path)
+    model = _emb_model(graph, datasets.rule_file("umls"), dev, aggregator)
+    with torch.no_grad():
+        model.rule_emb[3, 5] = bad
+    r0 = int(model.rules[3][0])
+    facts = [f for f in graph.test_facts if f[1] == r0][:8]
+    h = torch.tensor([f[0] for f in facts], device=dev)
+    r = torch.tensor([f[1] for f in facts], device=dev)
+    with pytest.raises(_native.NativeError) as ei:
+        with torch.no_grad():
+            model(h, r, None)
+    assert ei.value.code == _native.RNNL_ERR_RANGE, str(ei.value)
+
+
+def test_em_predictor_weights_out_of_range_fail_loudly(dev):
+    path = datasets.materialize("umls")
+    graph = KnowledgeGraph(path)
+    pred = Predictor(graph, entity_feature="bias")
+    pred.set_rules(datasets.rule_file("umls"))
+    with torch.no_grad():
+        pred.rule_weights.normal_()
+        pred.rule_weights[7] = float("nan")
+    pred = pred.to(dev).eval()
+    facts = graph.test_facts[:16]
+    with pytest.raises(_native.NativeError) as ei:
+        with torch.no_grad():
+            pred.forward_rows(torch.tensor([f[0] for f in facts], device=dev),
+                              torch.tensor([f[1] for f in facts], device=dev), None)
+    assert ei.value.code == _native.RNNL_ERR_RANGE, str(ei.value)
+
+
+@pytest.mark.parametrize("case", [("umls", "lstm", "sum"), ("kinship", "emb", "pna")])
+def test_workspace_overflow_retry_is_bit_identical(case, dev):
+    data, typ, agg = case
+    path = datasets.materialize(data)
+    graph = KnowledgeGraph(path)
+    torch.manual_seed(0)
+    model = PredictorPlus(graph, type=typ, entity_feature="bias", aggregator=agg)
+    model.set_rules(datasets.rule_file(data))
+    with torch.no_grad():
+        model.bias.normal_()
+    model = model.to(dev).eval()
+    rows = np.asarray(graph.test_facts[:512], dtype=np.int64)
+    h = torch.from_numpy(rows[:, 0]).to(dev)
+    r = torch.from_numpy(rows[:, 1]).to(dev)
+    with torch.no_grad():
+        want, wmask, wnc = model.forward_rows(h, r, None, return_ncand=True)
+    torch.cuda.synchronize()
+    _native.call("rnnl_debug_capacity", 256, 256, 4)
+    try:
+        model.capacity_scale = 1
+        model._ws = {}
+        with torch.no_grad():
+            got, gmask, gnc = model.forward_rows(h, r, None, return_ncand=True)
+        torch.cuda.synchronize()
+        retried = model.capacity_scale
+    finally:
+        _native.call("rnnl_debug_capacity", 0, 0, 0)
+        model.capacity_scale = 1
+        model._ws = {}
+    assert retried > 1, "the lowered capacities did not overflow"
+    assert torch.equal(gnc, wnc)
+    assert torch.equal(gmask, wmask)
+    assert torch.equal(got, want), float((got - want).abs().max())
+    print("%s: retried up to capacity_scale %d, bit-identical" % (data, retried))
