@@ -69,8 +69,9 @@ constexpr int EMPTY = -1;
 enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5 };
 // H_ERRBITS: 4 watchdog, 8 a path count or PNA degree reached 2^32 (the u32
 // sums would wrap), 16 the node-weight table is out of its fixed-point range
-// (a non-finite aggregate, or |sum| >= 2^30).  8 and 16 -> RNNL_ERR_RANGE.
-enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16 };
+// (a non-finite aggregate, or |sum| >= 2^30), 32 a candidate's counts sum past
+// the exact int64 feature sums.  8, 16 and 32 -> RNNL_ERR_RANGE.
+enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16, ERR_ACC_RANGE = 32 };
 constexpr int HDR_WORDS_BYTES = 256;
 
 // Packed MLP weights (written by pack_weights_kernel behind the header).
@@ -814,6 +815,16 @@ __device__ __forceinline__ void check_node_table(const KParams &p, const unsigne
   }
 }
 
+// A candidate whose path counts sum to more than the exact int64 feature
+// sums can hold (sum of counts x max |record| >= 2^63) fails the launch
+// (ERR_ACC_RANGE) instead of wrapping: the reference sums int64 counts in
+// fp32 (predictors.py:224) and never wraps.
+__device__ __forceinline__ void flag_acc_range(const KParams &p) {
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  atomicOr(&hdr[H_ERRBITS], (unsigned)ERR_ACC_RANGE);
+  atomicOr(&hdr[H_STATUS], 2u);
+}
+
 template <int AGG>
 __device__ __forceinline__ float score_one(const KParams &p, const float *__restrict__ wl, const float *relb,
                                            int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
@@ -833,11 +844,12 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
     }
   }
   long long deg = 0;
-  uint64_t fp = 0;
+  uint64_t fp = 0, csum = 0;
   for (int e = beg; e < beg + cnt; ++e) {
     const int2 be = p.bent[e];
     const int n = be.x;
     const long long c = (uint32_t)be.y;
+    csum += (uint64_t)c;
     const long long *rec = reinterpret_cast<const long long *>(p.node_w + (int64_t)n * STRIDE);
 #pragma unroll
     for (int d = 0; d < 16; ++d) a1[d] += c * rec[d];
@@ -855,6 +867,14 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
     }
   }
   if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+  {
+    // records: |fix| <= 2^30 (SUM: int32), PNA: max(|sum x|, |sum x^2|) * 2^28 from the table trailer
+    double rmax = 0x1p30;
+    if constexpr (AGG == RNNL_AGG_PNA)
+      rmax = (double)__uint_as_float(reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes *
+                                                                            kStridePna)[0]) * 0x1p28 + 1.0;
+    if ((double)csum * rmax >= 0x1p63) flag_acc_range(p);
+  }
 #ifdef RNNL_SCORE_NOMLP  // diagnostic build: the node-sum gather alone
   return (float)a1[0] + (float)a1[15];
 #endif
@@ -1032,11 +1052,13 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
   for (int d = 0; d < 16; ++d) acc[d] = 0;
   deg = 0;
   fp = 0;
+  uint64_t csum = 0;
   for (int e = beg; e < beg + cnt; ++e) {
     const int2 be = p.bent[e];
     const int n = be.x;
     const uint32_t cu = (uint32_t)be.y;
     const long long c = cu;
+    csum += cu;
     const int *x;
     int nr;
     uint64_t nf;
@@ -1070,6 +1092,7 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
     deg += c * nr;
     fp += (uint64_t)c * nf;
   }
+  if (csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33 total count
 #pragma unroll
   for (int d = 0; d < 16; ++d) f[d] = (float)((double)acc[d] * (double)inv_scale);
 }
@@ -1321,6 +1344,8 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
       // |x| * 2^28 must stay well inside int64 (and be finite): else flag the table
       const bool ok = fabs((double)s1) < 0x1p30 && fabs((double)s2) < 0x1p30 && !isnan(mn) && !isnan(mx);
       if (!ok) atomicOr(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStridePna) + 2, 1u);
+      // trailer[0]: max |record| (f32 bits) for the scoring kernels' int64 range bound
+      m = max(m, __float_as_uint(ok ? fmaxf(fabsf(s1), fabsf(s2)) : 0.f));
       rec[d] = ok ? llrint((double)s1 * sc) : 0;
       rec[16 + d] = ok ? llrint((double)s2 * sc) : 0;
       float *fr = reinterpret_cast<float *>(rec + 32);
@@ -1328,7 +1353,6 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
       fr[16 + d] = mx;
     }
   }
-  if (agg != RNNL_AGG_SUM) return;  // uniform across the grid
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
   __shared__ unsigned int s_m[4];
@@ -1336,7 +1360,9 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
   __syncthreads();
   if (threadIdx.x == 0) {
     m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
-    if (m) atomicMax(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStrideSum), m);
+    if (m)
+      atomicMax(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes *
+                                                 (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna)), m);
   }
 }
 
@@ -1461,10 +1487,13 @@ __global__ __launch_bounds__(BS) void score_linear_kernel(KParams p, const int *
       const int4 cr = p.cand[qb + s];
       const int t = cr.x;
       long long acc = 0;
+      uint64_t csum = 0;
       for (int e = cr.y; e < cr.y + cr.z; ++e) {
         const int2 be = p.bent[e];
+        csum += (uint32_t)be.y;
         acc += (long long)(uint32_t)be.y * fix[be.x];
       }
+      if (csum >> 33) flag_acc_range(p);  // |int32 fix| < 2^30
       const float out = (float)((double)acc * inv);
       const int64_t idx = (int64_t)q * p.g.E + t;
       if (p.feature == RNNL_FEATURE_NONE)
@@ -1910,11 +1939,12 @@ int rnnl_forward_status(void *ws, void *stream) {
   RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
   if (st[H_STATUS] & 2u) {
     const unsigned bits = st[H_ERRBITS];
-    if (bits & (ERR_COUNT_WIDTH | ERR_NODE_RANGE) && !(bits & ERR_WATCHDOG)) {
+    if (bits & (ERR_COUNT_WIDTH | ERR_NODE_RANGE | ERR_ACC_RANGE) && !(bits & ERR_WATCHDOG)) {
       std::string msg = "rnnl_predictorplus_forward:";
       if (bits & ERR_COUNT_WIDTH)
         msg += " a path count or PNA degree reached 2^32 (query " + std::to_string(st[H_ERRQ]) + ");";
       if (bits & ERR_NODE_RANGE) msg += " rule-embedding / rule-weight aggregates are non-finite or >= 2^30;";
+      if (bits & ERR_ACC_RANGE) msg += " a candidate's path counts sum beyond the exact int64 feature sum;";
       set_error(msg);
       return RNNL_ERR_RANGE;
     }

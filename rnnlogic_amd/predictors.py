@@ -177,7 +177,8 @@ class _HipGrounding(object):
         _native.call("rnnl_ground_export_entries", ws.data_ptr(), nq, scale, n_cand.data_ptr(), ent_off.data_ptr(),
                      node.data_ptr(), count.data_ptr(), stream)
         cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent)
-        return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64)
+        # path counts are u32 in the kernel (< 2^32, carry-checked): reinterpret the int32 bits
+        return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64) & 0xFFFFFFFF
 
     def _needs_grad(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())

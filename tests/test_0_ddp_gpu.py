@@ -64,6 +64,8 @@ def _worker(rank, world, port, out_dir):
     # on the batches train() will draw (make_batches under the same random state)
     import random
     state = random.getstate()
+    # make_batches shuffles r2instances in place: restore them with the RNG state
+    r2i = [list(x) for x in train_set.r2instances]
     train_set.make_batches()
     sampler = torch.utils.data.DistributedSampler(train_set, world, rank)
     sampler.set_epoch(0)
@@ -74,6 +76,7 @@ def _worker(rank, world, port, out_dir):
     for i in idx:
         solver.train_step(model, [x.unsqueeze(0) for x in train_set[i]], 0.2)
     random.setstate(state)
+    train_set.r2instances = r2i
     # the same two steps through train(): DDP all-reduces over the gloo group
     rec = _Recorder(model)
     solver.optimizer = rec
@@ -93,6 +96,9 @@ def test_ddp_world2_gradients_are_the_rank_mean(tmp_path):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
     res = [torch.load(os.path.join(str(tmp_path), "rank%d.pt" % r), weights_only=True) for r in range(world)]
     assert res[0]["idx"] != res[1]["idx"]
+    for s in range(2):  # the all-reduced gradients are identical on both ranks
+        for n in res[0]["ddp"][s]:
+            assert torch.equal(res[0]["ddp"][s][n], res[1]["ddp"][s][n]), (s, n)
     for s in range(2):
         g0, g1 = res[0]["ddp"][s], res[1]["ddp"][s]
         assert sorted(g0) == sorted(g1)

@@ -70,15 +70,21 @@ def test_reference_scores_through_device_ranks(dev):
         if c["split"] == "test":
             table[(int(c["r"][0]),) + tuple(int(x) for x in c["h"])] = (c["score"], c["mask"])
     ranks = []
-    for i in range(len(test_set)):
+    # the reference evaluate()'s DistributedSampler order: a (h, r, t) that
+    # occurs in two batches keeps its later row, and the reference's scores
+    # of one (h, r) may differ in the last bits between batches
+    for i in torch.utils.data.DistributedSampler(test_set, 1, 0):
         h, r, t, flag = test_set[i]
         s, m = table[(int(r[0]),) + tuple(int(x) for x in h)]
         L, H = TrainerPredictor.filtered_ranks(torch.from_numpy(s).to(dev), torch.from_numpy(m).to(dev),
                                                flag.to(dev), t.to(dev), graph.entity_size)
         ranks.append(torch.stack([h.to(dev), r.to(dev), t.to(dev), L, H], 1))
     m = TrainerPredictor.rank_metrics(torch.cat(ranks).cpu().numpy().tolist(), True)
+    # eval/mrr is evaluate()'s return value (float64); the other metrics are
+    # the reference's log lines, printed to 6 decimals
+    assert abs(m["MRR"] - float(fx.z["eval/mrr"])) <= 1e-12
     for key in ("MRR", "Hit1", "Hit3", "Hit10", "MR"):
-        assert abs(m[key] - float(fx.z["eval/" + key])) <= 1e-12 * max(1.0, abs(m[key])), key
+        assert abs(m[key] - float(fx.z["eval/" + key])) <= 5e-7, key
 
 
 @pytest.mark.parametrize("case", EVAL_CASES)

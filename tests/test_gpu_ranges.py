@@ -2,7 +2,7 @@
 HIP forward.
 
 * Path counts are u32 in the grounding kernel's LDS hash (the reference counts
-  in int64, src/data.py:139-171).  A graph with parallel edges whose path
+  in int64, src/data.py:139-171).  A layered graph whose path
   count reaches 2^32 must fail loudly (RNNL_ERR_RANGE), and one just below
   (255^4 paths, above 2^31) must match the oracle.
 * Rule-embedding / rule-weight aggregates that are non-finite or too large
@@ -33,27 +33,30 @@ def dev():
     return torch.device("cuda:0")
 
 
-def chain_graph(tmp_path, mult):
-    """e0 =r1=> e1 =r1=> e2 =r1=> e3 =r1=> e4 with `mult` parallel edges per
-    hop (duplicate train lines are separate edges, as in the reference),
-    e4 -r1-> e5, plus the query relation r0 (e0 -r0-> e5); rules r0 <- r1^4
-    and r0 <- r1^5, so the depth-4 trie node is inner and its path count
-    (mult^4 at e4) is summed in the grounding hash."""
-    d = tmp_path / ("chain%d" % mult)
+def chain_graph(tmp_path, m, w5=1):
+    """A layered graph e0 -r1-> L1 -r1-> L2 -r1-> L3 -r1-> L4 -r1-> L5 -r1-> e6
+    with m entities in L1..L4 and w5 in L5, consecutive layers wired complete
+    bipartite (the reference rejects parallel edges, data.py:68), plus the
+    query edge e0 -r0-> e6, and the rule r0 <- r1^6.  Each L5 entity is
+    reached by m^4 paths, summed in the grounding kernel's phase-A hash at the
+    inner depth-5 trie node (m path counts of m^3 each); e6 then gets w5
+    (depth-6, rule-end) entries of m^4 each."""
+    d = tmp_path / ("layers%d_%d" % (m, w5))
     d.mkdir()
-    ents = ["e%d" % i for i in range(6)]
+    layers = [["e0"]] + [["l%d_%d" % (k, i) for i in range(m)] for k in range(1, 5)]
+    layers += [["l5_%d" % i for i in range(w5)], ["e6"]]
+    ents = [e for layer in layers for e in layer]
     (d / "entities.dict").write_text("".join("%d\t%s\n" % (i, e) for i, e in enumerate(ents)))
     (d / "relations.dict").write_text("0\tr0\n1\tr1\n")
     lines = []
-    for k in range(4):
-        lines += ["e%d\tr1\te%d\n" % (k, k + 1)] * mult
-    lines.append("e4\tr1\te5\n")
-    lines.append("e0\tr0\te5\n")
+    for a, b in zip(layers[:-1], layers[1:]):
+        lines += ["%s\tr1\t%s\n" % (x, y) for x in a for y in b]
+    lines.append("e0\tr0\te6\n")
     (d / "train.txt").write_text("".join(lines))
-    (d / "valid.txt").write_text("e1\tr0\te5\n")
-    (d / "test.txt").write_text("e0\tr0\te5\n")
+    (d / "valid.txt").write_text("e0\tr0\te6\n")
+    (d / "test.txt").write_text("e0\tr0\te6\n")
     rules = d / "rules.txt"
-    rules.write_text("0 1 1 1 1\n0 1 1 1 1 1\n")
+    rules.write_text("0 1 1 1 1 1 1\n")
     return str(d), str(rules)
 
 
@@ -65,7 +68,7 @@ def _emb_model(graph, rule_path, dev, aggregator="sum"):
 
 
 def test_path_count_at_2_32_fails_loudly(tmp_path, dev):
-    path, rules = chain_graph(tmp_path, 256)  # 256^4 = 2^32 paths e0 -> e4
+    path, rules = chain_graph(tmp_path, 256)  # 256^4 = 2^32 paths e0 -> each L5 entity
     model = _emb_model(KnowledgeGraph(path), rules, dev)
     h = torch.tensor([0], device=dev)
     r = torch.tensor([0], device=dev)
@@ -89,6 +92,22 @@ def test_path_count_above_2_31_matches_oracle(tmp_path, dev, aggregator):
                                            ref.Rules(rules, g.relation_size), np.asarray([0]), np.asarray([0]), None)
     assert np.array_equal(mask.cpu().numpy(), wmask)
     np.testing.assert_allclose(score.cpu().numpy(), want, atol=1e-4, rtol=1e-5)
+    # the training path's COO carries the same u32 count (not a negative int32)
+    row, ent, ce, node, count = model.ground_coo(torch.tensor([0], device=dev), torch.tensor([0], device=dev))
+    assert ent.tolist() == [graph.entity_size - 1] and count.tolist() == [255 ** 4]
+
+
+@pytest.mark.parametrize("aggregator", ["sum", "pna"])
+def test_count_sum_past_int64_features_fails_loudly(tmp_path, dev, aggregator):
+    # three depth-6 entries of 255^4 at e6: the counts sum to 1.27e10 >= 2^33,
+    # past what the int64 fixed-point feature sums hold exactly (SUM); for PNA
+    # the u32 degree (sum of count x rules) wraps first
+    path, rules = chain_graph(tmp_path, 255, w5=3)
+    model = _emb_model(KnowledgeGraph(path), rules, dev, aggregator)
+    with pytest.raises(_native.NativeError) as ei:
+        with torch.no_grad():
+            model(torch.tensor([0], device=dev), torch.tensor([0], device=dev), None)
+    assert ei.value.code == _native.RNNL_ERR_RANGE, str(ei.value)
 
 
 @pytest.mark.parametrize("bad", [float("nan"), float("inf"), 2.0 ** 31])
@@ -143,7 +162,7 @@ def test_workspace_overflow_retry_is_bit_identical(case, dev):
     with torch.no_grad():
         want, wmask, wnc = model.forward_rows(h, r, None, return_ncand=True)
     torch.cuda.synchronize()
-    _native.call("rnnl_debug_capacity", 256, 256, 4)
+    _native.call("rnnl_debug_capacity", 1024, 1024, 64)
     try:
         model.capacity_scale = 1
         model._ws = {}
