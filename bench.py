@@ -461,7 +461,7 @@ def main():
         ghz = clock_ghz or 2.4
         cyc = base_ms * 1e-3 * ghz * 1e9 * 1024 / (nq * E * D / 64.0)
         floor = 19.1 if mode == "direct" else 13.1
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+        roof = {"bound": "valu", "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": traffic.get("rotate_%s_kernel" % mode),
                 "kernel": "rotate_%s_kernel" % mode,
                 "ms": round(base_ms / n_rot, 3), "alg_flops": rotate_flops / n_rot, "launches_per_step": n_rot,
