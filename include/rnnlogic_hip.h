@@ -136,6 +136,8 @@ typedef struct {
   const float *s1_w;       /* score_model.layers.1.weight (1 x 128) */
   const float *s1_b;       /* (1) */
   const float *rel_emb;    /* relation_emb.weight (R x 16) */
+  const float *base_row;   /* nullable: the base score every row starts from (the bias vector, E floats);
+                              candidates are then written as out + base_row[t] without reading score */
 } rnnl_predictor_params;
 
 /* Workspace bytes for one launch of rnnl_predictorplus_forward (host). */

@@ -79,7 +79,7 @@ class PredictorParams(ctypes.Structure):
     """rnnl_predictor_params (include/rnnlogic_hip.h)."""
     _fields_ = [("aggregator", _I32), ("feature", _I32), ("node_w", _P), ("add_w", _P), ("add_b", _P),
                 ("ln_w", _P), ("ln_b", _P), ("s0_w", _P), ("s0_b", _P), ("s1_w", _P), ("s1_b", _P),
-                ("rel_emb", _P)]
+                ("rel_emb", _P), ("base_row", _P)]
 
 
 class NativeError(RuntimeError):

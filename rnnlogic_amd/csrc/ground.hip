@@ -64,6 +64,10 @@ constexpr int HB_LOAD = HB * 3 / 4;  // max contributions per hash pass
 constexpr int WG_PER_CU = RNNL_WG_PER_CU;
 constexpr int NUM_CU = 256;
 constexpr int EMPTY = -1;
+// Phase-B hash passes rank their candidates by entity through an LDS bitmap
+// over the pass's entity range (it shares phase A's per-thread arrays, 36 B
+// per thread): ranges up to SORT_WORDS x 32 entities (49,152 at GBS = 256).
+constexpr int SORT_WORDS = (9 * GBS * 4 / 6) & ~(GBS - 1);
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
 enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5 };
@@ -105,6 +109,7 @@ struct KParams {
   int32_t agg, feature;
   const unsigned char *node_w;
   const float *add_w, *add_b, *ln_w, *ln_b, *s0_w, *s0_b, *s1_w, *s1_b, *rel_emb;
+  const float *base_row;  // nullable: every row's base score (bias), read instead of score[q][t]
   const int64_t *all_h, *all_r, *etr;
   int32_t nq;
   float *score;
@@ -135,6 +140,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 }
 
 __device__ __forceinline__ uint32_t hash32(uint32_t k) { return k * 2654435761u; }
+
 
 // Per-slot scratch: two frontier buffers and the contribution list, each an
 // array of 12-B entries (a, b, count) — one contiguous run per list, so a
@@ -268,10 +274,18 @@ struct __align__(16) Smem {
       int cid[HB];   // candidate index within the pass
     } c;
   } u;
-  int ent_v[GBS], ent_fch[GBS], item_off[GBS];
-  uint32_t ent_c[GBS];
-  int it_child[GBS], it_beg[GBS], it_flags[GBS], edge_off[GBS];
-  uint32_t it_c[GBS];
+  union {
+    struct {  // phase A: per-thread frontier items and edge batches
+      int ent_v[GBS], ent_fch[GBS], item_off[GBS];
+      uint32_t ent_c[GBS];
+      int it_child[GBS], it_beg[GBS], it_flags[GBS], edge_off[GBS];
+      uint32_t it_c[GBS];
+    };
+    struct {  // phase B: entity bitmap of one hash pass and its popcount prefix (candidate ranks)
+      uint32_t sbits[SORT_WORDS];
+      unsigned short spre[SORT_WORDS];
+    };
+  };
   int ws[GNW + 1];
   int q, nd, np, ovf, err;
   long long qbase;
@@ -545,9 +559,13 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
 // Sparse windows: contributions [beg, end) of consecutive entity windows
 // (end - beg <= HB_LOAD) bucketed through an LDS hash keyed by entity —
 // O(contributions) work and six barriers, against the dense window_pass's
-// O(WIN) passes.  Candidate order within the query is the hash order (nothing
-// downstream depends on it: scores scatter by entity, PNA's mean and the
-// digests are order-independent sums).  Same outputs as window_pass otherwise.
+// O(WIN) passes.  Candidates are emitted in ascending entity order (ranked
+// through an LDS bitmap of the pass's entity range, as window_pass's slots
+// are), so a query's candidate records — and the scoring pass's score
+// accesses, one lane per candidate — run along the score row; a range wider
+// than SORT_WORDS x 32 entities keeps the hash order (nothing downstream
+// depends on the order for correctness: scores scatter by entity, PNA's mean
+// and the digests are order-independent sums).
 __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
   uint32_t h = hash32((uint32_t)t) >> (32 - WBITS);
 #pragma unroll 1
@@ -560,37 +578,95 @@ __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
 }
 
 __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int end, int64_t cbase,
-                         bool degree_only) {
-  // w: contributions (a = entity, b = node, c = count), window-sorted or raw
+                         bool degree_only, int lo, int hi) {
+  // w: contributions (a = entity, b = node, c = count), window-sorted or raw;
+  // every entity lies in [lo, hi)
   const int tid = threadIdx.x;
+  const int w0 = lo >> 5, nw = ((hi - 1) >> 5) - w0 + 1;
+  // candidates in ascending entity order (the reference's nonzero order, and
+  // neighbouring lanes of the scoring pass then touch neighbouring score entries)
+  const bool by_rank = !degree_only && nw <= SORT_WORDS;
   for (int i = tid; i < HB; i += GBS) {
     S.u.c.key[i] = EMPTY;
     S.u.c.cnt[i] = 0;
+    S.u.c.off[i] = 0;
   }
+  if (by_rank)
+    for (int i = tid; i < nw; i += GBS) S.sbits[i] = 0u;
   __syncthreads();
   for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, w[i].a, true)], 1);
   __syncthreads();
-  // one scan of (bucket size << 12 | occupied): bucket offsets and candidate ids
   constexpr int PER = HB / GBS;
   int loc[PER];
-  int sum = 0;
+  int nc;
+  if (by_rank) {
+    for (int i = tid; i < HB; i += GBS) {
+      const int k = S.u.c.key[i];
+      if (k != EMPTY) atomicOr(&S.sbits[(k >> 5) - w0], 1u << (k & 31));
+    }
+    __syncthreads();
+    // rank of a bit = popcounts of the words before it + of its word below it
+    const int per = (nw + GBS - 1) / GBS;
+    int sum = 0;
+    for (int j = 0; j < per; ++j) {
+      const int i = tid * per + j;
+      if (i < nw) sum += __popc(S.sbits[i]);
+    }
+    int base = block_scan(sum, S.ws, nc);
+    for (int j = 0; j < per; ++j) {
+      const int i = tid * per + j;
+      if (i < nw) {
+        S.spre[i] = (unsigned short)base;
+        base += __popc(S.sbits[i]);
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < HB; i += GBS) {
+      const int k = S.u.c.key[i];
+      if (k != EMPTY) {
+        const int kk = k - (w0 << 5), wd = kk >> 5;
+        const int rank = S.spre[wd] + __popc(S.sbits[wd] & ((1u << (kk & 31)) - 1u));
+        S.u.c.cid[i] = rank;
+        S.u.c.off[rank] = S.u.c.cnt[i];  // bucket sizes in rank order
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the bucket sizes (rank order): off[rank] = bucket start
+    int s2 = 0;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int sidx = tid * PER + j;
-    loc[j] = (S.u.c.cnt[sidx] << 12) | (S.u.c.key[sidx] != EMPTY ? 1 : 0);
-    sum += loc[j];
-  }
-  int total;
-  int run = block_scan(sum, S.ws, total);
+    for (int j = 0; j < PER; ++j) {
+      loc[j] = S.u.c.off[tid * PER + j];
+      s2 += loc[j];
+    }
+    int tot;
+    int run = block_scan(s2, S.ws, tot);
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int sidx = tid * PER + j;
-    S.u.c.off[sidx] = run >> 12;
-    S.u.c.cid[sidx] = run & 4095;
-    run += loc[j];
+    for (int j = 0; j < PER; ++j) {
+      S.u.c.off[tid * PER + j] = run;
+      run += loc[j];
+    }
+    __syncthreads();
+  } else {
+    // one scan of (bucket size << 12 | occupied): bucket offsets and candidate ids (hash order)
+    int sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int sidx = tid * PER + j;
+      loc[j] = (S.u.c.cnt[sidx] << 12) | (S.u.c.key[sidx] != EMPTY ? 1 : 0);
+      sum += loc[j];
+    }
+    int total;
+    int run = block_scan(sum, S.ws, total);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int sidx = tid * PER + j;
+      S.u.c.off[sidx] = run >> 12;
+      S.u.c.cid[sidx] = run & 4095;
+      run += loc[j];
+    }
+    nc = total & 4095;
+    __syncthreads();
   }
-  const int nc = total & 4095;
-  __syncthreads();
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
     for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
@@ -608,11 +684,13 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
     __syncthreads();
     return nc;
   }
+  // bucket start of hash slot i: off is indexed by rank (by_rank) or by slot
   const int64_t qb = S.qbase;
   for (int i = tid; i < HB; i += GBS) {
     if (S.u.c.key[i] != EMPTY) {
-      const int64_t c = cbase + S.u.c.cid[i];
-      p.cand[c] = make_int4(S.u.c.key[i], (int32_t)(qb + beg + S.u.c.off[i]), S.u.c.cnt[i], 0);
+      const int cid = S.u.c.cid[i];
+      const int64_t c = cbase + cid;
+      p.cand[c] = make_int4(S.u.c.key[i], (int32_t)(qb + beg + S.u.c.off[by_rank ? cid : i]), S.u.c.cnt[i], 0);
     }
   }
   __syncthreads();
@@ -620,7 +698,7 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
   __syncthreads();
   for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
     const int sl2 = hb_slot(S, w[i].a, false);
-    const int64_t pos = qb + beg + S.u.c.off[sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
+    const int64_t pos = qb + beg + S.u.c.off[by_rank ? S.u.c.cid[sl2] : sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
     p.bent[pos] = make_int2(w[i].b, (int)w[i].c);
   }
   __syncthreads();
@@ -633,7 +711,7 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
   const int tid = threadIdx.x;
   // all contributions fit one hash pass: no window sort (it exists only to
   // bound the hash load) — one read of the raw list instead of a sorted copy
-  if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only) : 0;
+  if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only, 0, p.g.E) : 0;
   const int nwin = (p.g.E + WIN - 1) >> WBITS;
   if (!sorted) {
     for (int i = tid; i < nwin; i += GBS) S.whist[i] = 0;
@@ -671,7 +749,9 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
     }
     int w2 = w + 1;
     while (w2 < nwin && S.wbeg[w2 + 1] - beg <= HB_LOAD) ++w2;
-    if (S.wbeg[w2] > beg) ncand += hash_pass(p, S, sl.f(0), beg, S.wbeg[w2], S.qbase + ncand, degree_only);
+    if (S.wbeg[w2] > beg)
+      ncand += hash_pass(p, S, sl.f(0), beg, S.wbeg[w2], S.qbase + ncand, degree_only, w << WBITS,
+                         min(w2 << WBITS, p.g.E));
     w = w2;
   }
   return ncand;
@@ -1010,7 +1090,7 @@ __global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__res
       if (p.feature == RNNL_FEATURE_NONE)
         p.score[idx] = out;
       else
-        p.score[idx] = out + p.score[idx];
+        p.score[idx] = out + (p.base_row ? p.base_row[t] : p.score[idx]);
       if (p.mask) p.mask[idx] = 1;
     }
     __syncthreads();
@@ -1081,7 +1161,9 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
         nf = p.rl.node_fp[n];
       }
     }
-    if (cu < 0x80000000u) {  // one v_mad_i64_i32 per element
+    // (the compiler folds the two forms into the uint32 one: two v_mad_u64_u32
+    // per element; an explicit v_mad_i64_i32 measured slower, 16.2 -> 16.6 ms)
+    if (cu < 0x80000000u) {
       const int ci = (int)cu;
 #pragma unroll
       for (int d = 0; d < 16; ++d) acc[d] += (long long)ci * x[d];
@@ -1233,7 +1315,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
 #ifdef RNNL_DIAG_NOSCORE
         const float base = 0.f;
 #else
-        const float base = (p.feature == RNNL_FEATURE_NONE || p.cand_out) ? 0.f : p.score[idx];
+        const float base = (p.feature == RNNL_FEATURE_NONE || p.cand_out) ? 0.f
+                           : p.base_row                                    ? p.base_row[t]
+                                                                           : p.score[idx];
 #endif
 #ifdef RNNL_DIAG_NOENTRIES  // diagnostic build: no bucket-entry walk
         for (int d = 0; d < 16; ++d) f[d] = (float)(cr.z * d);
@@ -1653,6 +1737,7 @@ static void set_score_params(KParams &p, const rnnl_predictor_params *pp, float 
   p.s1_w = pp->s1_w;
   p.s1_b = pp->s1_b;
   p.rel_emb = pp->rel_emb;
+  p.base_row = pp->base_row;
   p.score = score;
   p.mask = mask;
   p.digest = digest;

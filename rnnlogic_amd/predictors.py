@@ -513,6 +513,9 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         keep = [t.detach().float().contiguous() for t in tensors]
         (p.add_w, p.add_b, p.ln_w, p.ln_b, p.s0_w, p.s0_b, p.s1_w, p.s1_b,
          p.rel_emb) = [t.data_ptr() for t in keep]
+        if self.entity_feature == "bias":  # the scoring kernels add bias[t] without reading the filled row
+            keep.append(self.bias.detach().float().contiguous())
+            p.base_row = keep[-1].data_ptr()
         return p, keep
 
     def base_score(self, all_h, all_r, out):
