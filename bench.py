@@ -210,6 +210,53 @@ def isolated_ground_ms(model, graph, h, r, dev):
         return e0.elapsed_time(e1)
 
 
+def wn18rr_line(dev, reps=5):
+    """Config 3 of BASELINE.json as a secondary line: PredictorPlus(emb, pna)
+    + RotatE(D=500, gamma=6) over the WN18RR test split (206 batches, 6,268
+    queries, real rnnlogic_rules.txt: 7,386 rules, L <= 5), seeded synthetic
+    train graph and RotatE tables — the same timed step as `value` (rule
+    aggregates recomputed, RotatE + grounding + PNA scoring), plus the
+    grounding/scoring kernels alone and the RotatE kernel's VALU roofline."""
+    path = datasets.materialize("wn18rr", with_rotate=True)
+    random.seed(1)
+    np.random.seed(1)
+    torch.manual_seed(1)
+    with contextlib.redirect_stdout(sys.stderr):
+        graph = KnowledgeGraph(path)
+        TrainDataset(graph, 32)
+        ValidDataset(graph, 32)
+        test_set = TestDataset(graph, 32)
+        model = PredictorPlus(graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="RotatE",
+                              aggregator="pna", embedding_path=datasets.rotate_path("wn18rr"))
+        model.set_rules(datasets.rule_file("wn18rr"))
+    model = model.to(dev).eval()
+    rows = np.asarray([x for b in test_set.batches for x in b], dtype=np.int64)
+    h = torch.from_numpy(np.ascontiguousarray(rows[:, 0])).to(dev)
+    r = torch.from_numpy(np.ascontiguousarray(rows[:, 1])).to(dev)
+
+    def step():
+        model.invalidate_cache()
+        with torch.no_grad():
+            return model.forward_rows(h, r, None)
+    sec = time_forward(step, reps)
+    nq, E, D = len(rows), graph.entity_size, model.RotatE.emb_dim
+    with torch.no_grad():
+        tmp = torch.empty((nq, E), dtype=torch.float32, device=dev)
+        rot_ms = time_forward(lambda: model.RotatE.score_into(h, r, tmp), reps) * 1e3
+        del tmp
+    ground_ms = isolated_ground_ms(model, graph, h, r, dev)
+    flops = 7.0 * nq * E * D
+    return {"queries_per_s": round(nq / sec, 1), "ms_per_step": round(sec * 1e3, 3), "rows": nq,
+            "batches": len(test_set), "rules": model.num_rules,
+            "kernels_ms": {"rotate_alone": round(rot_ms, 3), "ground+score_isolated": round(ground_ms, 3)},
+            "roofline_rotate": {"bound": "valu", "achieved": round(flops / (rot_ms * 1e-3) / 1e12, 2),
+                                "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+                                "frac": round(flops / (rot_ms * 1e-3) / 1e12 / FP32_PEAK_TFS, 4),
+                                "alg_flops": flops, "kernel": "rotate_direct_kernel (alone, one launch)"},
+            "workload": "WN18RR test split, PredictorPlus(emb,3,16,pna) + RotatE(D=500,gamma=6); "
+                        "rnnlogic_rules.txt (L<=5); seeded synthetic train graph and RotatE tables"}
+
+
 def algorithmic_work(model, graph, rows, threads):
     """Exact per-rule work counts of the SURVEY §8(d) formula: F (frontier
     expansions), T (edge traversals), P ((rule, dest) pairs) and C
@@ -422,6 +469,44 @@ def main():
         extra["em_predictor_forward"] = {"queries_per_s": round(nq / sec, 1), "ms": round(sec * 1e3, 3),
                                          "rows": nq, "note": "Predictor(bias) over the test split, same rules"}
         del pred
+        extra["wn18rr_forward"] = wn18rr_line(dev)
+        # end-to-end evaluate('test') (trainer.py:145-248): device rows + filter
+        # flags, one forward over the split, device ranks, host metrics
+        from rnnlogic_amd.trainer import TrainerPredictor
+        solver = TrainerPredictor(model, model.train_set, None, test_set, None, gpus=[local])
+        t_first = time.perf_counter()
+        solver.evaluate("test")
+        torch.cuda.synchronize(dev)
+        t_first = time.perf_counter() - t_first
+        sec = time_forward(lambda: solver.evaluate("test"), 3)
+        extra["evaluate_test"] = {"queries_per_s": round(n_split / sec, 1), "ms": round(sec * 1e3, 3),
+                                  "first_call_ms": round(t_first * 1e3, 3), "rows": n_split,
+                                  "note": "TrainerPredictor.evaluate('test') end to end (MRR/Hits on the host); "
+                                          "the first call also uploads the split's rows and filter lists"}
+        # training steps (trainer.py:72-98): HIP grounding with edge removal,
+        # autograd on the path-count COO + RotatE (torch), Adam
+        opt = torch.optim.Adam(model.parameters(), lr=5e-3)
+        solver.optimizer = opt
+        from rnnlogic_amd.data import DeviceTrainBatches
+        dtb = DeviceTrainBatches(model.train_set, dev)
+        model.train()
+        batches = [[x.unsqueeze(0) for x in dtb[i]] for i in range(12)]
+        for b in batches[:2]:
+            solver.train_step(model, b, 0.2)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        nrow = 0
+        for b in batches[2:]:
+            solver.train_step(model, b, 0.2)
+            nrow += b[0].numel()
+        torch.cuda.synchronize(dev)
+        sec = time.perf_counter() - t1
+        model.eval()
+        extra["train_step"] = {"queries_per_s": round(nrow / sec, 1), "ms_per_batch": round(sec * 1e3 / 10, 3),
+                               "batches": 10, "rows": nrow,
+                               "note": "TrainerPredictor.train_step on FB15k-237 train batches (B=32, edge removal, "
+                                       "RotatE feature, Adam): forward + loss + backward + step"}
+        del solver, opt, dtb, batches
 
     if rank != 0:
         if world > 1:

@@ -165,7 +165,7 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
 /* workgroups: cap on the persistent workgroups of the launch (0 = the full
  * default occupancy); a smaller grid leaves room on the CUs for a kernel on
  * another stream (the RotatE overlap).
- * deferred (sum aggregator): the score pass writes each candidate's
+ * deferred (either aggregator): the score pass writes each candidate's
  * score_model output into the workspace instead of adding it into `score`
  * (it then neither reads nor writes `score`, so it can run beside
  * rnnl_rotate_score); rnnl_predictorplus_apply adds the outputs into the

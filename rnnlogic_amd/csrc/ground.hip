@@ -1086,6 +1086,10 @@ __global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__res
       const float out = score_one<AGG>(p, s_w, s_relb, cr.y, cr.z, ms,
                                        p.digest ? &dg : nullptr, t);
       if (p.digest) atomicAdd(&s_dig, (unsigned long long)dg);
+      if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
+        p.cand_out[qb + s] = out;
+        continue;
+      }
       const int64_t idx = (int64_t)q * p.g.E + t;
       if (p.feature == RNNL_FEATURE_NONE)
         p.score[idx] = out;
@@ -1831,10 +1835,6 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
   if (nq == 0) return RNNL_OK;
   set_score_params(p, pp, score, mask, digest);
   if (deferred) {
-    if (pp->aggregator != RNNL_AGG_SUM) {
-      set_error("rnnl_predictorplus_score: deferred scoring supports the sum aggregator only");
-      return RNNL_ERR_INVALID;
-    }
     p.cand_out = reinterpret_cast<float *>(static_cast<unsigned char *>(ws) + make_layout(nq, scale).off_cout);
   }
   hipStream_t st = (hipStream_t)stream;

@@ -648,7 +648,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         K = self.overlap_chunks
         bounds = [nq * k // K for k in range(K + 1)]
         agg = params.aggregator
-        deferred = self.overlap_deferred and agg == _native.AGG_SUM
+        deferred = self.overlap_deferred
         while True:
             scale = self.capacity_scale
             wss = [self._chunk_workspace(device, k, bounds[k + 1] - bounds[k], scale) for k in range(K)]
