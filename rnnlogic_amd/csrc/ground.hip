@@ -112,6 +112,8 @@ struct KParams {
   const float *base_row;  // nullable: every row's base score (bias), read instead of score[q][t]
   const int64_t *all_h, *all_r, *etr;
   int32_t nq;
+  int32_t ebits;     // entity bits of the packed (trie node, entity) keys
+  uint32_t emask;    // (1 << ebits) - 1
   float *score;
   uint8_t *mask;
   int32_t *n_cand;
@@ -143,12 +145,12 @@ __device__ __forceinline__ uint32_t hash32(uint32_t k) { return k * 2654435761u;
 
 
 // Per-slot scratch: two frontier buffers and the contribution list, each an
-// array of 12-B entries (a, b, count) — one contiguous run per list, so a
-// query touches a few compact address ranges (frontier: a = trie node,
-// b = entity; contribution: a = entity, b = trie node).
+// array of 8-B entries (key, count) — one contiguous run per list, so a query
+// touches a few compact address ranges.  key = (trie node - head root) <<
+// ebits | entity, the phase-A hash key (ebits = bits of |E|; the host checks
+// that a head's trie nodes fit the remaining 31 - ebits bits).
 struct Ent {
-  int32_t a, b;
-  uint32_t c;
+  uint32_t k, c;
 };
 
 struct Slot {
@@ -158,14 +160,16 @@ struct Slot {
   __device__ __forceinline__ Ent *f(int k) const { return f0 + (int64_t)k * fcap; }
 };
 
-__host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) { return 2 * fcap * 12 + pcap * 12; }
+__host__ __device__ inline int64_t slot_bytes(int64_t fcap, int64_t pcap) {
+  return 2 * fcap * (int64_t)sizeof(Ent) + pcap * (int64_t)sizeof(Ent);
+}
 
 __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, int64_t pcap) {
   unsigned char *b = base + (int64_t)slot * slot_bytes(fcap, pcap);
   Slot s;
   s.f0 = reinterpret_cast<Ent *>(b);
   s.fcap = fcap;
-  s.ct = reinterpret_cast<Ent *>(b + 2 * fcap * 12);
+  s.ct = reinterpret_cast<Ent *>(b + 2 * fcap * (int64_t)sizeof(Ent));
   return s;
 }
 
@@ -287,7 +291,7 @@ struct __align__(16) Smem {
     };
   };
   int ws[GNW + 1];
-  int q, nd, np, ovf, err;
+  int q, nd, np, ovf, err, root;
   long long qbase;
   unsigned long long t0;
   int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
@@ -295,20 +299,20 @@ struct __align__(16) Smem {
   unsigned long long tp[8];  // diagnostic sub-phase cycles (thread 0)
 };
 
-__device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pcap, int t, int node, uint32_t c) {
+__device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pcap, uint32_t key, uint32_t c) {
   const int pos = atomicAdd(&S.np, 1);
   if (pos < pcap) {
-    sl.ct[pos] = Ent{t, node, c};
+    sl.ct[pos] = Ent{key, c};
   } else {
     S.ovf = 1;
   }
 }
 
-__device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, int64_t fcap, int node, int v,
+__device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, int64_t fcap, uint32_t key,
                                               uint32_t c) {
   const int pos = atomicAdd(&S.nd, 1);
   if (pos < fcap) {
-    sl.f(buf)[pos] = Ent{node, v, c};
+    sl.f(buf)[pos] = Ent{key, c};
   } else {
     S.ovf = 1;
   }
@@ -356,8 +360,8 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
   const int E = p.g.E, R = p.g.R;
   const int depth = p.rl.head_depth[r];
   if (tid == 0) {
-    sl.f(0)[0] = Ent{root, h, 1u};
-    if (p.rl.node_info[root].w > 0) emit_contrib(S, sl, p.pcap, h, root, 1u);
+    sl.f(0)[0] = Ent{(uint32_t)h, 1u};
+    if (p.rl.node_info[root].w > 0) emit_contrib(S, sl, p.pcap, (uint32_t)h, 1u);
   }
   wg_sync_global();
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
@@ -370,8 +374,8 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       int nch = 0;
       if (tid < ne) {
         const Ent fe = sl.f(cur)[cb + tid];
-        const int node = fe.a;
-        S.ent_v[tid] = fe.b;
+        const int node = root + (int)(fe.k >> p.ebits);
+        S.ent_v[tid] = (int)(fe.k & p.emask);
         S.ent_c[tid] = fe.c;
         const int4 ni = p.rl.node_info[node];
         S.ent_fch[tid] = ni.y;
@@ -429,11 +433,11 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
               const int tt = ev_t[k];
               const int fl = S.it_flags[it];
               if (!((fl & 4) && tt == rm_dst)) {
-                const int child = S.it_child[it];
+                const uint32_t key = ((uint32_t)(S.it_child[it] - root) << p.ebits) | (uint32_t)tt;
                 const uint32_t c = S.it_c[it];
-                if (fl & 1) emit_contrib(S, sl, p.pcap, tt, child, c);
+                if (fl & 1) emit_contrib(S, sl, p.pcap, key, c);
                 if (fl & 2) {
-                  if (!hash_add(S, (child - root) * E + tt, c)) emit_frontier(S, sl, nxt, p.fcap, child, tt, c);
+                  if (!hash_add(S, (int)key, c)) emit_frontier(S, sl, nxt, p.fcap, key, c);
                 }
               }
             }
@@ -447,7 +451,7 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
     for (int s = tid; s < HCAP; s += GBS) {
       const int k = S.u.a.key[s];
       if (k != EMPTY) {
-        emit_frontier(S, sl, nxt, p.fcap, root + k / E, k % E, S.u.a.val[s]);
+        emit_frontier(S, sl, nxt, p.fcap, (uint32_t)k, S.u.a.val[s]);
         S.u.a.key[s] = EMPTY;
         S.u.a.val[s] = 0u;
       }
@@ -503,7 +507,7 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
   for (int i = tid; i < WIN; i += GBS) S.u.b.map[i] = 0;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) S.u.b.map[w[i].a - lo] = 1;  // mark present entities
+  for (int i = beg + tid; i < end; i += GBS) S.u.b.map[(int)(w[i].k & p.emask) - lo] = 1;  // mark present entities
   __syncthreads();
   for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = S.u.b.map[i];
   __syncthreads();
@@ -522,8 +526,8 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
     for (int i = beg + tid; i < end; i += GBS)
-      degree_add(S, reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[w[i].a - lo]]), w[i].c,
-                 p.rl.node_nrules[w[i].b]);
+      degree_add(S, reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[(int)(w[i].k & p.emask) - lo]]), w[i].c,
+                 p.rl.node_nrules[S.root + (int)(w[i].k >> p.ebits)]);
     __syncthreads();
     for (int s2 = tid; s2 < nc; s2 += GBS) {
       const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
@@ -532,7 +536,7 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
     __syncthreads();
     return nc;
   }
-  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.b.cnt[S.u.b.map[w[i].a - lo]], 1);  // bucket sizes
+  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.b.cnt[S.u.b.map[(int)(w[i].k & p.emask) - lo]], 1);  // bucket sizes
   __syncthreads();
   for (int i = tid; i < WIN; i += GBS) S.u.b.off[i] = S.u.b.cnt[i];
   __syncthreads();
@@ -547,9 +551,9 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
   __syncthreads();
   PSTAMP(1);
   for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
-    const int s2 = S.u.b.map[w[i].a - lo];
+    const int s2 = S.u.b.map[(int)(w[i].k & p.emask) - lo];
     const int64_t pos = qb + beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
-    p.bent[pos] = make_int2(w[i].b, (int)w[i].c);
+    p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
   }
   __syncthreads();
   PSTAMP(2);
@@ -594,7 +598,7 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
   if (by_rank)
     for (int i = tid; i < nw; i += GBS) S.sbits[i] = 0u;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, w[i].a, true)], 1);
+  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, (int)(w[i].k & p.emask), true)], 1);
   __syncthreads();
   constexpr int PER = HB / GBS;
   int loc[PER];
@@ -672,8 +676,8 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
     for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
     __syncthreads();
     for (int i = beg + tid; i < end; i += GBS)
-      degree_add(S, reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, w[i].a, false)]), w[i].c,
-                 p.rl.node_nrules[w[i].b]);
+      degree_add(S, reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, (int)(w[i].k & p.emask), false)]), w[i].c,
+                 p.rl.node_nrules[S.root + (int)(w[i].k >> p.ebits)]);
     __syncthreads();
     for (int i = tid; i < HB; i += GBS) {
       if (S.u.c.key[i] != EMPTY) {
@@ -697,9 +701,9 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
   for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
   __syncthreads();
   for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
-    const int sl2 = hb_slot(S, w[i].a, false);
+    const int sl2 = hb_slot(S, (int)(w[i].k & p.emask), false);
     const int64_t pos = qb + beg + S.u.c.off[by_rank ? S.u.c.cid[sl2] : sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
-    p.bent[pos] = make_int2(w[i].b, (int)w[i].c);
+    p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
   }
   __syncthreads();
   return nc;
@@ -716,7 +720,7 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
   if (!sorted) {
     for (int i = tid; i < nwin; i += GBS) S.whist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < P; i += GBS) atomicAdd(&S.whist[sl.ct[i].a >> WBITS], 1);
+    for (int i = tid; i < P; i += GBS) atomicAdd(&S.whist[(int)(sl.ct[i].k & p.emask) >> WBITS], 1);
     __syncthreads();
     if (tid == 0) {
       int acc = 0;
@@ -731,7 +735,7 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
     __syncthreads();
     for (int i = tid; i < P; i += GBS) {
       const Ent ce = sl.ct[i];
-      const int t = ce.a;
+      const int t = (int)(ce.k & p.emask);
       const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
       sl.f(0)[pos] = ce;
     }
@@ -814,6 +818,7 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
     if (tid == 0) {
       S.t0 = __builtin_amdgcn_s_memrealtime();
       S.err = 0;
+      S.root = root;
       S.np = 0;
       S.nd = 0;
       S.ovf = 0;
@@ -1693,9 +1698,19 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
     set_error(std::string(who) + ": too many rows for one launch (pool index exceeds 31 bits)");
     return RNNL_ERR_INVALID;
   }
+  // packed scratch keys (trie node - head root) << ebits | entity must fit 31 bits
+  int ebits = 1;
+  while ((1ll << ebits) < (int64_t)g->d.E) ++ebits;
+  if (((int64_t)std::max(r->d.max_head_nodes, 1) << ebits) > (int64_t)INT32_MAX) {
+    set_error(std::string(who) + ": a head relation's rule trie (" + std::to_string(r->d.max_head_nodes) +
+              " nodes) x 2^" + std::to_string(ebits) + " entities exceeds the 31-bit grounding keys");
+    return RNNL_ERR_INVALID;
+  }
   unsigned char *base = static_cast<unsigned char *>(ws);
   p = KParams{};
   p.g = g->d;
+  p.ebits = ebits;
+  p.emask = (uint32_t)((1u << ebits) - 1u);
   p.rl = r->d;
   p.all_h = all_h;
   p.all_r = all_r;
