@@ -284,6 +284,16 @@ int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *
                       int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
                       size_t workspace_bytes, void *stream);
 
+/* Backward of the RotatE score (training; embedding.py:45-70 under autograd):
+ * for grad = dL/dscore (n_queries x E, row-major), hr = h o r per query
+ * (n_queries x 2 dim: re | im, as torch forms it) and the entity planes
+ * (dim x 2 x ld: planes[(2 d + part) * ld + e], ld >= E), writes
+ *   d_tail (dim x 2 x E, same plane order) = dL/d(tail entity embedding)
+ * and accumulates (atomically; zero it first) d_hr (n_queries x 2 dim) +=
+ * dL/d(h o r).  torch.norm's convention: zero gradient where |hr - t| = 0. */
+int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const float *grad, int32_t n_queries,
+                         int32_t n_entities, int32_t dim, float *d_hr, float *d_tail, void *stream);
+
 /* ------------------------------------------------------ training batches --
  * Device-side TrainDataset rows (reference src/data.py:201-219, the target
  * part): out (n_rows x width, f32, row-major) = multi-hot of the value list

@@ -551,6 +551,93 @@ static unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>((n + 25
 
 using namespace rnnl;
 
+// ------------------------------------------------------------ backward (training)
+// Gradient of score[q][e] = gamma - sum_d |hr[q][d] - t[e][d]| (complex
+// entries; embedding.py:45-70, torch.norm's backward with grad 0 at a zero
+// norm) for the incoming grad g (B x E):
+//   d_tail[e][d] = sum_q g[q][e] (hr - t) / |hr - t|   (both parts)
+//   d_hr[q][d]  -= sum_e g[q][e] (hr - t) / |hr - t|
+// One thread per (entity, dim) for BW_EPT entities (stride 256, coalesced over
+// the transposed entity planes [D][2][ld]); the per-query sums over entities
+// are reduce-scattered over the wave (63 shuffles for 32 queries x 2 parts),
+// then over the block's waves in LDS, then one atomicAdd per (block, q, part).
+constexpr int BW_EPT = 4;
+constexpr int BW_BS = 256;
+
+__global__ __launch_bounds__(BW_BS) void rotate_backward_kernel(const float *__restrict__ planes, int ld,
+                                                                const float *__restrict__ hr,
+                                                                const float *__restrict__ g, int B, int E, int D,
+                                                                float *__restrict__ d_hr,
+                                                                float *__restrict__ d_tail) {
+  __shared__ float s_red[BW_BS / 64][64];
+  const int d = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e0 = blockIdx.x * (BW_BS * BW_EPT) + threadIdx.x;
+  float a[BW_EPT], b[BW_EPT], ta[BW_EPT], tb[BW_EPT];
+#pragma unroll
+  for (int k = 0; k < BW_EPT; ++k) {
+    const int e = e0 + k * BW_BS;
+    a[k] = e < E ? planes[(int64_t)(2 * d) * ld + e] : 0.f;
+    b[k] = e < E ? planes[(int64_t)(2 * d + 1) * ld + e] : 0.f;
+    ta[k] = tb[k] = 0.f;
+  }
+  for (int q0 = 0; q0 < B; q0 += 32) {
+    float v[64];  // v[j] = sum over this thread's entities of w x (query q0 + j), v[32 + j] = w y
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      float sx = 0.f, sy = 0.f;
+      const int q = q0 + j;
+      if (q < B) {  // uniform
+        const float hre = hr[(int64_t)q * 2 * D + d], him = hr[(int64_t)q * 2 * D + D + d];
+#pragma unroll
+        for (int k = 0; k < BW_EPT; ++k) {
+          const int e = e0 + k * BW_BS;
+          if (e < E) {
+            const float x = hre - a[k], y = him - b[k];
+            const float s = fmaf(x, x, y * y);
+            const float w = s > 0.f ? g[(int64_t)q * E + e] / sqrtf(s) : 0.f;
+            sx = fmaf(w, x, sx);
+            sy = fmaf(w, y, sy);
+            ta[k] = fmaf(w, x, ta[k]);
+            tb[k] = fmaf(w, y, tb[k]);
+          }
+        }
+      }
+      v[j] = sx;
+      v[32 + j] = sy;
+    }
+    // reduce-scatter over the wave: lane L ends with the wave's total of v[L]
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const bool up = (lane & m) != 0;
+#pragma unroll
+      for (int o = 0; o < m; ++o) {
+        const float keep = up ? v[o + m] : v[o];
+        const float give = up ? v[o] : v[o + m];
+        v[o] = keep + __shfl_xor(give, m, 64);
+      }
+    }
+    s_red[wave][lane] = v[0];
+    __syncthreads();
+    if (wave == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < BW_BS / 64; ++w2) t += s_red[w2][lane];
+      const int q = q0 + (lane & 31);
+      if (q < B) atomicAdd(&d_hr[(int64_t)q * 2 * D + (lane < 32 ? d : D + d)], -t);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < BW_EPT; ++k) {
+    const int e = e0 + k * BW_BS;
+    if (e < E) {
+      d_tail[(int64_t)(2 * d) * E + e] = ta[k];
+      d_tail[(int64_t)(2 * d + 1) * E + e] = tb[k];
+    }
+  }
+}
+
 extern "C" {
 
 int rnnl_fill_rows(const float *row, int32_t nq, int32_t E, float *score, void *stream) {
@@ -659,6 +746,20 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
                        (hipStream_t)stream, eemb, (const uint2 *)etab, (const float2 *)rtab, D, gamma, all_h, all_r,
                        nq, E, score, accumulate, g_clk);
   }
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const float *grad, int32_t nq,
+                         int32_t E, int32_t D, float *d_hr, float *d_tail, void *stream) {
+  if (!planes || !hr || !grad || !d_hr || !d_tail || nq < 0 || E <= 0 || D <= 0 || ld < E) {
+    set_error("rnnl_rotate_backward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  const unsigned bx = (unsigned)((E + BW_BS * BW_EPT - 1) / (BW_BS * BW_EPT));
+  hipLaunchKernelGGL(rotate_backward_kernel, dim3(bx, (unsigned)D), dim3(BW_BS), 0, (hipStream_t)stream, planes, ld,
+                     hr, grad, nq, E, D, d_hr, d_tail);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -16,6 +16,37 @@ import torch
 from . import _native
 
 
+class _RotatEScore(torch.autograd.Function):
+    """score = gamma - sum_d |hr - t| for every (row, entity): forward by the
+    HIP scorer (rnnl_rotate_score), backward by rnnl_rotate_backward, which
+    writes dL/d(tail embeddings) and dL/d(h o r) without the (B, |E|, D)
+    difference tensors of the torch formulation; h o r is formed by torch
+    ops from eemb / remb so autograd carries d(h o r) on to h and r."""
+
+    @staticmethod
+    def forward(ctx, eemb, hr_re, hr_im, module, all_h, all_r):
+        out = torch.empty((all_h.numel(), module.num_entities), dtype=torch.float32, device=eemb.device)
+        module.score_into(all_h, all_r, out)
+        ctx.module = module
+        ctx.save_for_backward(eemb, hr_re, hr_im)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        eemb, hr_re, hr_im = ctx.saved_tensors
+        E, D = ctx.module.num_entities, ctx.module.emb_dim
+        nq = hr_re.size(0)
+        planes = eemb.detach().view(E, 2, D).permute(2, 1, 0).contiguous()  # [D][2][E]
+        hr = torch.cat([hr_re, hr_im], dim=1).detach().float().contiguous()
+        grad = grad.detach().float().contiguous()
+        d_hr = torch.zeros((nq, 2 * D), dtype=torch.float32, device=eemb.device)
+        d_tail = torch.empty((D, 2, E), dtype=torch.float32, device=eemb.device)
+        _native.call("rnnl_rotate_backward", planes.data_ptr(), E, hr.data_ptr(), grad.data_ptr(), nq, E, D,
+                     d_hr.data_ptr(), d_tail.data_ptr(), torch.cuda.current_stream(eemb.device).cuda_stream)
+        d_eemb = d_tail.permute(2, 1, 0).reshape(E, 2 * D)
+        return d_eemb, d_hr[:, :D], d_hr[:, D:], None, None, None
+
+
 class RotatE(torch.nn.Module):
     def __init__(self, path):
         super(RotatE, self).__init__()
@@ -98,10 +129,27 @@ class RotatE(torch.nn.Module):
         diff = torch.stack([re_hr.unsqueeze(1) - re_t.unsqueeze(0), im_hr.unsqueeze(1) - im_t.unsqueeze(0)], dim=0)
         return self.gamma - diff.norm(dim=0).sum(dim=-1)
 
+    def forward_grad(self, all_h, all_r):
+        """Differentiable (B, |E|) scores for training: the HIP scorer forward
+        and rnnl_rotate_backward (_RotatEScore); h o r by torch ops, as in
+        forward_torch, so autograd reaches eemb rows of h and remb."""
+        pi = 3.141592653589793238462643383279
+        D = self.emb_dim
+        all_h = all_h.to(self.eemb.device, torch.int64)
+        all_r = all_r.to(self.eemb.device, torch.int64)
+        h = self.eemb.index_select(0, all_h)
+        phase = self.remb.index_select(0, all_r) / (self.range / pi)
+        re_r, im_r = torch.cos(phase), torch.sin(phase)
+        re_h, im_h = h[:, :D], h[:, D:]
+        re_hr = re_h * re_r - im_h * im_r
+        im_hr = re_h * im_r + im_h * re_r
+        return _RotatEScore.apply(self.eemb, re_hr, im_hr, self, all_h, all_r)
+
     def forward(self, all_h, all_r):
         """(B, |E|) = gamma - sum_d |h o r - e| (embedding.py:64-70): the HIP
-        kernel, or forward_torch when autograd needs the graph (training)."""
+        kernel; with autograd active (training) the same kernel plus its HIP
+        backward (forward_grad)."""
         if torch.is_grad_enabled() and (self.eemb.requires_grad or self.remb.requires_grad):
-            return self.forward_torch(all_h.to(self.eemb.device), all_r.to(self.eemb.device))
+            return self.forward_grad(all_h, all_r)
         out = torch.empty((all_h.numel(), self.num_entities), dtype=torch.float32, device=self.eemb.device)
         return self.score_into(all_h, all_r, out)

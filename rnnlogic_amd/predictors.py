@@ -722,7 +722,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             if self.entity_feature == "bias":
                 return zero + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
             if self.entity_feature == "RotatE":
-                return zero + self.RotatE.forward_torch(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
+                return zero + self.RotatE.forward_grad(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
                                                                                  device=device)
             return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
         nr = self.native_rules(device)
@@ -762,7 +762,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if self.entity_feature == "bias":
             return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
         if self.entity_feature == "RotatE":
-            return score + self.RotatE.forward_torch(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
+            return score + self.RotatE.forward_grad(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
                                                                                 device=device)
         mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
         return score.masked_fill(~mask, float("-inf")), mask

@@ -53,7 +53,7 @@ class Fixture:
 
 
 ALL_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN)
-                   if f.endswith(".npz") and not f.startswith(("_", "train_", "pred_", "rules_", "eval_", "em_")))
+                   if f.endswith(".npz") and not f.startswith(("_", "train_", "pred_", "rules_", "eval_", "em_", "flow_")))
 # reference miner rule pools (tools/make_golden_rules.py)
 RULE_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("rules_") and f.endswith(".npz"))
 
