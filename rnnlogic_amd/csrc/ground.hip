@@ -26,6 +26,7 @@
 // streaming shape.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 
 #include "internal.h"
@@ -129,6 +130,7 @@ struct KParams {
   int4 *cand;        // per pool index: candidate record (entity, bucket start, bucket length, 0)
                      // (the first n_cand entries of a query's run)
   int2 *bent;        // bucket entries: (trie node, path count bits)
+  float *memo;       // SUM: score_model output of a candidate reached by one path of one leaf node
   unsigned long long *prof;  // diagnostic phase cycle counters (nullable)
 };
 
@@ -176,7 +178,7 @@ __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, in
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
-  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, total;
+  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, off_memo, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -185,7 +187,9 @@ static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 // them so tests can force the overflow -> retry path.
 static int64_t g_fcap_base = FCAP_BASE, g_pcap_base = PCAP_BASE, g_pool_per_query = POOL_PER_QUERY;
 
-static Layout make_layout(int64_t nq, int64_t scale) {
+// n_nodes: the rules' trie nodes, for the SUM scoring memo at the end of the
+// workspace (0 where only the offsets before it are needed)
+static Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   Layout L;
   L.nslots = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)NUM_CU * WG_PER_CU));
   L.fcap = g_fcap_base * scale;
@@ -204,6 +208,8 @@ static Layout make_layout(int64_t nq, int64_t scale) {
   o += 4 * L.pool_cap;
   L.off_slots = o = align256(o);
   o += L.nslots * slot_bytes(L.fcap, L.pcap);
+  L.off_memo = o = align256(o);
+  o += 4 * n_nodes;
   L.total = o;
   return L;
 }
@@ -1188,6 +1194,19 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
   for (int d = 0; d < 16; ++d) f[d] = (float)((double)acc[d] * (double)inv_scale);
 }
 
+// The feature of a candidate whose only bucket entry is (n, c): gather_sum's
+// arithmetic for that single entry (the memo of score_sum_memo_kernel).
+template <bool DIGEST>
+__device__ __forceinline__ void gather_sum_entry(const KParams &p, int n, uint32_t cu, float inv_scale, float f[16],
+                                                 long long &deg, uint64_t &fp) {
+  const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+  const long long c = cu;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) f[d] = (float)((double)(0ll + c * x[d]) * (double)inv_scale);
+  deg = DIGEST ? c * p.rl.node_nrules[n] : 0;
+  fp = DIGEST ? (uint64_t)c * p.rl.node_fp[n] : 0;
+}
+
 // FuncToNodeSum tail + score_model on the candidate's feature sums
 __device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const float *relb, const float f[16]) {
   using L = WL<RNNL_AGG_SUM>;
@@ -1364,6 +1383,182 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
   }
 }
 
+
+// ---------------------------------------------------------------- K2 (sum): single-path memo
+// Most candidates are reached by few paths; 38 % of the FB15k-237 test
+// candidates by exactly one path of one rule-end node n (one bucket entry of
+// count 1).  Their feature is n's record itself, so their score_model output
+// depends on (head relation, n) only: memo_sum_kernel computes it once per
+// launch for every leaf node of every head (131,883 MLPs instead of ~22 M).
+// score_sum_memo_kernel sends those candidates down a short path (candidate
+// record, one bucket entry, the memo: three loads and the store) and queues
+// the others in LDS, running the full gather + MLP over full tiles of queued
+// candidates — the MLP tiles are full, and a query needs ~62 % as many.  The
+// memo entry is computed by the same code from the same integer record as
+// the full path (gather_sum with one entry of count 1, mlp_sum), so the two
+// paths give the same output for such a candidate.
+__device__ __forceinline__ void load_sum_weights(float *s_w, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_SUM>;
+  for (int i = threadIdx.x; i < L::N; i += blockDim.x) {
+    float v = 0.f;
+    if (i < L::ADDB) v = W[W_ADDW + i];
+    else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
+    else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
+    else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
+    else if (i < L::S1W) v = W[W_S0X + i - L::S0X];
+    else if (i < L::S1B) v = W[W_S1W + i - L::S1W];
+    else if (i == L::S1B) v = W[W_S1B];
+    s_w[i] = v;
+  }
+}
+
+__device__ __forceinline__ void fold_relation_bias(const KParams &p, float *s_relb, int r) {
+  if (threadIdx.x < 128) {
+    // relation half of score_model.layers.0 folded into a per-query bias
+    float acc = p.s0_b[threadIdx.x];
+    for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[threadIdx.x * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+    s_relb[threadIdx.x] = acc;
+  }
+}
+
+// One workgroup per head relation with rules: memo[n] for its leaf nodes.
+__global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_SUM>;
+  __shared__ __attribute__((aligned(16))) float s_w[L::N];
+  __shared__ float s_relb[128];
+  const int r = blockIdx.x;
+  const int lp = p.rl.head_leaf_ptr[r], nl = p.rl.head_leaf_ptr[r + 1] - lp;
+  if (nl <= 0) return;  // uniform
+  load_sum_weights(s_w, W);
+  fold_relation_bias(p, s_relb, r);
+  __syncthreads();
+  const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
+  const float inv_scale = ldexpf(1.f, -shift);
+  SumStage st{};
+  for (int i = threadIdx.x; i < nl; i += BS) {
+    const int n = p.rl.head_leaf_node[lp + i];
+    float f[16];
+    long long deg;
+    uint64_t fp;
+    // the full path's feature for a candidate with the single entry (n, 1)
+    gather_sum_entry<false>(p, n, 1u, inv_scale, f, deg, fp);
+    asm volatile("" ::: "memory");
+    p.memo[n] = mlp_sum(s_w, s_relb, f);
+  }
+}
+
+__device__ __forceinline__ void sum_write_out(const KParams &p, int q, int64_t ci, int t, float out, float base) {
+  if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
+    p.cand_out[ci] = out;
+    return;
+  }
+  const int64_t idx = (int64_t)q * p.g.E + t;
+  p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + base;
+  if (p.mask) p.mask[idx] = 1;
+}
+
+__device__ __forceinline__ float sum_base(const KParams &p, int q, int t) {
+  if (p.feature == RNNL_FEATURE_NONE || p.cand_out) return 0.f;
+  return p.base_row ? p.base_row[t] : p.score[(int64_t)q * p.g.E + t];
+}
+
+template <bool DIGEST>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_WAVES, 8))) void score_sum_memo_kernel(
+    KParams p, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_SUM>;
+  __shared__ __attribute__((aligned(16))) float s_w[L::N];
+  __shared__ float s_relb[128];
+  __shared__ int s_queue[2 * BS];
+  __shared__ int s_q, s_r, s_n;
+  __shared__ unsigned long long s_dig;
+  const int tid = threadIdx.x;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  load_sum_weights(s_w, W);
+  if (tid == 0) s_r = -1;
+  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum));
+  const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
+  const float inv_scale = ldexpf(1.f, -shift);
+  SumStage st{};
+#pragma unroll 1
+  while (true) {
+    __syncthreads();
+    if (tid == 0) {
+      s_q = (int)atomicAdd(&hdr[H_DEQUEUE2], 1u);
+      s_dig = 0ull;
+      s_n = 0;
+    }
+    __syncthreads();
+    const int q = s_q;
+    if (q >= p.nq) break;
+    const int nc = p.n_cand[q];
+    if (nc <= 0) {
+      if (tid == 0 && DIGEST && nc == 0) p.digest[q] = 0;
+      continue;
+    }
+    const int r = (int)p.all_r[q];
+    const int root = p.rl.head_root[r];
+    if (r != s_r) {
+      fold_relation_bias(p, s_relb, r);
+      __syncthreads();
+      if (tid == 0) s_r = r;
+    }
+    const int64_t qb = p.q_base[q];
+    for (int s0 = 0; s0 < nc; s0 += BS) {
+      const int s2 = s0 + tid;
+      if (s2 < nc) {
+        const int4 cr = p.cand[qb + s2];
+        bool queued = true;
+        if (cr.z == 1) {
+          const int2 be = p.bent[cr.y];
+          if (be.y == 1) {  // one path of one leaf node: the memo
+            queued = false;
+            const float base = sum_base(p, q, cr.x);
+            if constexpr (DIGEST)
+              atomicAdd(&s_dig, (unsigned long long)mix64((uint64_t)cr.x ^
+                                                          mix64((uint64_t)p.rl.node_nrules[be.x] ^
+                                                                mix64(p.rl.node_fp[be.x]))));
+            sum_write_out(p, q, qb + s2, cr.x, p.memo[be.x], base);
+          }
+        }
+        if (queued) s_queue[atomicAdd(&s_n, 1)] = s2;
+      }
+      __syncthreads();
+      const bool last = s0 + BS >= nc;
+#pragma unroll 1
+      while (true) {
+        const int n = s_n;  // uniform (read after a barrier)
+        if (!(n >= BS || (last && n > 0))) break;
+        const int take = min(n, BS);
+        if (tid < take) {
+          const int c2 = s_queue[tid];
+          const int4 cr = p.cand[qb + c2];
+          const float base = sum_base(p, q, cr.x);  // issued before the gather: its latency hides under it
+          float f[16];
+          long long deg;
+          uint64_t fp;
+          gather_sum<false, DIGEST>(p, st, root, cr.y, cr.z, inv_scale, f, deg, fp);
+          if constexpr (DIGEST)
+            atomicAdd(&s_dig, (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
+          // keep the loop-invariant LDS weight reads inside the loop (hoisted,
+          // they would pin ~200 VGPRs and starve occupancy)
+          asm volatile("" ::: "memory");
+          sum_write_out(p, q, qb + c2, cr.x, mlp_sum(s_w, s_relb, f), base);
+        }
+        __syncthreads();  // every lane has read its queue entry
+        const int rest = n - take;
+        const int v = tid < rest ? s_queue[take + tid] : 0;
+        __syncthreads();
+        if (tid < rest) s_queue[tid] = v;
+        if (tid == 0) s_n = rest;
+        __syncthreads();
+      }
+    }
+    if (DIGEST) {
+      __syncthreads();
+      if (tid == 0) p.digest[q] = s_dig;
+    }
+  }
+}
 
 // Deferred scoring, second half: score[q][t] = out + score[q][t] (the same
 // fp32 sum as the direct path, operands commuted) and mask[q][t] = 1 for every
@@ -1672,7 +1867,7 @@ int rnnl_forward_workspace_size(rnnl_graph g, rnnl_rules r, int32_t nq, int32_t 
     set_error("rnnl_forward_workspace_size: bad arguments");
     return RNNL_ERR_INVALID;
   }
-  *bytes = (size_t)make_layout(nq, scale).total;
+  *bytes = (size_t)make_layout(nq, scale, r->d.n_nodes).total;
   return RNNL_OK;
 }
 
@@ -1689,7 +1884,7 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
     set_error(std::string(who) + ": more entities than the kernel's window table supports");
     return RNNL_ERR_INVALID;
   }
-  const Layout Ly = make_layout(nq, scale);
+  const Layout Ly = make_layout(nq, scale, r->d.n_nodes);
   if ((int64_t)ws_bytes < Ly.total) {
     set_error(std::string(who) + ": workspace too small");
     return RNNL_ERR_INVALID;
@@ -1727,6 +1922,7 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
   p.q_scale = reinterpret_cast<float *>(base + Ly.off_qscale);
   p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
   p.bent = reinterpret_cast<int2 *>(base + Ly.off_bent);
+  p.memo = reinterpret_cast<float *>(base + Ly.off_memo);
   p.prof = g_prof;
   return RNNL_OK;
 }
@@ -1762,6 +1958,15 @@ static void set_score_params(KParams &p, const rnnl_predictor_params *pp, float 
   p.digest = digest;
 }
 
+// RNNL_SCORE_MEMO=0 selects the scoring pass without the single-path memo (A/B)
+static bool score_memo_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("RNNL_SCORE_MEMO");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int grid = 0) {
   const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
@@ -1776,6 +1981,14 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int gri
 #define RNNL_STAGE_LIMIT 0  // staging measured slower (lower occupancy); kept for A/B
 #endif
     const bool staged = base_lds + stage <= RNNL_STAGE_LIMIT;
+    if (!staged && score_memo_enabled() && p.memo) {
+      hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, (const float *)W);
+      if (p.digest)
+        hipLaunchKernelGGL((score_sum_memo_kernel<true>), dim3(sgrid), dim3(BS), 0, st, p, (const float *)W);
+      else
+        hipLaunchKernelGGL((score_sum_memo_kernel<false>), dim3(sgrid), dim3(BS), 0, st, p, (const float *)W);
+      return;
+    }
     const size_t lds = (size_t)(staged ? base_lds + stage : base_lds);
     if (staged)
       hipLaunchKernelGGL((score_sum_kernel<true, true>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
