@@ -365,8 +365,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self.num_entities = graph.entity_size
         self.num_relations = graph.relation_size
         self.padding_index = graph.relation_size
-        if hidden_dim != 16:
-            raise NotImplementedError("the HIP kernels are specialised for hidden_dim == 16 (reference default)")
+        # the fused scoring kernels are specialised for the reference's hidden_dim
+        # 16; other sizes run the HIP grounding + the aggregation / MLP as torch
+        # ops on the grounding COO (forward_coo), on the GPU as well
+        self.fused = hidden_dim == 16
 
         # module creation order == reference (identical RNG consumption under set_seed)
         self.vocab_emb = torch.nn.Embedding(self.num_relations + 1, self.hidden_dim, padding_idx=self.num_relations)
@@ -564,6 +566,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             out = (torch.empty((0, self.num_entities), dtype=torch.float32, device=device),
                    torch.empty((0, self.num_entities), dtype=torch.bool, device=device))
             return out + (torch.empty(0, dtype=torch.int32, device=device),) if return_ncand else out
+        if not self.fused:
+            with torch.no_grad():
+                score, mask, n_cand = self.forward_coo(all_h, all_r, etr)
+            return (score, mask, n_cand) if return_ncand else (score, mask)
         g = self.graph.device_graph(device)
         nr = self.native_rules(device)
         rec = (lambda k: events.setdefault(k, torch.cuda.Event(enable_timing=True)).record()) \
@@ -715,8 +721,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         all_r = all_r.to(torch.int64)
         nq, E = all_h.numel(), self.num_entities
         row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
-        C = ent.numel()
-        if C == 0:
+        if ent.numel() == 0:
             # predictors.py:230-237 early return
             zero = torch.zeros((nq, E), device=device)
             if self.entity_feature == "bias":
@@ -725,6 +730,36 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 return zero + self.RotatE.forward_grad(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
                                                                                  device=device)
             return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
+        return self._score_coo(all_h, all_r, row, ent, ce, node, count)
+
+    def forward_coo(self, all_h, all_r, edges_to_remove=None):
+        """Rows of any relations through the HIP grounding COO and the torch
+        aggregation / MLP (any hidden_dim): (score, mask, n_cand), the
+        forward_rows contract — rows without candidates keep their base score
+        (bias / RotatE) or -inf with the mask False (entity_feature none)."""
+        device = all_h.device
+        all_h = all_h.to(torch.int64)
+        all_r = all_r.to(torch.int64)
+        nq, E = all_h.numel(), self.num_entities
+        row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
+        n_cand = torch.zeros(nq, dtype=torch.int32, device=device).index_add_(
+            0, row, torch.ones_like(row, dtype=torch.int32))
+        if ent.numel() == 0:
+            if self.entity_feature == "bias":
+                return self.bias.detach().float().unsqueeze(0).expand(nq, E).contiguous(), \
+                    torch.ones((nq, E), dtype=torch.bool, device=device), n_cand
+            if self.entity_feature == "RotatE":
+                return self.RotatE(all_h, all_r), torch.ones((nq, E), dtype=torch.bool, device=device), n_cand
+            return torch.full((nq, E), float("-inf"), device=device), \
+                torch.zeros((nq, E), dtype=torch.bool, device=device), n_cand
+        score, mask = self._score_coo(all_h, all_r, row, ent, ce, node, count)
+        return score, mask, n_cand
+
+    def _score_coo(self, all_h, all_r, row, ent, ce, node, count):
+        """predictors.py:238-271 on the grounding COO (torch ops)."""
+        device = all_h.device
+        nq, E = all_h.numel(), self.num_entities
+        C = ent.numel()
         nr = self.native_rules(device)
         rels = torch.unique(all_r).tolist()
         ridx = torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
@@ -762,8 +797,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if self.entity_feature == "bias":
             return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
         if self.entity_feature == "RotatE":
-            return score + self.RotatE.forward_grad(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
-                                                                                device=device)
+            rot = self.RotatE.forward_grad(all_h, all_r) if self._needs_grad() else self.RotatE(all_h, all_r)
+            return score + rot, torch.ones((nq, E), dtype=torch.bool, device=device)
         mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
         return score.masked_fill(~mask, float("-inf")), mask
 
