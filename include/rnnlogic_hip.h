@@ -311,6 +311,14 @@ int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals
 int rnnl_filter_flags(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
                       const int64_t *row_keys, int32_t n_rows, int32_t width, uint8_t *out, void *stream);
 
+/* evaluate()'s filtered rank bounds (reference src/trainer.py:191-203) in one
+ * pass per row: for row i with target t = all_t[i], L[i] = #(flag & score >
+ * score[t]) + 1 and H[i] = #(flag & score >= score[t]) + 2 when mask[i][t],
+ * else (1, n_entities + 1).  score f32, mask / flag bytes, all n_rows x
+ * n_entities row-major. */
+int rnnl_filtered_ranks(const float *score, const uint8_t *mask, const uint8_t *flag, const int64_t *all_t,
+                        int32_t n_rows, int32_t n_entities, int64_t *L, int64_t *H, void *stream);
+
 /* ---------------------------------------------------------- rule mining --
  * The reference miner's RuleMiner::search (miner/rnnlogic.cpp:505-589 with
  * KnowledgeGraph::rule_search :350-382) on the GPU: for every train triple

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("rnnl_rotate_workspace_size", ctypes.c_int, [_I32, _I32, _I32, _P]),
     ("rnnl_multi_hot", ctypes.c_int, [_P, _P, _P, _I64, _P, _I32, _I32, _P, _P]),
     ("rnnl_filter_flags", ctypes.c_int, [_P, _P, _P, _I64, _P, _I32, _I32, _P, _P]),
+    ("rnnl_filtered_ranks", ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _P, _P, _P]),
     ("rnnl_miner_create", ctypes.c_int, [_P, _I64, _I32, _I32, _P]),
     ("rnnl_miner_destroy", ctypes.c_int, [_P]),
     ("rnnl_rule_search", ctypes.c_int, [_P, _I32, _P, _I64, _P, _I64, _P, _P]),

@@ -65,6 +65,44 @@ static int check_lists(const char *fn, const int64_t *keys, const int64_t *offs,
 
 using namespace rnnl;
 
+// Filtered rank bounds of evaluate() (trainer.py:191-203) for one row per
+// workgroup, in one pass over the row: L = #(flagged scores > s_t) + 1,
+// H = #(flagged scores >= s_t) + 2, or (1, E + 1) when t is not a candidate.
+__global__ __launch_bounds__(256) void filtered_ranks_kernel(const float *__restrict__ score,
+                                                             const uint8_t *__restrict__ mask,
+                                                             const uint8_t *__restrict__ flag,
+                                                             const int64_t *__restrict__ all_t, int E,
+                                                             int64_t *__restrict__ L, int64_t *__restrict__ H) {
+  __shared__ int s_gt[4], s_ge[4];
+  const int64_t row = blockIdx.x;
+  const float *sr = score + row * E;
+  const uint8_t *fr = flag + row * E;
+  const int t = (int)all_t[row];
+  const float val = sr[t];
+  int gt = 0, ge = 0;
+  for (int e = threadIdx.x; e < E; e += 256) {
+    const float v = sr[e];
+    const int f = fr[e] != 0;
+    gt += f & (v > val);
+    ge += f & (v >= val);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    gt += __shfl_xor(gt, o, 64);
+    ge += __shfl_xor(ge, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_gt[threadIdx.x >> 6] = gt;
+    s_ge[threadIdx.x >> 6] = ge;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const bool hit = mask[row * E + t] != 0;
+    L[row] = hit ? (int64_t)(s_gt[0] + s_gt[1] + s_gt[2] + s_gt[3]) + 1 : 1;
+    H[row] = hit ? (int64_t)(s_ge[0] + s_ge[1] + s_ge[2] + s_ge[3]) + 2 : (int64_t)E + 1;
+  }
+}
+
 extern "C" {
 
 int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
@@ -83,6 +121,19 @@ int rnnl_filter_flags(const int64_t *keys, const int64_t *offs, const int32_t *v
   if (rc != RNNL_OK || n_rows == 0) return rc;
   hipLaunchKernelGGL(multi_hot_kernel<uint8_t>, dim3(n_rows), dim3(256), 0, (hipStream_t)stream, keys, offs, vals,
                      n_keys, row_keys, width, out, (uint8_t)1, (uint8_t)0);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_filtered_ranks(const float *score, const uint8_t *mask, const uint8_t *flag, const int64_t *all_t,
+                        int32_t n_rows, int32_t n_entities, int64_t *L, int64_t *H, void *stream) {
+  if (!score || !mask || !flag || !all_t || !L || !H || n_rows < 0 || n_entities <= 0) {
+    set_error("rnnl_filtered_ranks: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (n_rows == 0) return RNNL_OK;
+  hipLaunchKernelGGL(filtered_ranks_kernel, dim3(n_rows), dim3(256), 0, (hipStream_t)stream, score, mask, flag, all_t,
+                     n_entities, L, H);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

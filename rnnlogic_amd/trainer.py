@@ -22,7 +22,7 @@ from torch import distributed as dist
 from torch import nn
 from torch.utils import data as torch_data
 
-from . import comm
+from . import _native, comm
 from .data import DeviceEvalBatches, DeviceTrainBatches, Iterator
 
 
@@ -176,6 +176,17 @@ class TrainerPredictor(object):
         """(L, H) per row, trainer.py:191-203: L = #(flagged scores > s_t) + 1,
         H = #(flagged scores >= s_t) + 2, or (1, |E| + 1) when t is not a
         candidate — computed for all rows at once on the device."""
+        if logits.is_cuda and logits.dtype == torch.float32 and mask.dtype == torch.bool and flag.dtype == torch.bool:
+            # one pass per row on the device (rnnl_filtered_ranks)
+            n = all_t.numel()
+            L = torch.empty(n, dtype=torch.int64, device=logits.device)
+            H = torch.empty(n, dtype=torch.int64, device=logits.device)
+            t = all_t.to(logits.device, torch.int64).contiguous()
+            sc, mk, fl = logits.contiguous(), mask.contiguous(), flag.contiguous()
+            _native.call("rnnl_filtered_ranks", sc.data_ptr(), mk.data_ptr(), fl.data_ptr(), t.data_ptr(), n,
+                         num_entities, L.data_ptr(), H.data_ptr(),
+                         torch.cuda.current_stream(logits.device).cuda_stream)
+            return L, H
         rows = torch.arange(all_t.numel(), device=logits.device)
         val = logits[rows, all_t].unsqueeze(1)
         L = ((logits > val) & flag).sum(1) + 1
@@ -199,8 +210,13 @@ class TrainerPredictor(object):
         n_rows = len(a)
         if n_rows == 0:
             return dict(Data=0, Hit1=0.0, Hit3=0.0, Hit10=0.0, MR=0.0, MRR=0.0)
-        # last occurrence of each (h, r, t)
-        _, first_rev = np.unique(a[::-1, :3], axis=0, return_index=True)
+        # last occurrence of each (h, r, t): one int64 key per triple (ids < 2^21 each)
+        hi = int(a[:, :3].max()) + 1
+        if hi < (1 << 21):
+            key = (a[::-1, 0] * hi + a[::-1, 1]) * hi + a[::-1, 2]
+            _, first_rev = np.unique(key, return_index=True)
+        else:
+            _, first_rev = np.unique(a[::-1, :3], axis=0, return_index=True)
         q = a[::-1][first_rev]
         L, H = q[:, 3].astype(np.int64), q[:, 4].astype(np.int64)
         if not expectation:
@@ -214,10 +230,18 @@ class TrainerPredictor(object):
             inv = np.zeros(len(q), dtype=np.float64)
             short = (H - L) <= 256
             if short.any():
-                Ls, Hs = L[short], H[short]
-                k = np.arange(256, dtype=np.int64)
-                rk = Ls[:, None] + k[None, :]
-                inv[short] = np.where(rk < Hs[:, None], 1.0 / rk, 0.0).sum(1)
+                # direct sums over each short range, one rank position at a time over
+                # the rows still inside their range (total work = sum of range lengths)
+                idx = np.nonzero(short)[0]
+                Ls, ns = L[idx], (H - L)[idx]
+                acc = np.zeros(len(idx), dtype=np.float64)
+                act = np.nonzero(ns > 0)[0]
+                k = 0
+                while act.size:
+                    acc[act] += 1.0 / (Ls[act] + k)
+                    k += 1
+                    act = act[ns[act] > k]
+                inv[idx] = acc
             if (~short).any():
                 harm = np.concatenate([[0.0], np.cumsum(1.0 / np.arange(1, int(H.max()), dtype=np.float64))])
                 inv[~short] = harm[H[~short] - 1] - harm[L[~short] - 1]
@@ -261,7 +285,7 @@ class TrainerPredictor(object):
                 ranks = torch.cat([ranks.to(dev), torch.stack([all_h, all_r, all_t, L, H], 1).to(torch.long)])
         if self.world_size > 1:
             ranks = comm.cat(ranks.to(self.device))
-        m = self.rank_metrics(ranks.cpu().numpy().tolist(), expectation)
+        m = self.rank_metrics(ranks.cpu().numpy(), expectation)
         if comm.get_rank() == 0:
             logging.info("Data : {}".format(m["Data"]))
             logging.info("Hit1 : {:.6f}".format(m["Hit1"]))
