@@ -293,9 +293,18 @@ def main():
     if args.gpus != world:
         raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d: launch N>1 with torch.distributed.run "
                          "--nproc-per-node N" % (args.gpus, world))
+    # rehearsal of the N > 1 path on a one-GPU box (never for measurements):
+    # RNNL_BENCH_ONE_DEVICE=1 puts every rank on cuda:0, RNNL_BENCH_BACKEND=gloo
+    # replaces RCCL (which refuses two ranks on one device)
+    if os.environ.get("RNNL_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("RNNL_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     if rank == 0:
         datasets.materialize("FB15k-237", with_rotate=(args.feature == "RotatE"))
@@ -429,8 +438,9 @@ def main():
         with open(tpath) as f:
             tj = json.load(f)
         return {k.split("::")[-1].split("<")[0]: v["bytes"] for k, v in tj.get("kernels", {}).items()}
-    traffic = load_traffic(args.feature.lower())
-    gtraffic = load_traffic("bias")
+    # (the committed PMC summaries describe the one-rank workload: no traffic figure for a shard)
+    traffic = load_traffic(args.feature.lower()) if world == 1 else {}
+    gtraffic = load_traffic("bias") if world == 1 else {}
 
     # secondary lines (untimed by the driver; not `value`): the train-mode
     # forward with per-row edge removal, and the EM loop's
