@@ -535,11 +535,13 @@ def main():
     rotate_bytes = 8.0 * D * E * ((nq + 15) // 16) + 8.0 * D * nq + 4.0 * nq * E
     if ground_ms is None:  # --profile-only with the RotatE overlap: no isolated grounding time
         ground_ms = float("nan")
-    gt = [gtraffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_kernel")]
+    gt = [gtraffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_sum_memo_kernel", "memo_sum_kernel",
+                                    "score_kernel")]
     gt = sum(x for x in gt if x) or None
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-              "traffic": gt, "kernel": "ground_kernel + score_kernel", "ms": round(ground_ms, 3),
+              "traffic": gt, "kernel": "ground_kernel + scoring (score_sum_memo_kernel + memo_sum_kernel)",
+              "ms": round(ground_ms, 3),
               "measured": ground_how,
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
     if ground_ms != ground_ms:  # nan

@@ -266,6 +266,17 @@ class DeviceTrainBatches(object):
         return all_h, all_r, all_t, target, etr
 
 
+    def rows(self, idx):
+        """(all_h, all_r, all_t, edges_to_remove) of many batches at once
+        (their concatenation, in `idx` order), without the dense targets."""
+        g = self.train_set.graph
+        E = g.entity_size
+        all_h, all_r, all_t = _batch_rows(self.train_set.batches, list(idx), self.device)
+        ekey = (all_r * E + all_t) * E + all_h
+        pos = torch.searchsorted(self.edge_keys, ekey).clamp(max=max(self.edge_keys.numel() - 1, 0))
+        return all_h, all_r, all_t, self.edge_ids[pos]
+
+
 class DeviceEvalBatches(object):
     """ValidDataset / TestDataset rows built on the device:
     item `idx` equals `eval_set[idx]` — (all_h, all_r, all_t, flag), reference

@@ -348,6 +348,66 @@ class Predictor(_HipGrounding, torch.nn.Module):
         neg_score = tot[:, k].to(w.dtype) * w / torch.clamp(n_cand.to(w.dtype), min=1).unsqueeze(1)
         return torch.softmax(pos_score - neg_score, dim=-1).sum(0), rule_index
 
+    def _rule_table(self, device):
+        """Per relation its rules padded to the longest list: (R, Rmax) rule ids
+        (-1 pad) and the rules' trie-node index local to the head's root."""
+        key = ("rule_table", self._device_index(device))
+        hit = self._lin_cache.get(key)
+        if hit is not None:
+            return hit
+        nr = self.native_rules(device)
+        roots, ld = self.head_roots(device)
+        R = self.num_relations
+        rmax = max([len(self.relation2rules[q]) for q in range(R)] + [1])
+        idx = np.full((R, rmax), -1, dtype=np.int64)
+        for q in range(R):
+            ids = [i for i, _ in self.relation2rules[q]]
+            idx[q, :len(ids)] = ids
+        idx = torch.from_numpy(idx).to(device)
+        root = torch.tensor(roots, dtype=torch.int64, device=device).clamp(min=0).unsqueeze(1)
+        node = nr.node_of_rule.to(device, torch.int64)[idx.clamp(min=0)] - root
+        out = (idx, node.clamp(min=0, max=ld - 1), ld)
+        self._lin_cache[key] = out
+        return out
+
+    @torch.no_grad()
+    def compute_H_rows(self, all_h, all_r, all_t, edges_to_remove, chunk=32768):
+        """Σ over rows of compute_H's per-row softmax (predictors.py:82-119),
+        for rows of any relations in a few launches: the per-row terms are
+        independent, so the sum over the reference's batches equals the sum
+        over all their rows.  Returns (num_rules,) (rules of relations that
+        have none get 0)."""
+        device = all_h.device
+        n = all_h.numel()
+        H = torch.zeros(self.num_rules, device=device)
+        if n == 0 or self.num_rules == 0:
+            return H
+        idx, node, ld = self._rule_table(device)
+        nr = self.native_rules(device)
+        w_all = self.rule_weights.detach()
+        for s0 in range(0, n, chunk):
+            h, r, t = all_h[s0:s0 + chunk], all_r[s0:s0 + chunk], all_t[s0:s0 + chunk]
+            e = edges_to_remove[s0:s0 + chunk] if edges_to_remove is not None else None
+            m = h.numel()
+            ws, scale, n_cand = self.ground(h, r, e)
+            r = r.to(device, torch.int64).contiguous()
+            t = t.to(device, torch.int64).contiguous()
+            pos = torch.zeros((m, ld), dtype=torch.int64, device=device)
+            tot = torch.zeros((m, ld), dtype=torch.int64, device=device)
+            _native.call("rnnl_predictor_rule_stats", ws.data_ptr(), m, scale, n_cand.data_ptr(), nr.ptr,
+                         r.data_ptr(), t.data_ptr(), ld, pos.data_ptr(), tot.data_ptr(),
+                         torch.cuda.current_stream(device).cuda_stream)
+            ridx, k = idx[r], node[r]  # (m, Rmax)
+            valid = ridx >= 0
+            w = w_all[ridx.clamp(min=0)]
+            pos_score = pos.gather(1, k).to(w.dtype) * w
+            neg_score = tot.gather(1, k).to(w.dtype) * w / torch.clamp(n_cand.to(w.dtype), min=1).unsqueeze(1)
+            sm = torch.softmax((pos_score - neg_score).masked_fill(~valid, float("-inf")), dim=-1)
+            has = valid.any(1, keepdim=True)
+            sm = torch.where(valid & has, sm, torch.zeros_like(sm))
+            H.index_add_(0, ridx.clamp(min=0).reshape(-1), sm.reshape(-1))
+        return H
+
 
 class PredictorPlus(_HipGrounding, torch.nn.Module):
     """Reference src/predictors.py:121-271, forward on the HIP path."""

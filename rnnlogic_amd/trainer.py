@@ -150,9 +150,21 @@ class TrainerPredictor(object):
         """trainer.py:107-143 (the model must provide compute_H, e.g. Predictor)."""
         if comm.get_rank() == 0:
             logging.info(">>>>> Predictor: Computing H scores of rules")
-        _, dataloader = self._loader(self.train_set)
         model = self.model
         model.eval()
+        if self.device.type == "cuda" and self.device_batches and hasattr(model, "compute_H_rows"):
+            # every row of the rank's sampler batches in a few launches: the
+            # reference's per-batch H is a sum of independent per-row terms
+            sampler = torch_data.DistributedSampler(self.train_set, self.world_size, self.rank)
+            torch.empty((), dtype=torch.int64).random_()  # the reference DataLoader's base-seed draw
+            if getattr(self, "_dev_batches", None) is None:
+                self._dev_batches = DeviceTrainBatches(self.train_set, self.device)
+            h, r, t, etr = self._dev_batches.rows(list(iter(sampler)))
+            all_H_score = model.compute_H_rows(h, r, t, etr) / len(model.graph.train_facts)
+            if self.world_size > 1:
+                all_H_score = comm.stack(all_H_score).sum(0)
+            return all_H_score.data.cpu().numpy().tolist()
+        _, dataloader = self._loader(self.train_set)
         all_H_score = torch.zeros(model.num_rules, device=self.device)
         for batch_id, batch in enumerate(dataloader):
             all_h, all_r, all_t, target, edges_to_remove = [x.squeeze(0) for x in batch]
