@@ -919,20 +919,16 @@ __device__ __forceinline__ void flag_acc_range(const KParams &p) {
 template <int AGG>
 __device__ __forceinline__ float score_one(const KParams &p, const float *__restrict__ wl, const float *relb,
                                            int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
+  static_assert(AGG == RNNL_AGG_PNA, "the SUM aggregator scores in score_sum_kernel / score_sum_memo_kernel");
   using L = WL<AGG>;
-  constexpr int STRIDE = AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna;
-  long long a1[16];
-  long long a2[AGG == RNNL_AGG_PNA ? 16 : 1];
-  float mn[AGG == RNNL_AGG_PNA ? 16 : 1], mx[AGG == RNNL_AGG_PNA ? 16 : 1];
+  long long a1[16], a2[16];
+  float mn[16], mx[16];
 #pragma unroll
-  for (int d = 0; d < 16; ++d) a1[d] = 0;
-  if constexpr (AGG == RNNL_AGG_PNA) {
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a2[d] = 0;
-      mn[d] = __builtin_huge_valf();
-      mx[d] = -__builtin_huge_valf();
-    }
+  for (int d = 0; d < 16; ++d) {
+    a1[d] = 0;
+    a2[d] = 0;
+    mn[d] = __builtin_huge_valf();
+    mx[d] = -__builtin_huge_valf();
   }
   long long deg = 0;
   uint64_t fp = 0, csum = 0;
@@ -941,77 +937,72 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
     const int n = be.x;
     const long long c = (uint32_t)be.y;
     csum += (uint64_t)c;
-    const long long *rec = reinterpret_cast<const long long *>(p.node_w + (int64_t)n * STRIDE);
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStridePna);
 #pragma unroll
     for (int d = 0; d < 16; ++d) a1[d] += c * rec[d];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) a2[d] += c * rec[16 + d];
+#if !RNNL_PNA_SPLIT
+    const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      mn[d] = fminf(mn[d], fr[d]);
+      mx[d] = fmaxf(mx[d], fr[16 + d]);
+    }
+#endif
     deg += c * p.rl.node_nrules[n];
     if (dig_out) fp += (uint64_t)c * p.rl.node_fp[n];
-    if constexpr (AGG == RNNL_AGG_PNA) {
+  }
+#if RNNL_PNA_SPLIT
+  // min / max in a second walk over the entries (fewer registers live in either walk)
+  asm volatile("" ::: "memory");
+  for (int e = beg; e < beg + cnt; ++e) {
+    const float *fr = reinterpret_cast<const float *>(p.node_w + (int64_t)p.bent[e].x * kStridePna) + 32;
 #pragma unroll
-      for (int d = 0; d < 16; ++d) a2[d] += c * rec[16 + d];
-      const float *fr = reinterpret_cast<const float *>(rec + 32);
-#pragma unroll
-      for (int d = 0; d < 16; ++d) {
-        mn[d] = fminf(mn[d], fr[d]);
-        mx[d] = fmaxf(mx[d], fr[16 + d]);
-      }
+    for (int d = 0; d < 16; ++d) {
+      mn[d] = fminf(mn[d], fr[d]);
+      mx[d] = fmaxf(mx[d], fr[16 + d]);
     }
   }
+#endif
   if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
-  {
-    // records: |fix| <= 2^30 (SUM: int32), PNA: max(|sum x|, |sum x^2|) * 2^28 from the table trailer
-    double rmax = 0x1p30;
-    if constexpr (AGG == RNNL_AGG_PNA)
-      rmax = (double)__uint_as_float(reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes *
-                                                                            kStridePna)[0]) * 0x1p28 + 1.0;
-    if ((double)csum * rmax >= 0x1p63) flag_acc_range(p);
-  }
+  if (csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33 total count
 #ifdef RNNL_SCORE_NOMLP  // diagnostic build: the node-sum gather alone
   return (float)a1[0] + (float)a1[15];
 #endif
-  constexpr double inv_fix = 1.0 / (double)(1 << kFixShift);
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  const double inv1 = ldexp(1.0, -(int)trailer[1]), inv2 = ldexp(1.0, -(int)trailer[4]);
+  // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123).
+  // Each dim's four features are folded into the 16 outputs as soon as they
+  // exist (input j = (block * 16 + d) * 3 + s3; weights in LDS as [j][o]).
+  const float degf = (float)(deg + 1);
+  const float dcl = fmaxf(degf, 1e-6f);
+  const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
+  const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
   float x1[16];
-  if constexpr (AGG == RNNL_AGG_SUM) {
-    // FuncToNodeSum: Linear(16,16) on the rule-weighted sum (layers.py:68-74)
-    float f[16];
 #pragma unroll
-    for (int d = 0; d < 16; ++d) f[d] = (float)((double)a1[d] * inv_fix);
+  for (int o = 0; o < 16; ++o) x1[o] = 0.f;
 #pragma unroll
-    for (int o = 0; o < 16; ++o) {
-      float acc = 0.f;
+  for (int d = 0; d < 16; ++d) {
+    const float s = (float)((double)a1[d] * inv1);
+    const float sq = (float)((double)a2[d] * inv2);
+    const float mean = s / dcl;
+    const float sqm = sq / dcl;
+    const float fv[4] = {mean, mn[d], mx[d], sqrtf(fmaxf(sqm - mean * mean, 1e-6f))};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc = fmaf(f[i], wl[L::ADDW + o * 16 + i], acc);
-      x1[o] = acc + wl[L::ADDB + o];
-    }
-  } else {
-    // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123)
-    const float degf = (float)(deg + 1);
-    const float dcl = fmaxf(degf, 1e-6f);
-    float feat[64];
+    for (int b = 0; b < 4; ++b) {
 #pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      const float s = (float)((double)a1[d] * inv_fix);
-      const float sq = (float)((double)a2[d] * inv_fix);
-      const float mean = s / dcl;
-      const float sqm = sq / dcl;
-      feat[d] = mean;
-      feat[16 + d] = mn[d];
-      feat[32 + d] = mx[d];
-      feat[48 + d] = sqrtf(fmaxf(sqm - mean * mean, 1e-6f));
-    }
-    const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
-    const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
-#pragma unroll 1
-    for (int o = 0; o < 16; ++o) {
-      float acc = 0.f;
+      for (int s3 = 0; s3 < 3; ++s3) {
+        asm volatile("" ::: "memory");  // one input's 16 weights live at a time
+        const float v = fv[b] * sc[s3];
+        const float *w = wl + L::ADDW + ((b * 16 + d) * 3 + s3) * 16;
 #pragma unroll
-      for (int f = 0; f < 64; ++f) {
-#pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) acc = fmaf(feat[f] * sc[s3], wl[L::ADDW + o * 192 + f * 3 + s3], acc);
+        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
       }
-      x1[o] = acc + wl[L::ADDB + o];
     }
   }
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] += wl[L::ADDB + o];
   // LayerNorm(16) + ReLU (layers.py:74-75 / 124-125)
   float mu = 0.f;
 #pragma unroll
@@ -1040,8 +1031,15 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
   return out + wl[L::S1B];
 }
 
+#ifndef RNNL_PNA_SPLIT
+#define RNNL_PNA_SPLIT 0
+#endif
+#ifndef RNNL_PNA_WAVES
+#define RNNL_PNA_WAVES 1
+#endif
 template <int AGG>
-__global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__restrict__ W) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAVES, 8))) void score_kernel(
+    KParams p, const float *__restrict__ W) {
   using L = WL<AGG>;
   __shared__ __attribute__((aligned(16))) float s_w[L::N];
   __shared__ float s_relb[128];
@@ -1053,7 +1051,7 @@ __global__ __launch_bounds__(BS) void score_kernel(KParams p, const float *__res
                           p.node_w + (int64_t)p.rl.n_nodes * (AGG == RNNL_AGG_SUM ? kStrideSum : kStridePna)));
   for (int i = tid; i < L::N; i += BS) {
     float v = 0.f;
-    if (i < L::ADDB) v = W[W_ADDW + i];
+    if (i < L::ADDB) v = W[W_ADDW + (i % 16) * L::KIN + i / 16];  // add_w transposed: [input j][output o]
     else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
     else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
     else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
@@ -1609,9 +1607,8 @@ __global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
 // block (one atomic per lane on a single word serialised at ~0.5 ms).
 __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, int ld,
                                                           int agg, unsigned char *__restrict__ out) {
-  const double sc = (double)(1 << kFixShift);
   const int64_t total = (int64_t)rl.n_nodes * 16;
-  unsigned int m = 0;
+  unsigned int m = 0, m2 = 0;
   for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
        gid += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(gid >> 4), d = (int)(gid & 15);
@@ -1628,29 +1625,65 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
       reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = s1;
       m = max(m, __float_as_uint(fabsf(s1)));
     } else {
-      long long *rec = reinterpret_cast<long long *>(out + (int64_t)n * kStridePna);
-      // |x| * 2^28 must stay well inside int64 (and be finite): else flag the table
-      const bool ok = fabs((double)s1) < 0x1p30 && fabs((double)s2) < 0x1p30 && !isnan(mn) && !isnan(mx);
-      if (!ok) atomicOr(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStridePna) + 2, 1u);
-      // trailer[0]: max |record| (f32 bits) for the scoring kernels' int64 range bound
-      m = max(m, __float_as_uint(ok ? fmaxf(fabsf(s1), fabsf(s2)) : 0.f));
-      rec[d] = ok ? llrint((double)s1 * sc) : 0;
-      rec[16 + d] = ok ? llrint((double)s2 * sc) : 0;
-      float *fr = reinterpret_cast<float *>(rec + 32);
-      fr[d] = mn;
-      fr[16 + d] = mx;
+      // f32 sums for now; pna_fix_kernel turns them into int32 fixed point with
+      // one shift per column (max |sum x| bits -> trailer[0], max |sum x^2| -> trailer[3])
+      float *rec = reinterpret_cast<float *>(out + (int64_t)n * kStridePna);
+      if (isnan(mn) || isnan(mx)) atomicOr(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * kStridePna) + 2, 1u);
+      m = max(m, __float_as_uint(fabsf(s1)));
+      m2 = max(m2, __float_as_uint(fabsf(s2)));
+      rec[d] = s1;
+      rec[16 + d] = s2;
+      rec[32 + d] = mn;
+      rec[48 + d] = mx;
     }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
-  __shared__ unsigned int s_m[4];
-  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  for (int o = 32; o > 0; o >>= 1) {
+    m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+    m2 = max(m2, (unsigned int)__shfl_xor((int)m2, o, 64));
+  }
+  __shared__ unsigned int s_m[4], s_m2[4];
+  if ((threadIdx.x & 63) == 0) {
+    s_m[threadIdx.x >> 6] = m;
+    s_m2[threadIdx.x >> 6] = m2;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
+    unsigned int *trailer =
+        reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes * (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna));
     m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
-    if (m)
-      atomicMax(reinterpret_cast<unsigned int *>(out + (int64_t)rl.n_nodes *
-                                                 (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna)), m);
+    m2 = max(max(s_m2[0], s_m2[1]), max(s_m2[2], s_m2[3]));
+    if (m) atomicMax(trailer, m);
+    if (m2 && agg != RNNL_AGG_SUM) atomicMax(trailer + 3, m2);
+  }
+}
+
+// PNA records: sum x and sum x^2 to int32 fixed point, each column with its
+// own table-wide shift (as the SUM table: every value fits 2^30, so count x
+// record is exact in int64); shifts in trailer[1] / trailer[4], trailer[2]
+// flags a table that cannot be represented (or held a NaN min / max).
+__global__ void pna_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
+  unsigned int *trailer = reinterpret_cast<unsigned int *>(out + (int64_t)n_nodes * kStridePna);
+  const unsigned int b1 = trailer[0], b2 = trailer[3];
+  int e1 = 0, e2 = 0;
+  bool bad = b1 >= 0x7f800000u || b2 >= 0x7f800000u || trailer[2] != 0;
+  if (!bad && b1) frexpf(__uint_as_float(b1), &e1);
+  if (!bad && b2) frexpf(__uint_as_float(b2), &e2);
+  bad = bad || e1 > 30 || e2 > 30;
+  const int sh1 = bad ? 0 : min(30 - e1, 60), sh2 = bad ? 0 : min(30 - e2, 60);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    trailer[1] = (unsigned)sh1;
+    trailer[4] = (unsigned)sh2;
+    trailer[2] = bad ? 1u : 0u;
+  }
+  const float sc1 = ldexpf(1.f, sh1), sc2 = ldexpf(1.f, sh2);
+  const int64_t n = (int64_t)n_nodes * 32;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t node = i >> 5;
+    const int w = (int)(i & 31);
+    float *rec = reinterpret_cast<float *>(out + node * kStridePna);
+    const float f = rec[w];
+    reinterpret_cast<int *>(rec)[w] = bad ? 0 : (int)rintf(f * (w < 16 ? sc1 : sc2));
   }
 }
 
@@ -1840,12 +1873,15 @@ int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, v
   }
   const int64_t n = (int64_t)r->d.n_nodes * 16;
   unsigned char *out = static_cast<unsigned char *>(node_w);
-  RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna), 0, 16,
+  RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna), 0, 32,
                                 (hipStream_t)stream));
   if (n == 0) return RNNL_OK;
   const int bs = 256;
   hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 2048)), dim3(bs), 0,
                      (hipStream_t)stream, r->d, emb, ld, agg, out);
+  if (agg == RNNL_AGG_PNA)
+    hipLaunchKernelGGL(pna_fix_kernel, dim3((unsigned)std::min<int64_t>((2 * n + bs - 1) / bs, 4096)), dim3(bs), 0,
+                       (hipStream_t)stream, r->d.n_nodes, out);
   if (agg == RNNL_AGG_SUM)
     hipLaunchKernelGGL(node_fix_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 4096)), dim3(bs), 0,
                        (hipStream_t)stream, r->d.n_nodes, out);

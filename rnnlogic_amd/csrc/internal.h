@@ -60,8 +60,8 @@ struct RulesDev {
 // Node-weight records (bytes per node); see rnnl_node_weights.
 constexpr int kHidden = 16;
 constexpr int kStrideSum = 64;   // f32 sum x[16]
-constexpr int kStridePna = 384;  // int64 fix(sum x)[16] | int64 fix(sum x^2)[16] | f32 min[16] | f32 max[16]
-constexpr int kFixShift = 28;    // fix(v) = round(v * 2^28)
+constexpr int kStridePna = 256;  // int32 fix(sum x)[16] | int32 fix(sum x^2)[16] | f32 min[16] | f32 max[16]
+                                 // (one shift per table and column: trailer[1], trailer[4])
 
 void set_error(const std::string &msg);
 
