@@ -1137,6 +1137,55 @@ __host__ __device__ inline int64_t sum_stage_bytes(int max_leaves, int max_head_
   return (int64_t)max_leaves * (64 + 4 + 8) + (int64_t)max_head_nodes * 2 + 64;
 }
 
+#ifndef RNNL_MAC
+#define RNNL_MAC 2  // count x record MAC: 0 C++ int64, 1 v_mad_i64_i32, 2 exact fp64 (default; measured fastest)
+#endif
+#if RNNL_MAC == 2
+// The candidate's exact feature sums in fp64: with |record| < 2^30 every
+// count x record product below 2^53 is an exact double and so is every
+// partial sum while sum(count) < 2^23, so accd equals the int64 sum bit for
+// bit (one v_cvt_f64_i32 + one v_fma_f64 per element instead of two 64-bit
+// integer multiply-adds and their fix-ups); a candidate whose counts sum
+// past that takes the int64 walk below.
+template <bool STAGED, bool DIGEST>
+__device__ __forceinline__ void gather_sum_int64(const KParams &p, const SumStage &st, int root, int beg, int cnt,
+                                                 float inv_scale, float f[16], long long &deg, uint64_t &fp);
+template <bool STAGED, bool DIGEST>
+__device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st, int root, int beg, int cnt,
+                                           float inv_scale, float f[16], long long &deg, uint64_t &fp) {
+  if constexpr (STAGED) {  // the LDS-staged variant keeps the int64 walk
+    gather_sum_int64<STAGED, DIGEST>(p, st, root, beg, cnt, inv_scale, f, deg, fp);
+    return;
+  }
+  double accd[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) accd[d] = 0.0;
+  deg = 0;
+  fp = 0;
+  uint64_t csum = 0;
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const uint32_t cu = (uint32_t)be.y;
+    csum += cu;
+    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const double cd = (double)cu;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) accd[d] = fma(cd, (double)x[d], accd[d]);
+    if constexpr (DIGEST) {
+      deg += (long long)cu * p.rl.node_nrules[n];
+      fp += (uint64_t)cu * p.rl.node_fp[n];
+    }
+  }
+  if (csum >= (1ull << 23)) {  // rare: the exact int64 walk
+    gather_sum_int64<STAGED, DIGEST>(p, st, root, beg, cnt, inv_scale, f, deg, fp);
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 16; ++d) f[d] = (float)(accd[d] * (double)inv_scale);
+}
+#define gather_sum gather_sum_int64
+#endif
 template <bool STAGED, bool DIGEST>
 __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st, int root, int beg, int cnt,
                                            float inv_scale, float f[16], long long &deg, uint64_t &fp) {
@@ -1176,6 +1225,20 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
     }
     // (the compiler folds the two forms into the uint32 one: two v_mad_u64_u32
     // per element; an explicit v_mad_i64_i32 measured slower, 16.2 -> 16.6 ms)
+#if RNNL_MAC == 1
+    if (cu < 0x80000000u) {
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        long long r;
+        unsigned long long carry;
+        asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"((int)cu), "v"(x[d]), "v"(acc[d]));
+        acc[d] = r;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 16; ++d) acc[d] += c * x[d];
+    }
+#else
     if (cu < 0x80000000u) {
       const int ci = (int)cu;
 #pragma unroll
@@ -1184,6 +1247,7 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
 #pragma unroll
       for (int d = 0; d < 16; ++d) acc[d] += c * x[d];
     }
+#endif
     deg += c * nr;
     fp += (uint64_t)c * nf;
   }
@@ -1191,6 +1255,9 @@ __device__ __forceinline__ void gather_sum(const KParams &p, const SumStage &st,
 #pragma unroll
   for (int d = 0; d < 16; ++d) f[d] = (float)((double)acc[d] * (double)inv_scale);
 }
+#if RNNL_MAC == 2
+#undef gather_sum
+#endif
 
 // The feature of a candidate whose only bucket entry is (n, c): gather_sum's
 // arithmetic for that single entry (the memo of score_sum_memo_kernel).
