@@ -71,15 +71,39 @@ int rnnl_graph_create(const int32_t *hrt, int64_t n, int32_t E, int32_t R, rnnl_
     esrc[e] = h;
     edst[e] = t;
   }
+  // compact per-vertex relation bitmaps + dense offsets (see GraphDev)
+  const int W = (R + 31) / 32;
+  std::vector<uint2> vbits((size_t)E * W);
+  std::vector<int32_t> dvoff;
+  dvoff.reserve((size_t)E + (size_t)n + 1);
+  for (int64_t v = 0; v < E; ++v) {
+    for (int w = 0; w < W; ++w) {
+      uint32_t bits = 0;
+      const uint32_t first = (uint32_t)dvoff.size();
+      for (int b = 0; b < 32; ++b) {
+        const int64_t r = (int64_t)w * 32 + b;
+        if (r >= R) break;
+        const int64_t o = v * R + r;
+        if (off[o + 1] > off[o]) {
+          bits |= 1u << b;
+          dvoff.push_back(off[o]);
+        }
+      }
+      vbits[(size_t)v * W + w] = make_uint2(bits, first);
+    }
+    dvoff.push_back(off[(v + 1) * R]);  // end of v's edges: the last present relation's end
+  }
   auto *g = new rnnl_graph_s;
   (void)hipGetDevice(&g->device);
   g->d.E = E;
   g->d.R = R;
+  g->d.W = W;
   g->d.n_edges = n;
   int rc = RNNL_OK;
   if ((rc = upload(off, &g->mem[0], &g->d.off)) || (rc = upload(col, &g->mem[1], &g->d.col)) ||
       (rc = upload(ebase, &g->mem[2], &g->d.edge_base)) || (rc = upload(esrc, &g->mem[3], &g->d.edge_src)) ||
-      (rc = upload(edst, &g->mem[4], &g->d.edge_dst))) {
+      (rc = upload(edst, &g->mem[4], &g->d.edge_dst)) || (rc = upload(vbits, &g->mem[5], &g->d.vbits)) ||
+      (rc = upload(dvoff, &g->mem[6], &g->d.dvoff))) {
     rnnl_graph_destroy(g);
     return rc;
   }

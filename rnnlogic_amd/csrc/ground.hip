@@ -52,6 +52,9 @@ constexpr int EPT = RNNL_EPT;  // phase-A edges per lane per pass
 #ifndef RNNL_WG_PER_CU
 #define RNNL_WG_PER_CU 3
 #endif
+#ifndef RNNL_CSR_COMPACT
+#define RNNL_CSR_COMPACT 1  // (v, rel) edge ranges from the compact per-vertex view (0: the E x R offsets)
+#endif
 constexpr int HBITS = RNNL_HBITS;
 constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count)
 constexpr int WBITS = RNNL_WBITS;  // phase-B entity window: WIN entities
@@ -401,9 +404,21 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
           const int4 ci = p.rl.node_info[child];
           const int rel = ci.x;
           const int v = S.ent_v[ent];
+#if RNNL_CSR_COMPACT
+          // the (v, rel) edge range from v's relation bitmap word + the dense offsets (L2-sized)
+          const uint2 vb = p.g.vbits[(int64_t)v * p.g.W + (rel >> 5)];
+          const uint32_t bit = 1u << (rel & 31);
+          int beg = 0;
+          if (vb.x & bit) {
+            const int pos = (int)vb.y + __popc(vb.x & (bit - 1u));
+            beg = p.g.dvoff[pos];
+            deg = p.g.dvoff[pos + 1] - beg;
+          }
+#else
           const int64_t o = (int64_t)v * R + rel;
           const int beg = p.g.off[o];
           deg = p.g.off[o + 1] - beg;
+#endif
           S.it_child[tid] = child;
           S.it_beg[tid] = beg;
           S.it_c[tid] = S.ent_c[ent];

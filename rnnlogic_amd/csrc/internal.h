@@ -18,6 +18,14 @@ struct GraphDev {
   int64_t n_edges = 0;
   const int32_t *off = nullptr;        // E*R + 1
   const int32_t *col = nullptr;        // n_edges
+  // compact per-vertex view of off (L2-sized): for vertex v and relation word
+  // w = rel >> 5, vbits[v * W + w] = (bitmap of v's relations with edges in
+  // that word, index into dvoff of the word's first present relation); the
+  // edges of (v, rel) are col[dvoff[pos] .. dvoff[pos + 1]) with
+  // pos = .y + popcount(.x below rel's bit)
+  int32_t W = 0;
+  const uint2 *vbits = nullptr;        // E * W
+  const int32_t *dvoff = nullptr;      // sum over v of (present relations + 1)
   const int32_t *edge_base = nullptr;  // R + 1: start of relation r's edge table
   const int32_t *edge_src = nullptr;   // relation-major, relation-local file order
   const int32_t *edge_dst = nullptr;
@@ -70,7 +78,7 @@ void set_error(const std::string &msg);
 struct rnnl_graph_s {
   rnnl::GraphDev d;
   int device = 0;
-  void *mem[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  void *mem[7] = {};
 };
 
 struct rnnl_rules_s {
