@@ -257,6 +257,39 @@ def wn18rr_line(dev, reps=5):
                         "rnnlogic_rules.txt (L<=5); seeded synthetic train graph and RotatE tables"}
 
 
+def kinship_line(dev, reps=10):
+    """Config 2 of BASELINE.json as a secondary line: PredictorPlus(lstm, 3,
+    16, sum) without an entity feature on the kinship test split (178 batches,
+    5,343 queries; the mined L <= 3 rule file, top 100 per relation: 2,500
+    rules), real kinship train graph — the same timed step as `value`."""
+    path = datasets.materialize("kinship")
+    random.seed(1)
+    np.random.seed(1)
+    torch.manual_seed(1)
+    with contextlib.redirect_stdout(sys.stderr):
+        graph = KnowledgeGraph(path)
+        TrainDataset(graph, 32)
+        ValidDataset(graph, 32)
+        test_set = TestDataset(graph, 32)
+        model = PredictorPlus(graph, type="lstm", num_layers=3, hidden_dim=16, entity_feature="none",
+                              aggregator="sum")
+        model.set_rules(datasets.rule_file("kinship"))
+    model = model.to(dev).eval()
+    rows = np.asarray([x for b in test_set.batches for x in b], dtype=np.int64)
+    h = torch.from_numpy(np.ascontiguousarray(rows[:, 0])).to(dev)
+    r = torch.from_numpy(np.ascontiguousarray(rows[:, 1])).to(dev)
+
+    def step():
+        model.invalidate_cache()
+        with torch.no_grad():
+            return model.forward_rows(h, r, None)
+    sec = time_forward(step, reps)
+    return {"queries_per_s": round(len(rows) / sec, 1), "ms_per_step": round(sec * 1e3, 3), "rows": len(rows),
+            "batches": len(test_set), "rules": model.num_rules,
+            "workload": "kinship test split, PredictorPlus(lstm,3,16,sum), entity_feature none; mined rules "
+                        "(L<=3, top 100 per relation); real train graph"}
+
+
 def algorithmic_work(model, graph, rows, threads):
     """Exact per-rule work counts of the SURVEY §8(d) formula: F (frontier
     expansions), T (edge traversals), P ((rule, dest) pairs) and C
@@ -480,6 +513,7 @@ def main():
                                          "rows": nq, "note": "Predictor(bias) over the test split, same rules"}
         del pred
         extra["wn18rr_forward"] = wn18rr_line(dev)
+        extra["kinship_forward"] = kinship_line(dev)
         # end-to-end evaluate('test') (trainer.py:145-248): device rows + filter
         # flags, one forward over the split, device ranks, host metrics
         from rnnlogic_amd.trainer import TrainerPredictor
