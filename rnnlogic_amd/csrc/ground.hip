@@ -1046,8 +1046,178 @@ __device__ __forceinline__ float score_one(const KParams &p, const float *__rest
   return out + wl[L::S1B];
 }
 
+// Exact int64 sums of count x record word (off + d) over a candidate's bucket
+// entries, one dim at a time (few registers), as the double the one-walk
+// score_one converts them to: the fallback of score_one_2walk's fp64 sums.
+__device__ __forceinline__ void exact_sums(const KParams &p, int beg, int cnt, int off, double (&a)[16]) {
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    long long acc = 0;
+#pragma unroll 1
+    for (int e = beg; e < beg + cnt; ++e) {
+      const int2 be = p.bent[e];
+      acc += (long long)(uint32_t)be.y * reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna)[off + d];
+    }
+    a[d] = (double)acc;
+  }
+}
+
+// Two walks over the candidate's bucket entries, one per half of the node
+// record, each folding its features into the Linear(192, 16) sums as soon
+// as it ends: walk 1 the mean and min features (Σ c·x, min), walk 2 the max
+// and std ones (Σ c·x², max; std from walk 1's means).  Only one half's
+// accumulators (16 int64 + 16 float) and the 16 sums and 16 means are live
+// in either walk instead of both halves' (the one-walk score_one holds ~250
+// VGPRs, 2 waves/SIMD); the entries are read twice (the second walk's loads
+// hit L2).  Same arithmetic per feature as score_one; only the order in
+// which the 192 inputs are summed into the 16 outputs differs.
+// Materialise the 16 sums here, and keep later loads below: the FMAs of one
+// Linear input complete before the next input's weights are read (a plain
+// memory clobber orders the loads but lets the scheduler hoist all of them
+// ahead of the FMAs, which spills).
+__device__ __forceinline__ void pin16(float (&x)[16]) {
+  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+               "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
+               :
+               : "memory");
+}
+
+template <int AGG>
+__device__ __forceinline__ float score_one_2walk(const KParams &p, const float *wl, const float *relb,
+                                                 int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
+  static_assert(AGG == RNNL_AGG_PNA, "the SUM aggregator scores in score_sum_kernel / score_sum_memo_kernel");
+  using L = WL<AGG>;
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  double a[16];  // exact: see the walk
+  float m[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    a[d] = 0;
+    m[d] = __builtin_huge_valf();
+  }
+  long long deg = 0;
+  uint64_t fp = 0, csum = 0;
+#pragma unroll 1
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const long long c = (uint32_t)be.y;
+    const double cd = (double)(uint32_t)be.y;
+    csum += (uint64_t)c;
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStridePna);
+    const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] = fma(cd, (double)rec[d], a[d]);
+      m[d] = fminf(m[d], fr[d]);
+    }
+    deg += c * p.rl.node_nrules[n];
+    if (dig_out) fp += (uint64_t)c * p.rl.node_fp[n];
+  }
+  if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+  if (csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33 total count
+  // |record| < 2^30, so below a total count of 2^23 every product and partial
+  // sum is an integer under 2^53 and the fp64 FMAs are exact: a[d] is the
+  // int64 sum itself.  Past it (rare), exact int64 sums one dim at a time.
+  if (csum >> 23) exact_sums(p, beg, cnt, 0, a);
+  const double inv1 = ldexp(1.0, -(int)trailer[1]);
+  // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123);
+  // input j = (block * 16 + d) * 3 + s3, weights in LDS as [j][o]
+  const float degf = (float)(deg + 1);
+  const float dcl = fmaxf(degf, 1e-6f);
+  const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
+  const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
+  float x1[16], mean[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float s = (float)(a[d] * inv1);
+    mean[d] = s / dcl;
+    const float fv[2] = {mean[d], m[d]};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) {
+        pin16(x1);  // one input's 16 weights live at a time: its FMAs end before the next loads
+        const float v = fv[b] * sc[s3];
+        const float *w = wl + L::ADDW + ((b * 16 + d) * 3 + s3) * 16;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
+      }
+    }
+  }
+  // walk 2: the squared half of the records and the max
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    a[d] = 0;
+    m[d] = -__builtin_huge_valf();
+  }
+  asm volatile("" ::: "memory");
+#pragma unroll 1
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const double cd = (double)(uint32_t)be.y;
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna);
+    const float *fr = reinterpret_cast<const float *>(rec + 48);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] = fma(cd, (double)rec[16 + d], a[d]);
+      m[d] = fmaxf(m[d], fr[d]);
+    }
+  }
+  if (csum >> 23) exact_sums(p, beg, cnt, 16, a);
+  const double inv2 = ldexp(1.0, -(int)trailer[4]);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float sq = (float)(a[d] * inv2);
+    const float sqm = sq / dcl;
+    const float fv[2] = {m[d], sqrtf(fmaxf(sqm - mean[d] * mean[d], 1e-6f))};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) {
+        pin16(x1);  // one input's 16 weights live at a time: its FMAs end before the next loads
+        const float v = fv[b] * sc[s3];
+        const float *w = wl + L::ADDW + (((b + 2) * 16 + d) * 3 + s3) * 16;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] += wl[L::ADDB + o];
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+  float out = 0.f;
+#pragma unroll 2
+  for (int o = 0; o < 128; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], wl[L::S0X + o * 16 + i], acc);
+    acc = fmaxf(acc + relb[o], 0.f);
+    out = fmaf(acc, wl[L::S1W + o], out);
+  }
+  return out + wl[L::S1B];
+}
+
 #ifndef RNNL_PNA_SPLIT
 #define RNNL_PNA_SPLIT 0
+#endif
+#ifndef RNNL_PNA_2WALK
+#define RNNL_PNA_2WALK 1
 #endif
 #ifndef RNNL_PNA_WAVES
 #define RNNL_PNA_WAVES 1
@@ -1107,8 +1277,12 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
       // keep the loop-invariant LDS weight reads inside the loop (hoisted,
       // they would pin ~200 VGPRs and starve occupancy)
       asm volatile("" ::: "memory");
+#if RNNL_PNA_2WALK
+      const float out = score_one_2walk<AGG>(p, s_w, s_relb, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t);
+#else
       const float out = score_one<AGG>(p, s_w, s_relb, cr.y, cr.z, ms,
                                        p.digest ? &dg : nullptr, t);
+#endif
       if (p.digest) atomicAdd(&s_dig, (unsigned long long)dg);
       if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
         p.cand_out[qb + s] = out;

@@ -79,8 +79,12 @@ def test_path_count_at_2_32_fails_loudly(tmp_path, dev):
 
 
 @pytest.mark.parametrize("aggregator", ["sum", "pna"])
-def test_path_count_above_2_31_matches_oracle(tmp_path, dev, aggregator):
-    path, rules = chain_graph(tmp_path, 255)  # 255^4 = 4.23e9 paths: above 2^31, below 2^32
+@pytest.mark.parametrize("m,w5", [(255, 1), (100, 3)])
+def test_path_count_above_2_31_matches_oracle(tmp_path, dev, aggregator, m, w5):
+    # (255, 1): 255^4 = 4.23e9 paths, above 2^31, below 2^32; (100, 3): three
+    # entries of 1e8 at e6 — both past the 2^23 total count below which the
+    # scoring kernels' fp64 feature sums are exact (their int64 fallback)
+    path, rules = chain_graph(tmp_path, m, w5)
     graph = KnowledgeGraph(path)
     model = _emb_model(graph, rules, dev, aggregator)
     with torch.no_grad():
@@ -94,7 +98,7 @@ def test_path_count_above_2_31_matches_oracle(tmp_path, dev, aggregator):
     np.testing.assert_allclose(score.cpu().numpy(), want, atol=1e-4, rtol=1e-5)
     # the training path's COO carries the same u32 count (not a negative int32)
     row, ent, ce, node, count = model.ground_coo(torch.tensor([0], device=dev), torch.tensor([0], device=dev))
-    assert ent.tolist() == [graph.entity_size - 1] and count.tolist() == [255 ** 4]
+    assert sorted(set(ent.tolist())) == [graph.entity_size - 1] and count.tolist() == [m ** 4] * w5
 
 
 @pytest.mark.parametrize("aggregator", ["sum", "pna"])
