@@ -1121,6 +1121,31 @@ __device__ __forceinline__ float score_one_2walk(const KParams &p, const float *
   // int64 sum itself.  Past it (rare), exact int64 sums one dim at a time.
   if (csum >> 23) exact_sums(p, beg, cnt, 0, a);
   const double inv1 = ldexp(1.0, -(int)trailer[1]);
+#ifdef RNNL_SCORE_NOMLP  // diagnostic build: the two walks without the Linear / MLP
+  {
+    float z = (float)deg;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) z += (float)(a[d] * inv1) + m[d];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] = 0;
+      m[d] = -__builtin_huge_valf();
+    }
+    for (int e = beg; e < beg + cnt; ++e) {
+      const int2 be = p.bent[e];
+      const double cd = (double)(uint32_t)be.y;
+      const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        a[d] = fma(cd, (double)rec[16 + d], a[d]);
+        m[d] = fmaxf(m[d], reinterpret_cast<const float *>(rec + 48)[d]);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 16; ++d) z += (float)a[d] + m[d];
+    return z * wl[L::S1B];
+  }
+#endif
   // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123);
   // input j = (block * 16 + d) * 3 + s3, weights in LDS as [j][o]
   const float degf = (float)(deg + 1);

@@ -473,8 +473,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # floor).  The grounding beside RotatE runs one workgroup per CU
         # (measured 88.1 vs 91.1 ms/step at full occupancy): it finishes in
         # ~18 ms, well inside the RotatE launch.
+        # The scoring pass beside RotatE runs 512 workgroups (2 per CU): FB15k-237
+        # 83.4-84.0 ms/step for 256-1024 vs 84.4-84.6 at full occupancy
+        # (tools/ab_env.sh, RNNL_OVERLAP_SCORE_WG).
         self.overlap_ground_wg = int(os.environ.get("RNNL_OVERLAP_GROUND_WG", "256"))
-        self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "0"))
+        self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "512"))
         # sum aggregator: the scoring pass also runs beside RotatE, writing its
         # per-candidate outputs to the workspace; a short apply pass adds them
         # into the finished RotatE rows (rnnl_predictorplus_apply)
