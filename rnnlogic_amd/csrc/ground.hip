@@ -102,7 +102,10 @@ struct WL {
 };
 
 // Per-slot scratch (entries), scaled by capacity_scale.
-constexpr int64_t FCAP_BASE = 1 << 16;  // frontier list (and window-sorted contributions)
+#ifndef RNNL_FCAP_BITS
+#define RNNL_FCAP_BITS 16
+#endif
+constexpr int64_t FCAP_BASE = 1 << RNNL_FCAP_BITS;  // frontier list (and window-sorted contributions)
 constexpr int64_t PCAP_BASE = 1 << 16;  // contributions of one query
 static_assert(FCAP_BASE >= PCAP_BASE, "phase B sorts contributions into the frontier buffer");
 constexpr int64_t POOL_PER_QUERY = 8192;  // global bucket pool entries per query (x scale)
