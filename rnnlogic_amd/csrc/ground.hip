@@ -74,12 +74,12 @@ constexpr int EMPTY = -1;
 constexpr int SORT_WORDS = (9 * GBS * 4 / 6) & ~(GBS - 1);
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
-enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5 };
+enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6 };
 // H_ERRBITS: 4 watchdog, 8 a path count or PNA degree reached 2^32 (the u32
 // sums would wrap), 16 the node-weight table is out of its fixed-point range
 // (a non-finite aggregate, or |sum| >= 2^30), 32 a candidate's counts sum past
 // the exact int64 feature sums.  8, 16 and 32 -> RNNL_ERR_RANGE.
-enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16, ERR_ACC_RANGE = 32 };
+enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16, ERR_ACC_RANGE = 32, ERR_CHUNKS = 64 };
 constexpr int HDR_WORDS_BYTES = 256;
 
 // Packed MLP weights (written by pack_weights_kernel behind the header).
@@ -137,6 +137,8 @@ struct KParams {
                      // (the first n_cand entries of a query's run)
   int2 *bent;        // bucket entries: (trie node, path count bits)
   float *memo;       // SUM: score_model output of a candidate reached by one path of one leaf node
+  int2 *chunks;      // PNA: scoring work units (query, first candidate) of <= 64 candidates each
+  int64_t chunk_cap;
   unsigned long long *prof;  // diagnostic phase cycle counters (nullable)
 };
 
@@ -184,7 +186,7 @@ __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, in
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
-  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, off_memo, total;
+  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, off_chunk, chunk_cap, off_memo, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -214,6 +216,10 @@ static Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   o += 4 * L.pool_cap;
   L.off_slots = o = align256(o);
   o += L.nslots * slot_bytes(L.fcap, L.pcap);
+  // PNA scoring chunks: sum over queries of ceil(candidates / 64) <= nq + pool_cap / 64
+  L.chunk_cap = std::max<int64_t>(nq, 1) + L.pool_cap / 64 + 1;
+  L.off_chunk = o = align256(o);
+  o += 8 * L.chunk_cap;
   L.off_memo = o = align256(o);
   o += 4 * n_nodes;
   L.total = o;
@@ -304,7 +310,7 @@ struct __align__(16) Smem {
   };
   int ws[GNW + 1];
   int q, nd, np, ovf, err, root;
-  long long qbase;
+  long long qbase, cbase;
   unsigned long long t0;
   int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
   unsigned long long sumlog;
@@ -887,6 +893,20 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
     }
     const int ncand = candidates_phase(p, S, sl, P, false, sorted);
     __syncthreads();  // S.err: a PNA degree may have hit 2^32 in phase B
+    if constexpr (AGG == RNNL_AGG_PNA) {
+      // the query's scoring work units: one per 64 candidates (score_pna_chunk_kernel
+      // balances them over waves, so one large query no longer sets the kernel's tail)
+      const int nck = (ncand + 63) >> 6;
+      if (tid == 0 && !S.err) {
+        const unsigned long long b = atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_CHUNKS),
+                                               (unsigned long long)nck);
+        if (b + nck > (unsigned long long)p.chunk_cap) S.err |= ERR_CHUNKS;  // cannot happen: chunk_cap bounds the sum
+        S.cbase = (long long)b;
+      }
+      __syncthreads();
+      if (!S.err)
+        for (int k = tid; k < nck; k += GBS) p.chunks[S.cbase + k] = make_int2(q, k << 6);
+    }
     if (tid == 0 && S.err) {
       flag_error(p, hdr, S, q);
     } else if (tid == 0) {
@@ -1325,6 +1345,87 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
     }
     __syncthreads();
     if (tid == 0 && p.digest) p.digest[q] = s_dig;
+  }
+}
+
+// PNA scoring over chunks (default; RNNL_PNA_CHUNKED=0 keeps score_kernel<PNA>).
+// The unit of work is one wave x one chunk of <= 64 consecutive candidates of
+// one query (lane = candidate), listed by the grounding kernel in
+// p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue chunks independently, so a
+// query with 17k candidates (WN18RR) is spread over ~280 waves instead of
+// holding one workgroup while the rest of the grid drains; no workgroup
+// barrier per query.  Each wave folds its relation's half of
+// score_model.layers.0 into its own LDS slice when the relation changes.
+// Same arithmetic per candidate as score_kernel<PNA> (score_one_2walk).
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAVES, 8))) void score_pna_chunk_kernel(
+    KParams p, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_PNA>;
+  __shared__ __attribute__((aligned(16))) float s_w[L::N];
+  __shared__ float s_relb[BS / 64][128];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna));
+  for (int i = tid; i < L::N; i += BS) {
+    float v = 0.f;
+    if (i < L::ADDB) v = W[W_ADDW + (i % 16) * L::KIN + i / 16];  // add_w transposed: [input j][output o]
+    else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
+    else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
+    else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
+    else if (i < L::S1W) v = W[W_S0X + i - L::S0X];
+    else if (i < L::S1B) v = W[W_S1W + i - L::S1W];
+    else if (i == L::S1B) v = W[W_S1B];
+    s_w[i] = v;
+  }
+  __syncthreads();  // the only workgroup barrier: waves run independently from here
+  const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
+  float *relb = s_relb[wv];
+  int cur_r = -1;
+#pragma unroll 1
+  while (true) {
+    unsigned c = 0;
+    if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    if ((long long)c >= nchunks) break;
+    const int2 ck = p.chunks[c];
+    const int q = __builtin_amdgcn_readfirstlane(ck.x);
+    const int s0 = __builtin_amdgcn_readfirstlane(ck.y);
+    const int r = __builtin_amdgcn_readfirstlane((int)p.all_r[q]);
+    if (r != cur_r) {
+      // relation half of score_model.layers.0 folded into a per-wave bias
+      __builtin_amdgcn_wave_barrier();  // the previous chunk's reads of the slice are done
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = lane + 64 * j;
+        float acc = p.s0_b[o];
+        for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+        relb[o] = acc;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      cur_r = r;
+    }
+    const int nc = p.n_cand[q];
+    const int s = s0 + lane;
+    if (s >= nc) continue;
+    const int64_t qb = p.q_base[q];
+    const float ms = p.q_scale[q];
+    const int4 cr = p.cand[qb + s];
+    const int t = cr.x;
+    uint64_t dg = 0;
+    asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop (see score_kernel)
+    const float out = score_one_2walk<RNNL_AGG_PNA>(p, s_w, relb, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t);
+    if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
+    if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
+      p.cand_out[qb + s] = out;
+      continue;
+    }
+    const int64_t idx = (int64_t)q * p.g.E + t;
+    if (p.feature == RNNL_FEATURE_NONE)
+      p.score[idx] = out;
+    else
+      p.score[idx] = out + (p.base_row ? p.base_row[t] : p.score[idx]);
+    if (p.mask) p.mask[idx] = 1;
   }
 }
 
@@ -2243,6 +2344,8 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
   p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
   p.bent = reinterpret_cast<int2 *>(base + Ly.off_bent);
   p.memo = reinterpret_cast<float *>(base + Ly.off_memo);
+  p.chunks = reinterpret_cast<int2 *>(base + Ly.off_chunk);
+  p.chunk_cap = Ly.chunk_cap;
   p.prof = g_prof;
   return RNNL_OK;
 }
@@ -2287,6 +2390,15 @@ static bool score_memo_enabled() {
   return on;
 }
 
+// RNNL_PNA_CHUNKED=0 selects the per-query PNA scoring kernel (A/B)
+static bool pna_chunked() {
+  static const bool on = [] {
+    const char *e = getenv("RNNL_PNA_CHUNKED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int grid = 0) {
   const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
@@ -2316,6 +2428,11 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int gri
       hipLaunchKernelGGL((score_sum_kernel<false, true>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
     else
       hipLaunchKernelGGL((score_sum_kernel<false, false>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
+  } else if (pna_chunked()) {
+    // per-query digests are sums over the query's chunks
+    if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);
+    const unsigned score_grid = (unsigned)(grid > 0 ? grid : NUM_CU * 8);
+    hipLaunchKernelGGL(score_pna_chunk_kernel, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
   } else {
     const unsigned score_grid = (unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8);
     hipLaunchKernelGGL(score_kernel<RNNL_AGG_PNA>, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
@@ -2581,8 +2698,8 @@ int rnnl_forward_status(void *ws, void *stream) {
       set_error(msg);
       return RNNL_ERR_RANGE;
     }
-    set_error("rnnl_predictorplus_forward: internal error bits 0x" + std::to_string(bits) +
-              " (4: watchdog) at query " + std::to_string(st[H_ERRQ]));
+    set_error("rnnl_predictorplus_forward: internal error bits " + std::to_string(bits) +
+              " (4: watchdog, 64: scoring chunk table) at query " + std::to_string(st[H_ERRQ]));
     return RNNL_ERR_INTERNAL;
   }
   if (st[H_STATUS] & 1u) {
