@@ -1,0 +1,30 @@
+#!/bin/bash
+# A/B of one environment switch over the bench lines (GPU box, repo root):
+#   VAR=RNNL_LPT VALS="0 1" LINES="bias wn rotate" bash tools/env_ab.sh
+# optional GPU tests first (TESTS=1).  Two runs per value, interleaved.
+set -o pipefail
+o=gpurun_out/${TAG:-envab}; mkdir -p $o
+export TMPDIR=/tmp
+if [ -n "$TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $o/pytest_gpu.log 2>&1 || { tail -40 $o/pytest_gpu.log; exit 1; }
+  tail -1 $o/pytest_gpu.log
+fi
+for rep in 1 2; do
+for v in ${VALS:-0 1}; do
+  for l in ${LINES:-bias wn rotate}; do
+    f=$o/${l}_${v}_$rep.log
+    case $l in
+      bias) env $VAR=$v timeout -k 10 300 python -u bench.py --feature bias --no-cpu-baseline --profile-only > $f 2> $f.err ;;
+      rotate) env $VAR=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --profile-only > $f 2> $f.err ;;
+      wn) env $VAR=$v timeout -k 10 300 python -u tools/wn_profile.py > $f 2> $f.err ;;
+    esac || { tail -20 $f.err; exit 1; }
+    python - "$f" "$l" "$VAR=$v" <<'PY'
+import ast, json, sys
+f, l, tag = sys.argv[1:]
+txt = open(f).read().strip().splitlines()[-1]
+d = json.loads(txt) if txt.startswith("{\"") else ast.literal_eval(txt)
+print(tag, l, d["ms_per_step"], d.get("kernels_ms"))
+PY
+  done
+done
+done
