@@ -893,9 +893,10 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
     }
     const int ncand = candidates_phase(p, S, sl, P, false, sorted);
     __syncthreads();  // S.err: a PNA degree may have hit 2^32 in phase B
-    if constexpr (AGG == RNNL_AGG_PNA) {
-      // the query's scoring work units: one per 64 candidates (score_pna_chunk_kernel
-      // balances them over waves, so one large query no longer sets the kernel's tail)
+    {
+      // the query's scoring work units: one per 64 candidates (score_pna_chunk_kernel /
+      // score_sum_chunk_kernel balance them over waves, so one large query no longer
+      // sets the kernel's tail)
       const int nck = (ncand + 63) >> 6;
       if (tid == 0 && !S.err) {
         const unsigned long long b = atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_CHUNKS),
@@ -1357,6 +1358,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
 // barrier per query.  Each wave folds its relation's half of
 // score_model.layers.0 into its own LDS slice when the relation changes.
 // Same arithmetic per candidate as score_kernel<PNA> (score_one_2walk).
+#ifndef RNNL_PNA_CK
+#define RNNL_PNA_CK 1
+#endif
+constexpr int PNA_CK = RNNL_PNA_CK;  // chunks per dequeue
+
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAVES, 8))) void score_pna_chunk_kernel(
     KParams p, const float *__restrict__ W) {
   using L = WL<RNNL_AGG_PNA>;
@@ -1380,11 +1386,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
   float *relb = s_relb[wv];
   int cur_r = -1;
+  unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
 #pragma unroll 1
-  while (true) {
-    unsigned c = 0;
-    if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], 1u);
-    c = __builtin_amdgcn_readfirstlane(c);
+  for (;; ++c) {
+    if (c == cend) {
+      if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], (unsigned)PNA_CK);
+      c = __builtin_amdgcn_readfirstlane(c);
+      cend = c + PNA_CK;
+    }
     if ((long long)c >= nchunks) break;
     const int2 ck = p.chunks[c];
     const int q = __builtin_amdgcn_readfirstlane(ck.x);
@@ -1943,6 +1952,138 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
   }
 }
 
+// SUM scoring over chunks (default; RNNL_SUM_CHUNKED=0 keeps
+// score_sum_memo_kernel): one wave x one 64-candidate chunk of one query at a
+// time (p.chunks, listed by the grounding kernel in completion order), no
+// workgroup barrier after the weight load.  Single-path candidates take the
+// memo (three loads and the store); the others are compacted (ballot + prefix)
+// into the wave's LDS queue of (query, pool index) and scored 64 at a time by
+// the full gather + MLP, so the MLP runs on full waves; the queue is flushed
+// early only when the next chunk's relation differs (the folded relation bias
+// is per wave) and at the end.  Same arithmetic per candidate as
+// score_sum_memo_kernel.
+template <bool DIGEST>
+__device__ __forceinline__ void sum_chunk_flush(const KParams &p, const float *s_w, const float *relb,
+                                                const int2 *queue, int m, float inv_scale) {
+  const int lane = threadIdx.x & 63;
+  if (lane < m) {
+    const int2 it = queue[lane];
+    const int4 cr = p.cand[it.y];
+    const float base = sum_base(p, it.x, cr.x);  // issued before the gather: its latency hides under it
+    float f[16];
+    long long deg;
+    uint64_t fp;
+    SumStage st{};
+    gather_sum<false, DIGEST>(p, st, 0, cr.y, cr.z, inv_scale, f, deg, fp);
+    if constexpr (DIGEST)
+      atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + it.x),
+                (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
+    asm volatile("" ::: "memory");  // keep the LDS weight reads inside (see score_sum_kernel)
+    sum_write_out(p, it.x, it.y, cr.x, mlp_sum(s_w, relb, f), base);
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifndef RNNL_SUM_CK
+#define RNNL_SUM_CK 8
+#endif
+constexpr int SUM_CK = RNNL_SUM_CK;  // chunks per dequeue
+
+template <bool DIGEST>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_WAVES, 8))) void score_sum_chunk_kernel(
+    KParams p, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_SUM>;
+  __shared__ __attribute__((aligned(16))) float s_w[L::N];
+  __shared__ float s_relb[BS / 64][128];
+  __shared__ int2 s_queue[BS / 64][128];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  load_sum_weights(s_w, W);
+  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum));
+  const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
+  const float inv_scale = ldexpf(1.f, -shift);
+  __syncthreads();  // the only workgroup barrier: waves run independently from here
+  const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
+  float *relb = s_relb[wv];
+  int2 *queue = s_queue[wv];
+  int cur_r = -1, n = 0;  // wave-uniform: the queue's relation and length
+  unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
+#pragma unroll 1
+  while (true) {
+    if (c == cend) {
+      // SUM_CK chunks per atomic: one counter word serialises ~10^6 single dequeues per launch
+      if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], (unsigned)SUM_CK);
+      c = __builtin_amdgcn_readfirstlane(c);
+      cend = c + SUM_CK;
+    }
+    const bool done = (long long)c >= nchunks;
+    int q = 0, s0 = 0, r = cur_r;
+    if (!done) {
+      const int2 ck = p.chunks[c];
+      q = __builtin_amdgcn_readfirstlane(ck.x);
+      s0 = __builtin_amdgcn_readfirstlane(ck.y);
+      r = __builtin_amdgcn_readfirstlane((int)p.all_r[q]);
+    }
+    const bool drain = done || r != cur_r;
+    // score full waves of queued candidates (all of them before a relation change / the exit)
+#pragma unroll 1
+    while (true) {
+      const int m = drain ? min(n, 64) : (n >= 64 ? 64 : 0);
+      if (m == 0) break;
+      wave_lds_sync();
+      sum_chunk_flush<DIGEST>(p, s_w, relb, queue, m, inv_scale);
+      n -= m;
+      const int2 v = lane < n ? queue[m + lane] : make_int2(0, 0);
+      wave_lds_sync();
+      if (lane < n) queue[lane] = v;
+    }
+    if (done) break;
+    if (r != cur_r) {
+      wave_lds_sync();  // every lane is done with the previous relation's bias
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = lane + 64 * j;
+        float acc = p.s0_b[o];
+        for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+        relb[o] = acc;
+      }
+      cur_r = r;
+    }
+    const int nc = p.n_cand[q];
+    const int64_t qb = p.q_base[q];
+    const int s = s0 + lane;
+    bool queued = false;
+    if (s < nc) {
+      const int4 cr = p.cand[qb + s];
+      queued = true;
+      if (cr.z == 1) {
+        const int2 be = p.bent[cr.y];
+        if (be.y == 1) {  // one path of one leaf node: the memo
+          queued = false;
+          const float base = sum_base(p, q, cr.x);
+          if constexpr (DIGEST)
+            atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q),
+                      (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)p.rl.node_nrules[be.x] ^
+                                                                        mix64(p.rl.node_fp[be.x]))));
+          sum_write_out(p, q, qb + s, cr.x, p.memo[be.x], base);
+        }
+      }
+    }
+    const uint64_t bal = __ballot(queued);
+    const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    wave_lds_sync();
+    if (queued) queue[pos] = make_int2(q, (int)(qb + s));
+    n += (int)__popcll(bal);  // < 128: the queue held < 64 before this chunk
+    ++c;
+  }
+}
+
 // Deferred scoring, second half: score[q][t] = out + score[q][t] (the same
 // fp32 sum as the direct path, operands commuted) and mask[q][t] = 1 for every
 // candidate record, once the base score (RotatE) is in place.  One workgroup
@@ -2399,6 +2540,15 @@ static bool pna_chunked() {
   return on;
 }
 
+// RNNL_SUM_CHUNKED=0 selects the per-query SUM memo scoring kernel (A/B)
+static bool sum_chunked() {
+  static const bool on = [] {
+    const char *e = getenv("RNNL_SUM_CHUNKED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int grid = 0) {
   const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
@@ -2415,6 +2565,15 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int gri
     const bool staged = base_lds + stage <= RNNL_STAGE_LIMIT;
     if (!staged && score_memo_enabled() && p.memo) {
       hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, (const float *)W);
+      if (sum_chunked()) {
+        if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);
+        const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * RNNL_SCORE_WG_PER_CU);
+        if (p.digest)
+          hipLaunchKernelGGL((score_sum_chunk_kernel<true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+        else
+          hipLaunchKernelGGL((score_sum_chunk_kernel<false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+        return;
+      }
       if (p.digest)
         hipLaunchKernelGGL((score_sum_memo_kernel<true>), dim3(sgrid), dim3(BS), 0, st, p, (const float *)W);
       else

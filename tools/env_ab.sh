@@ -12,7 +12,7 @@ fi
 for rep in 1 2; do
 for v in ${VALS:-0 1}; do
   for l in ${LINES:-bias wn rotate}; do
-    f=$o/${l}_${v}_$rep.log
+    f=$o/${l}_$(basename "$v" .so)_$rep.log
     case $l in
       bias) env $VAR=$v timeout -k 10 300 python -u bench.py --feature bias --no-cpu-baseline --profile-only > $f 2> $f.err ;;
       rotate) env $VAR=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --profile-only > $f 2> $f.err ;;
