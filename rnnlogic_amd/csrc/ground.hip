@@ -79,7 +79,7 @@ enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H
 // sums would wrap), 16 the node-weight table is out of its fixed-point range
 // (a non-finite aggregate, or |sum| >= 2^30), 32 a candidate's counts sum past
 // the exact int64 feature sums.  8, 16 and 32 -> RNNL_ERR_RANGE.
-enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16, ERR_ACC_RANGE = 32, ERR_CHUNKS = 64 };
+enum { ERR_WATCHDOG = 4, ERR_COUNT_WIDTH = 8, ERR_NODE_RANGE = 16, ERR_ACC_RANGE = 32 };
 constexpr int HDR_WORDS_BYTES = 256;
 
 // Packed MLP weights (written by pack_weights_kernel behind the header).
@@ -219,7 +219,7 @@ static Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   // PNA scoring chunks: sum over queries of ceil(candidates / 64) <= nq + pool_cap / 64
   L.chunk_cap = std::max<int64_t>(nq, 1) + L.pool_cap / 64 + 1;
   L.off_chunk = o = align256(o);
-  o += 8 * L.chunk_cap;
+  o += 8 * L.chunk_cap + 4 * (std::max<int64_t>(nq, 1) / 256 + 1);  // list | per-block chunk totals
   L.off_memo = o = align256(o);
   o += 4 * n_nodes;
   L.total = o;
@@ -310,7 +310,7 @@ struct __align__(16) Smem {
   };
   int ws[GNW + 1];
   int q, nd, np, ovf, err, root;
-  long long qbase, cbase;
+  long long qbase;
   unsigned long long t0;
   int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
   unsigned long long sumlog;
@@ -893,21 +893,6 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
     }
     const int ncand = candidates_phase(p, S, sl, P, false, sorted);
     __syncthreads();  // S.err: a PNA degree may have hit 2^32 in phase B
-    {
-      // the query's scoring work units: one per 64 candidates (score_pna_chunk_kernel /
-      // score_sum_chunk_kernel balance them over waves, so one large query no longer
-      // sets the kernel's tail)
-      const int nck = (ncand + 63) >> 6;
-      if (tid == 0 && !S.err) {
-        const unsigned long long b = atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_CHUNKS),
-                                               (unsigned long long)nck);
-        if (b + nck > (unsigned long long)p.chunk_cap) S.err |= ERR_CHUNKS;  // cannot happen: chunk_cap bounds the sum
-        S.cbase = (long long)b;
-      }
-      __syncthreads();
-      if (!S.err)
-        for (int k = tid; k < nck; k += GBS) p.chunks[S.cbase + k] = make_int2(q, k << 6);
-    }
     if (tid == 0 && S.err) {
       flag_error(p, hdr, S, q);
     } else if (tid == 0) {
@@ -1349,10 +1334,96 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
   }
 }
 
+// ---------------------------------------------------------------- scoring chunks
+// The scoring passes' unit of work: one wave x one chunk of <= 64 consecutive
+// candidates of one query.  The chunk list p.chunks (query, first candidate) is
+// in ROW order — eval and train rows come in same-relation batches, so waves
+// walking the list rarely change relation — and is built after the grounding
+// by two small kernels: per 256-row block the chunk total (chunk_sum_kernel),
+// then per block its prefix, a block scan and the entries (chunk_fill_kernel).
+// The total goes to hdr[H_CHUNKS].
+constexpr int CHB = 256;  // rows per chunk-list block (small blocks: they launch beside RotatE)
+
+__device__ __forceinline__ int row_chunks(const KParams &p, int q) {
+  const int nc = q < p.nq ? p.n_cand[q] : 0;
+  return nc > 0 ? (nc + 63) >> 6 : 0;
+}
+
+__global__ __launch_bounds__(CHB) void chunk_sum_kernel(KParams p, int *__restrict__ bsum) {
+  __shared__ int s_ws[CHB / 64];
+  int v = row_chunks(p, blockIdx.x * CHB + threadIdx.x);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s_ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < CHB / 64; ++w) t += s_ws[w];
+    bsum[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *__restrict__ bsum) {
+  __shared__ int s_ws[CHB / 64];
+  __shared__ long long s_pb[CHB / 64], s_pt[CHB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // this block's prefix and the list total from the per-block totals
+  long long pb = 0, pt = 0;
+  for (int k = tid; k < (int)gridDim.x; k += CHB) {
+    const int v = bsum[k];
+    pt += v;
+    if (k < (int)blockIdx.x) pb += v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pb += __shfl_xor(pb, o, 64);
+    pt += __shfl_xor(pt, o, 64);
+  }
+  if (lane == 0) {
+    s_pb[wid] = pb;
+    s_pt[wid] = pt;
+  }
+  const int q = blockIdx.x * CHB + tid;
+  const int n = row_chunks(p, q);
+  int v = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) s_ws[wid] = v;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < CHB / 64; ++w) {
+      const int t = s_ws[w];
+      s_ws[w] = acc;
+      acc += t;
+    }
+    long long base = 0, total = 0;
+    for (int w = 0; w < CHB / 64; ++w) {
+      base += s_pb[w];
+      total += s_pt[w];
+    }
+    s_pb[0] = base;
+    if (blockIdx.x == 0)
+      *reinterpret_cast<unsigned long long *>(reinterpret_cast<unsigned int *>(p.ws) + H_CHUNKS) = total;
+  }
+  __syncthreads();
+  const long long off = s_pb[0] + s_ws[wid] + v - n;
+  for (int k = 0; k < n; ++k) p.chunks[off + k] = make_int2(q, k << 6);
+}
+
+static void launch_chunk_list(const KParams &p, hipStream_t st) {
+  const unsigned nb = (unsigned)((p.nq + CHB - 1) / CHB);
+  int *bsum = reinterpret_cast<int *>(p.chunks + p.chunk_cap);  // nb ints after the list (layout)
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3(nb), dim3(CHB), 0, st, p, bsum);
+  hipLaunchKernelGGL(chunk_fill_kernel, dim3(nb), dim3(CHB), 0, st, p, (const int *)bsum);
+}
+
 // PNA scoring over chunks (default; RNNL_PNA_CHUNKED=0 keeps score_kernel<PNA>).
 // The unit of work is one wave x one chunk of <= 64 consecutive candidates of
-// one query (lane = candidate), listed by the grounding kernel in
-// p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue chunks independently, so a
+// one query (lane = candidate), p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue chunks independently, so a
 // query with 17k candidates (WN18RR) is spread over ~280 waves instead of
 // holding one workgroup while the rest of the grid drains; no workgroup
 // barrier per query.  Each wave folds its relation's half of
@@ -1954,7 +2025,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
 
 // SUM scoring over chunks (default; RNNL_SUM_CHUNKED=0 keeps
 // score_sum_memo_kernel): one wave x one 64-candidate chunk of one query at a
-// time (p.chunks, listed by the grounding kernel in completion order), no
+// time (p.chunks, in row order), no
 // workgroup barrier after the weight load.  Single-path candidates take the
 // memo (three loads and the store); the others are compacted (ballot + prefix)
 // into the wave's LDS queue of (query, pool index) and scored 64 at a time by
@@ -2013,13 +2084,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
   int2 *queue = s_queue[wv];
   int cur_r = -1, n = 0;  // wave-uniform: the queue's relation and length
   unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
+  // chunks per dequeue: SUM_CK on large launches, fewer where that would leave
+  // waves idle (at least 8 dequeues per wave)
+  const int ck = (int)max(1ll, min((long long)SUM_CK, nchunks / ((long long)gridDim.x * (BS / 64) * 8)));
 #pragma unroll 1
   while (true) {
     if (c == cend) {
       // SUM_CK chunks per atomic: one counter word serialises ~10^6 single dequeues per launch
-      if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], (unsigned)SUM_CK);
+      if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], (unsigned)ck);
       c = __builtin_amdgcn_readfirstlane(c);
-      cend = c + SUM_CK;
+      cend = c + ck;
     }
     const bool done = (long long)c >= nchunks;
     int q = 0, s0 = 0, r = cur_r;
@@ -2326,11 +2400,18 @@ __global__ __launch_bounds__(BS) void score_linear_kernel(KParams p, const int *
   const double inv = ldexp(1.0, -shift);
   check_node_table(p, reinterpret_cast<const unsigned int *>(reinterpret_cast<const unsigned char *>(fix) +
                                                              lin_trailer_off(p.rl.n_nodes)));
-  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+  // one wave per 64-candidate chunk of the grounding's chunk list (grid-stride)
+  const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(
+      reinterpret_cast<const unsigned int *>(p.ws) + H_CHUNKS);
+  const long long nw = (long long)gridDim.x * (BS / 64);
+  for (long long c = blockIdx.x * (BS / 64) + (threadIdx.x >> 6); c < nchunks; c += nw) {
+    const int2 ck = p.chunks[c];
+    const int q = ck.x;
     const int nc = p.n_cand[q];
-    if (nc <= 0) continue;
     const int64_t qb = p.q_base[q];
-    for (int s = threadIdx.x; s < nc; s += BS) {
+    {
+      const int s = ck.y + (int)(threadIdx.x & 63);
+      if (s >= nc) continue;
       const int4 cr = p.cand[qb + s];
       const int t = cr.x;
       long long acc = 0;
@@ -2566,6 +2647,7 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int gri
     if (!staged && score_memo_enabled() && p.memo) {
       hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, (const float *)W);
       if (sum_chunked()) {
+        launch_chunk_list(p, st);
         if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);
         const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * RNNL_SCORE_WG_PER_CU);
         if (p.digest)
@@ -2589,6 +2671,7 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int gri
       hipLaunchKernelGGL((score_sum_kernel<false, false>), dim3(sgrid), dim3(BS), lds, st, p, (const float *)W);
   } else if (pna_chunked()) {
     // per-query digests are sums over the query's chunks
+    launch_chunk_list(p, st);
     if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);
     const unsigned score_grid = (unsigned)(grid > 0 ? grid : NUM_CU * 8);
     hipLaunchKernelGGL(score_pna_chunk_kernel, dim3(score_grid), dim3(BS), 0, st, p, (const float *)W);
@@ -2790,6 +2873,7 @@ int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32
   p.score = score;
   p.mask = mask;
   hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
+  launch_chunk_list(p, st);
   hipLaunchKernelGGL(score_linear_kernel, dim3((unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8)), dim3(BS), 0, st,
                      p, static_cast<const int *>(node_w));
   RNNL_HIP_CHECK(hipGetLastError());
@@ -2858,7 +2942,7 @@ int rnnl_forward_status(void *ws, void *stream) {
       return RNNL_ERR_RANGE;
     }
     set_error("rnnl_predictorplus_forward: internal error bits " + std::to_string(bits) +
-              " (4: watchdog, 64: scoring chunk table) at query " + std::to_string(st[H_ERRQ]));
+              " (4: watchdog) at query " + std::to_string(st[H_ERRQ]));
     return RNNL_ERR_INTERNAL;
   }
   if (st[H_STATUS] & 1u) {
