@@ -1421,6 +1421,22 @@ static void launch_chunk_list(const KParams &p, hipStream_t st) {
   hipLaunchKernelGGL(chunk_fill_kernel, dim3(nb), dim3(CHB), 0, st, p, (const int *)bsum);
 }
 
+// A wave's next range of k chunks: its first range is static (its grid-wide
+// wave index), later ones come from the dequeue counter past the static part,
+// which is never touched when the static ranges cover the list.  Wave-uniform.
+__device__ __forceinline__ void next_chunks(unsigned int *ctr, long long nchunks, int k, unsigned &c, unsigned &cend) {
+  const unsigned long long stat = (unsigned long long)gridDim.x * (BS / 64) * k;
+  if (cend == 0u) {
+    c = (blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) * (unsigned)k;
+  } else if ((long long)stat >= nchunks) {
+    c = (unsigned)nchunks;
+  } else {
+    if ((threadIdx.x & 63) == 0) c = (unsigned)stat + atomicAdd(ctr, (unsigned)k);
+    c = __builtin_amdgcn_readfirstlane(c);
+  }
+  cend = c + (unsigned)k;
+}
+
 // PNA scoring over chunks (default; RNNL_PNA_CHUNKED=0 keeps score_kernel<PNA>).
 // The unit of work is one wave x one chunk of <= 64 consecutive candidates of
 // one query (lane = candidate), p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue chunks independently, so a
@@ -1460,11 +1476,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
   unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
 #pragma unroll 1
   for (;; ++c) {
-    if (c == cend) {
-      if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], (unsigned)PNA_CK);
-      c = __builtin_amdgcn_readfirstlane(c);
-      cend = c + PNA_CK;
-    }
+    if (c == cend) next_chunks(&hdr[H_DEQUEUE2], nchunks, PNA_CK, c, cend);
     if ((long long)c >= nchunks) break;
     const int2 ck = p.chunks[c];
     const int q = __builtin_amdgcn_readfirstlane(ck.x);
@@ -2089,12 +2101,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
   const int ck = (int)max(1ll, min((long long)SUM_CK, nchunks / ((long long)gridDim.x * (BS / 64) * 8)));
 #pragma unroll 1
   while (true) {
-    if (c == cend) {
-      // SUM_CK chunks per atomic: one counter word serialises ~10^6 single dequeues per launch
-      if (lane == 0) c = atomicAdd(&hdr[H_DEQUEUE2], (unsigned)ck);
-      c = __builtin_amdgcn_readfirstlane(c);
-      cend = c + ck;
-    }
+    // up to SUM_CK chunks per atomic: one counter word serialises ~10^6 single dequeues per launch
+    if (c == cend) next_chunks(&hdr[H_DEQUEUE2], nchunks, ck, c, cend);
     const bool done = (long long)c >= nchunks;
     int q = 0, s0 = 0, r = cur_r;
     if (!done) {

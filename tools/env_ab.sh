@@ -17,6 +17,7 @@ for v in ${VALS:-0 1}; do
       bias) env $VAR=$v timeout -k 10 300 python -u bench.py --feature bias --no-cpu-baseline --profile-only > $f 2> $f.err ;;
       rotate) env $VAR=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --profile-only > $f 2> $f.err ;;
       wn) env $VAR=$v timeout -k 10 300 python -u tools/wn_profile.py > $f 2> $f.err ;;
+      kin) env $VAR=$v timeout -k 10 300 python -u tools/kin_profile.py > $f 2> $f.err ;;
     esac || { tail -20 $f.err; exit 1; }
     python - "$f" "$l" "$VAR=$v" <<'PY'
 import ast, json, sys
