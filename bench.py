@@ -570,11 +570,12 @@ def main():
     if ground_ms is None:  # --profile-only with the RotatE overlap: no isolated grounding time
         ground_ms = float("nan")
     gt = [gtraffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_sum_memo_kernel", "memo_sum_kernel",
-                                    "score_kernel")]
+                                    "score_kernel", "score_sum_chunk_kernel", "score_pna_chunk_kernel",
+                                    "chunk_sum_kernel", "chunk_fill_kernel")]
     gt = sum(x for x in gt if x) or None
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-              "traffic": gt, "kernel": "ground_kernel + scoring (score_sum_memo_kernel + memo_sum_kernel)",
+              "traffic": gt, "kernel": "ground_kernel + scoring (chunk list + memo_sum_kernel + score_sum_chunk_kernel)",
               "ms": round(ground_ms, 3),
               "measured": ground_how,
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
