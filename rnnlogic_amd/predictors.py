@@ -475,7 +475,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # ~18 ms, well inside the RotatE launch.
         # The scoring pass beside RotatE runs 512 workgroups (2 per CU): FB15k-237
         # 83.4-84.0 ms/step for 256-1024 vs 84.4-84.6 at full occupancy
-        # (tools/ab_env.sh, RNNL_OVERLAP_SCORE_WG).
+        # (tools/env_ab.sh, RNNL_OVERLAP_SCORE_WG).
         self.overlap_ground_wg = int(os.environ.get("RNNL_OVERLAP_GROUND_WG", "256"))
         self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "512"))
         # sum aggregator: the scoring pass also runs beside RotatE, writing its
