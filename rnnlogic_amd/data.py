@@ -292,9 +292,31 @@ class DeviceEvalBatches(object):
     def __len__(self):
         return len(self.eval_set)
 
+    def _table(self):
+        """All batches' (h, r, t) rows on the device once, with per-batch
+        offsets, so `rows` gathers a whole split without a Python pass over
+        its triples (an eval set's batches are fixed at construction,
+        reference src/data.py:230-240; rebuilt if the list is replaced)."""
+        batches = self.eval_set.batches
+        key = (id(batches), len(batches))
+        if getattr(self, "_tab_key", None) != key:
+            lens = np.fromiter((len(b) for b in batches), dtype=np.int64, count=len(batches))
+            off = np.zeros(len(batches) + 1, dtype=np.int64)
+            np.cumsum(lens, out=off[1:])
+            flat = np.asarray([x for b in batches for x in b], dtype=np.int64).reshape(-1, 3)
+            self._tab = (torch.from_numpy(flat).to(self.device), lens, off)
+            self._tab_key = key
+        return self._tab
+
     def rows(self, indices):
         E = self.eval_set.graph.entity_size
-        all_h, all_r, all_t = _batch_rows(self.eval_set.batches, indices, self.device)
+        tab, lens, off = self._table()
+        idx = np.asarray(list(indices), dtype=np.int64)
+        n = lens[idx]
+        # positions of the selected batches' rows, in the order of `indices`
+        sel = np.repeat(off[idx] - (np.cumsum(n) - n), n) + np.arange(int(n.sum()), dtype=np.int64)
+        hrt = tab[torch.from_numpy(sel).to(self.device, non_blocking=True)]
+        all_h, all_r, all_t = hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
         flag = torch.empty((all_h.numel(), E), dtype=torch.bool, device=self.device)
         if all_h.numel():
             self.lists.rows("rnnl_filter_flags", (all_r * E + all_h).contiguous(), E, flag.view(torch.uint8))
