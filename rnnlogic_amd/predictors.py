@@ -311,7 +311,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         nr = self.native_rules(device)
         w = self.rule_weights
         node_w = torch.zeros(nr.n_nodes, device=device, dtype=w.dtype).index_add(0, nr.node_of_rule, w)
-        val = torch.zeros(C, device=device, dtype=w.dtype).index_add(0, ce, count.to(w.dtype) * node_w[node])
+        val = torch.zeros(C, device=device, dtype=w.dtype).index_add(0, ce, count.to(w.dtype) * node_w.index_select(0, node))
         score = torch.zeros(nq * E, device=device, dtype=w.dtype).scatter(0, row * E + ent, val).view(nq, E)
         if self.entity_feature == "bias":
             return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
@@ -827,14 +827,17 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         rels = torch.unique(all_r).tolist()
         ridx = torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
         if self.type == "emb":
-            x_f = self.rule_emb[ridx]
+            x_f = self.rule_emb.index_select(0, ridx)
         else:
             x_f = self.encode_rules(self.rule_features.to(device)[ridx])
         nodes = nr.node_of_rule[ridx]
         H = self.hidden_dim
+        # gathers of differentiable tables use index_select: its backward is an
+        # index_add, where x[idx]'s is the sort-based index_put accumulate
+        # (8 ms of a 16.5 ms FB15k-237 training step)
         cnt = count.to(x_f.dtype).unsqueeze(-1)
         node_sum = torch.zeros((nr.n_nodes, H), device=device, dtype=x_f.dtype).index_add(0, nodes, x_f)
-        wsum = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sum[node])
+        wsum = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sum.index_select(0, node))
         if self.aggregator == "sum":
             out = self.rule_to_entity.finish(wsum)
         else:
@@ -846,15 +849,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 0, idx_n, x_f, "amin", include_self=True)
             node_max = torch.full((nr.n_nodes, H), float("-inf"), device=device, dtype=x_f.dtype).scatter_reduce(
                 0, idx_n, x_f, "amax", include_self=True)
-            wsq = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sq[node])
-            deg = torch.zeros(C, device=device, dtype=x_f.dtype).index_add(0, ce, cnt.squeeze(-1) * node_n[node]) + 1
+            wsq = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sq.index_select(0, node))
+            deg = torch.zeros(C, device=device, dtype=x_f.dtype).index_add(0, ce, cnt.squeeze(-1) * node_n.index_select(0, node)) + 1
             idx_c = ce.unsqueeze(-1).expand(-1, H)
             mn = torch.full((C, H), float("inf"), device=device, dtype=x_f.dtype).scatter_reduce(
-                0, idx_c, node_min[node], "amin", include_self=True)
+                0, idx_c, node_min.index_select(0, node), "amin", include_self=True)
             mx = torch.full((C, H), float("-inf"), device=device, dtype=x_f.dtype).scatter_reduce(
-                0, idx_c, node_max[node], "amax", include_self=True)
+                0, idx_c, node_max.index_select(0, node), "amax", include_self=True)
             out = self.rule_to_entity.finish(wsum, wsq, mn, mx, deg, row, nq)
-        rel = self.relation_emb(all_r[row])
+        rel = self.relation_emb(all_r).index_select(0, row)  # per row, then per candidate
         output = self.score_model(torch.cat([out, rel], dim=-1)).squeeze(-1)
         score = torch.zeros(nq * E, device=device, dtype=output.dtype).scatter(0, row * E + ent, output).view(nq, E)
         if self.entity_feature == "bias":
