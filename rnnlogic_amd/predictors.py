@@ -167,7 +167,7 @@ class _HipGrounding(object):
         _native.call("rnnl_ground_export_candidates", ws.data_ptr(), nq, scale, n_cand.data_ptr(),
                      cand_off.data_ptr(), ent.data_ptr(), nent.data_ptr(), stream)
         ent, nent = ent[:C].to(torch.int64), nent[:C].to(torch.int64)
-        row = torch.repeat_interleave(torch.arange(nq, device=device), nc)
+        row = torch.repeat_interleave(torch.arange(nq, device=device), nc, output_size=C)  # (no size sync)
         per_row = torch.zeros(nq, dtype=torch.int64, device=device).index_add_(0, row, nent)
         ent_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
         torch.cumsum(per_row, 0, out=ent_off[1:])
@@ -176,7 +176,7 @@ class _HipGrounding(object):
         count = torch.empty(max(P, 1), dtype=torch.int32, device=device)
         _native.call("rnnl_ground_export_entries", ws.data_ptr(), nq, scale, n_cand.data_ptr(), ent_off.data_ptr(),
                      node.data_ptr(), count.data_ptr(), stream)
-        cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent)
+        cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent, output_size=P)
         # path counts are u32 in the kernel (< 2^32, carry-checked): reinterpret the int32 bits
         return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64) & 0xFFFFFFFF
 

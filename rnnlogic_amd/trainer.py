@@ -135,14 +135,15 @@ class TrainerPredictor(object):
             target_t = target_t.cuda(device=self.device)
         target = target * smoothing + target_t * (1 - smoothing)
         logits, mask = model(all_h, all_r, edges_to_remove)
-        if mask.sum().item() == 0:
+        msum = mask.sum().item()  # one host sync for the check and the returned size
+        if msum == 0:
             return None, None
         logits = (torch.softmax(logits, dim=1) + 1e-8).log()
         loss = -(logits[mask] * target[mask]).sum() / torch.clamp(target[mask].sum(), min=1)
         loss.backward()
         self.optimizer.step()
         self.optimizer.zero_grad()
-        return loss.item(), mask.sum().item()
+        return loss.item(), msum
 
     # ------------------------------------------------------------------ H scores
     @torch.no_grad()
