@@ -100,8 +100,9 @@ def train_rows(train_set, n_rows):
     return torch.cat(hs), torch.cat(rs), torch.cat(es), i + 1
 
 
-def time_forward(fn, reps):
-    fn()
+def time_forward(fn, reps, warmup=2):
+    for _ in range(warmup):
+        fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -210,7 +211,7 @@ def isolated_ground_ms(model, graph, h, r, dev):
         return e0.elapsed_time(e1)
 
 
-def wn18rr_line(dev, reps=5):
+def wn18rr_line(dev, reps=10):
     """Config 3 of BASELINE.json as a secondary line: PredictorPlus(emb, pna)
     + RotatE(D=500, gamma=6) over the WN18RR test split (206 batches, 6,268
     queries, real rnnlogic_rules.txt: 7,386 rules, L <= 5), seeded synthetic
@@ -257,7 +258,7 @@ def wn18rr_line(dev, reps=5):
                         "rnnlogic_rules.txt (L<=5); seeded synthetic train graph and RotatE tables"}
 
 
-def kinship_line(dev, reps=10):
+def kinship_line(dev, reps=50):
     """Config 2 of BASELINE.json as a secondary line: PredictorPlus(lstm, 3,
     16, sum) without an entity feature on the kinship test split (178 batches,
     5,343 queries; the mined L <= 3 rule file, top 100 per relation: 2,500
