@@ -176,6 +176,11 @@ int rnnl_predictorplus_apply(void *workspace, int32_t n_queries, int32_t capacit
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */
 int rnnl_forward_status(void *workspace, void *stream);
+/* rnnl_forward_status plus the grounding's totals from the same read-back:
+ * totals[0] = candidates (sum of n_cand), totals[1] = bucket entries (the
+ * (trie node, path count) entries of the COO), so a caller sizing the COO
+ * export needs no further synchronisation.  Valid when RNNL_OK. */
+int rnnl_forward_status_totals(void *workspace, void *stream, int64_t *totals);
 /* Grounding only (reference data.py:136-173 for every rule of every row,
  * predictors.py:221-244): fills the workspace's COO of the stacked rule_count
  * matrix and n_cand (per row candidate count, -1/-2 on overflow/error; check

@@ -48,6 +48,7 @@ SIGNATURES = [
      [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _I32, _I32, _P]),
     ("rnnl_predictorplus_apply", ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _I32, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
+    ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_ground", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_ground_export_candidates", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_ground_export_entries", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),

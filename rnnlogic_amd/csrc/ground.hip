@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "internal.h"
@@ -74,7 +75,8 @@ constexpr int EMPTY = -1;
 constexpr int SORT_WORDS = (9 * GBS * 4 / 6) & ~(GBS - 1);
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
-enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6 };
+enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6, H_NCAND = 8 };
+// (64-bit words: H_CHUNKS the scoring chunk total, H_NCAND the candidate total of the grounding)
 // H_ERRBITS: 4 watchdog, 8 a path count or PNA degree reached 2^32 (the u32
 // sums would wrap), 16 the node-weight table is out of its fixed-point range
 // (a non-finite aggregate, or |sum| >= 2^30), 32 a candidate's counts sum past
@@ -897,6 +899,7 @@ __global__ __launch_bounds__(GBS, RNNL_GROUND_MINB) void ground_kernel(KParams p
       flag_error(p, hdr, S, q);
     } else if (tid == 0) {
       p.n_cand[q] = ncand;
+      atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_NCAND), (unsigned long long)ncand);
       p.q_base[q] = S.qbase;
       if (p.prof) {
         pr[2] += __builtin_amdgcn_s_memtime() - t_a;
@@ -2934,10 +2937,17 @@ int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t poo
   return RNNL_OK;
 }
 
-int rnnl_forward_status(void *ws, void *stream) {
-  unsigned int st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+static int forward_status(void *ws, void *stream, int64_t *totals) {
+  unsigned int st[18] = {0};  // header words 0..17: status, ..., H_NCAND, the pool counter (byte 64)
   RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
   RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (totals) {
+    unsigned long long c, e;
+    memcpy(&c, st + H_NCAND, 8);
+    memcpy(&e, st + 16, 8);
+    totals[0] = (int64_t)c;  // candidates (sum of n_cand)
+    totals[1] = (int64_t)e;  // bucket entries (every contribution is one entry of its candidate's bucket)
+  }
   if (st[H_STATUS] & 2u) {
     const unsigned bits = st[H_ERRBITS];
     if (bits & (ERR_COUNT_WIDTH | ERR_NODE_RANGE | ERR_ACC_RANGE) && !(bits & ERR_WATCHDOG)) {
@@ -2958,6 +2968,16 @@ int rnnl_forward_status(void *ws, void *stream) {
     return RNNL_ERR_OVERFLOW;
   }
   return RNNL_OK;
+}
+
+int rnnl_forward_status(void *ws, void *stream) { return forward_status(ws, stream, nullptr); }
+
+int rnnl_forward_status_totals(void *ws, void *stream, int64_t *totals) {
+  if (!ws || !totals) {
+    set_error("rnnl_forward_status_totals: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  return forward_status(ws, stream, totals);
 }
 
 }  // extern "C"

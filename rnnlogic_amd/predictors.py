@@ -113,15 +113,21 @@ class _HipGrounding(object):
         etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
         return device, all_h, all_r, etr
 
-    def _launch(self, device, nq, run):
+    def _launch(self, device, nq, run, totals=None):
         """run(ws, scale) launches onto the workspace; retried with a doubled
-        capacity_scale while the launch reports overflow.  Returns (ws, scale)."""
+        capacity_scale while the launch reports overflow.  Returns (ws, scale).
+        `totals` (int64[2] numpy array): filled with the grounding's candidate
+        and bucket-entry totals by the same read-back as the status."""
         stream = torch.cuda.current_stream(device).cuda_stream
         while True:
             scale = self.capacity_scale
             ws = self._workspace(device, nq, scale)
             run(ws, scale)
-            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
+            if totals is not None:
+                rc = _native.lib().rnnl_forward_status_totals(ws.data_ptr(), stream,
+                                                             totals.ctypes.data_as(ctypes.c_void_p))
+            else:
+                rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
                 logging.info("%s: workspace overflow, capacity_scale -> %d", type(self).__name__,
@@ -130,9 +136,10 @@ class _HipGrounding(object):
             _native.check(rc)
             return ws, scale
 
-    def ground(self, all_h, all_r, edges_to_remove=None):
+    def ground(self, all_h, all_r, edges_to_remove=None, totals=None):
         """Grounding of every rule of every row into the workspace (HIP
-        rnnl_ground).  Returns (ws, scale, n_cand (n,) int32)."""
+        rnnl_ground).  Returns (ws, scale, n_cand (n,) int32); `totals` as in
+        _launch."""
         device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
         nq = all_h.numel()
         g, nr = self.graph.device_graph(device), self.native_rules(device)
@@ -143,7 +150,7 @@ class _HipGrounding(object):
             _native.call("rnnl_ground", g, nr.ptr, all_h.data_ptr(), all_r.data_ptr(),
                          etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
                          ws.numel(), scale, stream)
-        ws, scale = self._launch(device, nq, run)
+        ws, scale = self._launch(device, nq, run, totals)
         return ws, scale, n_cand
 
     def ground_coo(self, all_h, all_r, edges_to_remove=None):
@@ -156,12 +163,13 @@ class _HipGrounding(object):
         path count) entries; node ids index `native_rules(device).node_of_rule`."""
         device = all_h.device
         nq = all_h.numel()
-        ws, scale, n_cand = self.ground(all_h, all_r, edges_to_remove)
+        totals = np.zeros(2, dtype=np.int64)  # (candidates, bucket entries) with the status read-back
+        ws, scale, n_cand = self.ground(all_h, all_r, edges_to_remove, totals)
         stream = torch.cuda.current_stream(device).cuda_stream
         nc = n_cand.to(torch.int64)
         cand_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
         torch.cumsum(nc, 0, out=cand_off[1:])
-        C = int(cand_off[-1].item())
+        C, P = int(totals[0]), int(totals[1])
         ent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
         nent = torch.empty(max(C, 1), dtype=torch.int32, device=device)
         _native.call("rnnl_ground_export_candidates", ws.data_ptr(), nq, scale, n_cand.data_ptr(),
@@ -171,7 +179,6 @@ class _HipGrounding(object):
         per_row = torch.zeros(nq, dtype=torch.int64, device=device).index_add_(0, row, nent)
         ent_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
         torch.cumsum(per_row, 0, out=ent_off[1:])
-        P = int(ent_off[-1].item())
         node = torch.empty(max(P, 1), dtype=torch.int32, device=device)
         count = torch.empty(max(P, 1), dtype=torch.int32, device=device)
         _native.call("rnnl_ground_export_entries", ws.data_ptr(), nq, scale, n_cand.data_ptr(), ent_off.data_ptr(),
