@@ -291,8 +291,9 @@ class Predictor(_HipGrounding, torch.nn.Module):
     # ------------------------------------------------------------------ reference API
     def forward(self, all_h, all_r, edges_to_remove):
         """predictors.py:53-80: one single-relation batch -> (score, mask)."""
-        query_r = all_r[0].item()
-        assert (all_r != query_r).sum() == 0
+        # the reference's single-relation check (predictors.py:54-55) in one host read
+        query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
+        assert n_other == 0
         if self._needs_grad():
             return self.forward_autograd(all_h, all_r, edges_to_remove)
         score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
@@ -781,7 +782,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             break
 
     # ------------------------------------------------------------------ autograd (training) path
-    def forward_autograd(self, all_h, all_r, edges_to_remove):
+    def forward_autograd(self, all_h, all_r, edges_to_remove, query_r=None):
         """Differentiable forward (training): the HIP grounding's COO, then the
         reference's aggregation / MLP / entity feature as torch ops on it, so
         autograd yields the reference's gradients (predictors.py:210-271,
@@ -800,7 +801,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 return zero + self.RotatE.forward_grad(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
                                                                                  device=device)
             return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
-        return self._score_coo(all_h, all_r, row, ent, ce, node, count)
+        return self._score_coo(all_h, all_r, row, ent, ce, node, count, rels=query_r)
 
     def forward_coo(self, all_h, all_r, edges_to_remove=None):
         """Rows of any relations through the HIP grounding COO and the torch
@@ -825,13 +826,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         score, mask = self._score_coo(all_h, all_r, row, ent, ce, node, count)
         return score, mask, n_cand
 
-    def _score_coo(self, all_h, all_r, row, ent, ce, node, count):
-        """predictors.py:238-271 on the grounding COO (torch ops)."""
+    def _score_coo(self, all_h, all_r, row, ent, ce, node, count, rels=None):
+        """predictors.py:238-271 on the grounding COO (torch ops).  `rels`: the
+        rows' relations when the caller knows them (forward's single-relation
+        batch), which saves the host sync of torch.unique."""
         device = all_h.device
         nq, E = all_h.numel(), self.num_entities
         C = ent.numel()
         nr = self.native_rules(device)
-        rels = torch.unique(all_r).tolist()
+        rels = [rels] if isinstance(rels, int) else torch.unique(all_r).tolist()
         ridx = torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
         if self.type == "emb":
             x_f = self.rule_emb.index_select(0, ridx)
@@ -880,10 +883,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
 
         With autograd active (training) the differentiable path runs
         (forward_autograd); otherwise the fused HIP kernels (forward_rows)."""
-        query_r = all_r[0].item()
-        assert (all_r != query_r).sum() == 0
+        # the reference's single-relation check (predictors.py:211-212) in one host read
+        query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
+        assert n_other == 0
         if self._needs_grad():
-            return self.forward_autograd(all_h, all_r, edges_to_remove)
+            return self.forward_autograd(all_h, all_r, edges_to_remove, query_r=query_r)
         score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
         if self.entity_feature not in ("bias", "RotatE") and int(n_cand.sum().item()) == 0:
             # reference early return `mask - float('-inf')` (predictors.py:236-237): +inf, mask all False
