@@ -512,14 +512,25 @@ class TrainerGenerator(object):
         return all_rules
 
     @torch.no_grad()
-    def sample(self, num_samples, max_len, temperature=1.0):
+    def sample(self, num_samples, max_len, temperature=1.0, batched=False):
         """num_samples sequences per head relation drawn from the generator,
-        deduplicated per relation, [head, body..., Σ log p] (trainer.py:413-465).
-        All relations are drawn together (one multinomial per position)."""
+        deduplicated per relation, [head, body..., Σ log p] (trainer.py:412-458).
+
+        Default: the reference's draw order — relation by relation, one
+        multinomial over that relation's num_samples rows per position, the
+        same tensor shapes and ops — so a seeded run draws the reference's
+        rules (the global RNG is consumed identically), and each relation's
+        rules are deduplicated through a Python set as the reference does
+        (trainer.py:453-454), which fixes their order.  `batched=True` draws
+        every relation at once per position instead (one multinomial over
+        R * num_samples rows: fewer launches, a different RNG order, and rules
+        kept in first-drawn order)."""
         if comm.get_rank() == 0:
             logging.info(">>>>> Generator: Rule generation with sampling")
         model = self.model
         model.eval()
+        if not batched:
+            return self._sample_reference_order(num_samples, max_len, temperature)
         dev = self.device
         R, END = model.num_relations, model.ending_idx
         N = R * num_samples
@@ -545,6 +556,42 @@ class TrainerGenerator(object):
             for k in range(r * num_samples, (r + 1) * num_samples):
                 seen.setdefault(tuple(rules[k][:1 + length[k]] + [total[k]]), None)
             all_rules += [list(x) for x in seen]
+        return all_rules
+
+    def _sample_reference_order(self, num_samples, max_len, temperature):
+        """sample() in the reference's RNG order (trainer.py:419-456): per head
+        relation, num_samples sequences advanced one token per position by
+        the LSTM with a multinomial draw; rows whose previous token is END keep
+        END and log p 0.  One host read per relation (its tokens and
+        log-probability sums)."""
+        model = self.model
+        dev = self.device
+        END = model.ending_idx
+        S = num_samples
+        all_rules = []
+        for relation in range(model.num_relations):
+            rules = torch.full((S, max_len + 1), END, dtype=torch.long, device=dev)
+            logp = torch.zeros((S, max_len + 1), device=dev)
+            head = torch.full((S,), relation, dtype=torch.long, device=dev)
+            rules[:, 0] = relation
+            hidden = self.zero_state(S)
+            for pst in range(max_len):
+                logits, hidden = model(rules[:, pst].unsqueeze(-1), head, hidden)
+                logits = logits.squeeze(1) / temperature
+                draw = torch.multinomial(torch.softmax(logits, dim=-1), 1)
+                lp = torch.log_softmax(logits, dim=-1).gather(1, draw).squeeze(-1)
+                live = rules[:, pst] != END
+                rules[:, pst + 1] = torch.where(live, draw.squeeze(-1), rules[:, pst + 1])
+                logp[:, pst + 1] = torch.where(live, lp, logp[:, pst + 1])
+            length = (rules != END).sum(-1) - 1
+            # [length | tokens | Σ log p] in one host read
+            packed = torch.cat([length.unsqueeze(1).double(), rules.double(), logp.sum(-1).double().unsqueeze(1)], 1)
+            packed = packed.cpu().numpy()
+            seqs = []
+            for row in packed:
+                n = int(row[0])
+                seqs.append(tuple(int(x) for x in row[1:2 + n]) + (float(np.float32(row[-1])),))
+            all_rules += [list(x) for x in set(seqs)]
         return all_rules
 
     def load(self, checkpoint):

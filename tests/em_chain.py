@@ -3,8 +3,12 @@ mirroring tools/make_golden_em.py step for step, so its outputs compare with
 tests/golden/em_umls.npz (the reference's own run of the same sequence).
 
 `run(device, em=False)` stops after the generator pre-training / beam search
-(pure PyTorch, runs on CPU); `em=True` continues with one EM iteration, whose
-Predictor runs on the HIP path (GPU only)."""
+(pure PyTorch, runs on CPU); `em=True` continues with one EM iteration, which
+starts as run_rnnlogic.py:68 does, from TrainerGenerator.sample(), and whose
+Predictor runs on the HIP path (GPU only).  `gen_device` (default: `device`)
+places the generator: the reference's sample() draws from the CPU RNG in the
+fixture, so an EM iteration that must reproduce its rules keeps the generator
+on the CPU while the predictor runs on the GPU."""
 import json
 import os
 
@@ -27,7 +31,7 @@ def _probe():
     return torch.randint(0, 2 ** 31 - 1, (4,)).numpy()
 
 
-def run(device, em=False):
+def run(device, em=False, gen_device=None, stop_after_sample=False):
     from rnnlogic_amd import datasets
     from rnnlogic_amd.data import KnowledgeGraph, RuleDataset, TestDataset, TrainDataset, ValidDataset
     from rnnlogic_amd.generators import Generator
@@ -47,7 +51,8 @@ def run(device, em=False):
     gen = Generator(graph, **cfg["gen"])
     got["gen_init"] = {k: v.detach().cpu().numpy().copy() for k, v in gen.state_dict().items()}
     gpu = None if device.type == "cpu" else device.index or 0
-    solver_g = TrainerGenerator(gen, gpu=gpu)
+    gen_device = device if gen_device is None else gen_device
+    solver_g = TrainerGenerator(gen, gpu=None if gen_device.type == "cpu" else gen_device.index or 0)
     got["pre_train/loss"] = _logged(lambda: solver_g.train(dataset, **cfg["pre_train"]))
     got["probe/pre_train"] = _probe()
     got["gen_pre"] = {k: v.detach().cpu().numpy().copy() for k, v in gen.state_dict().items()}
@@ -56,14 +61,17 @@ def run(device, em=False):
     got["pre/next_logp"] = np.asarray([solver_g.next_relation_log_probability(p, 0.2) for p in prefixes])
     got["pre/beam"] = solver_g.beam_search(**cfg["beam"])
     got["probe/beam"] = _probe()
-    if not em:
+    # run_rnnlogic.py:67-70: the EM iteration starts from the generator's samples
+    got["em/sampled"] = solver_g.sample(**cfg["sample"])
+    got["probe/sample"] = _probe()
+    if not em or stop_after_sample:
         return z, got
 
     from rnnlogic_amd.predictors import Predictor
     from rnnlogic_amd.trainer import TrainerPredictor
-    chosen = [int(i) for i in z["em/rule_index"]]
-    rules = [list(mined[i]) for i in chosen]
-    prior = [rule_weight(i) for i in chosen]
+    sampled = json.loads(str(z["em/sampled"]))  # the reference's rules (equal to ours when the test passes)
+    prior = [rule[-1] for rule in sampled]
+    rules = [rule[0:-1] for rule in sampled]
     predictor = Predictor(graph, entity_feature="bias")
     predictor.set_rules([list(r) for r in rules])
     got["pred_init"] = {k: v.detach().cpu().numpy().copy() for k, v in predictor.state_dict().items()}
@@ -83,7 +91,7 @@ def run(device, em=False):
         rules[i].append(posterior[i])
     got["m_step/loss"] = _logged(lambda: solver_g.train(RuleDataset(graph.relation_size, rules), **cfg["m_step"]))
     got["probe/m_step"] = _probe()
-    got["m_step/log_prob"] = np.asarray(solver_g.log_probability([list(mined[i]) for i in chosen]))
+    got["m_step/log_prob"] = np.asarray(solver_g.log_probability([list(r[:-1]) for r in rules]))
     got["gen_m"] = {k: v.detach().cpu().numpy().copy() for k, v in gen.state_dict().items()}
     return z, got
 

@@ -5,9 +5,14 @@ tools/make_golden_em.py).
 
 CPU: seeded init identical; generator pre-training (losses, weights, global
 RNG probes — the batch order comes from the same DataLoader draws);
-log_probability, next_relation_log_probability, beam_search.
-GPU: the same on cuda:0, then one EM iteration through the package (the
-Predictor on the HIP path): predictor losses, MRRs, H scores, posterior, the
+log_probability, next_relation_log_probability, beam_search, and sample()
+(run_rnnlogic.py:68): the same rules per relation, their log-probabilities to
+1e-6, the reference's rule order whenever the log-probabilities are bitwise
+equal (the reference dedupes through a Python set, whose order follows the
+float hashes), and the same global-RNG consumption.
+GPU: the generator chain on cuda:0; then one EM iteration started from the
+CPU generator's sample() (the fixture's draws come from the CPU RNG) with the
+Predictor on the HIP path: predictor losses, MRRs, H scores, posterior, the
 M-step's generator losses and final log-probabilities.
 
 Tolerances: the generator and the EM Predictor train in fp32 with a few
@@ -38,11 +43,11 @@ def _check_states(got, want, tol):
         _close(got[k], want[k], tol)
 
 
-def _check_generator_part(z, got):
+def _check_generator_part(z, got, w_tol=W_TOL):
     _check_states(got["gen_init"], em_chain.state(z, "gen_init"), 0.0)
-    _close(got["pre_train/loss"], z["pre_train/loss"], W_TOL + 1e-6)
+    _close(got["pre_train/loss"], z["pre_train/loss"], w_tol + 1e-6)
     assert np.array_equal(got["probe/pre_train"], z["probe/pre_train"])
-    _check_states(got["gen_pre"], em_chain.state(z, "gen_pre"), W_TOL)
+    _check_states(got["gen_pre"], em_chain.state(z, "gen_pre"), w_tol)
     _close(got["pre/log_prob"], z["pre/log_prob"], 1e-4)
     _close(got["pre/next_logp"], z["pre/next_logp"], 1e-4)
     import json
@@ -50,9 +55,41 @@ def _check_generator_part(z, got):
     assert np.array_equal(got["probe/beam"], z["probe/beam"])
 
 
+def _check_sample(got, want_json):
+    """Same rules per head relation (as sets), log p within 1e-6, and the
+    reference's order when every log p is bitwise equal."""
+    import json
+    want = json.loads(str(want_json))
+    assert len(got) == len(want)
+    key = lambda rule: tuple(int(x) for x in rule[:-1])  # noqa: E731
+    gmap, wmap = {key(r): r[-1] for r in got}, {key(r): r[-1] for r in want}
+    assert len(gmap) == len(got) and set(gmap) == set(wmap)
+    _close([gmap[k] for k in wmap], [wmap[k] for k in wmap], 1e-6)
+    if all(gmap[k] == wmap[k] for k in wmap):
+        assert [key(r) for r in got] == [key(r) for r in want]
+        return True
+    return False
+
+
 def test_generator_chain_cpu():
     z, got = em_chain.run(torch.device("cpu"))
+    # on the CPU the pre-training reproduces the reference's weights bitwise
+    # (same batches, same gathered loss sums, same Adam), hence sample()'s
+    # log-probabilities and its set order too
+    _check_generator_part(z, got, w_tol=0.0)
+    exact = _check_sample(got["em/sampled"], z["em/sampled"])
+    print("sample(): %d rules, bitwise log p and order: %s" % (len(got["em/sampled"]), exact))
+    assert exact
+    assert np.array_equal(got["probe/sample"], z["probe/sample"])
+
+
+@pytest.mark.gpu
+def test_generator_chain_gpu():
+    """The generator chain on cuda:0 (sample() draws from the device RNG
+    there, so only its contract is checked)."""
+    z, got = em_chain.run(torch.device("cuda:0"))
     _check_generator_part(z, got)
+    assert len(got["em/sampled"]) > 0
 
 
 def test_generator_state_dict_names():
@@ -79,9 +116,10 @@ def test_rule_dataset_and_table_match_collate():
             assert torch.equal(a, b), (idx, a, b)
 
 
-def test_sample_shapes_and_dedupe_cpu():
-    """sample() is not pinned (device RNG streams differ from the reference);
-    check its output contract: [head, body..., log p], body ≤ max_len, one
+@pytest.mark.parametrize("batched", [False, True])
+def test_sample_shapes_and_dedupe_cpu(batched):
+    """The output contract of both draw orders (the reference order is pinned
+    by test_generator_chain_cpu): [head, body..., log p], body ≤ max_len, one
     entry per distinct sequence and head, log p = the generator's own
     log_probability of the rule."""
     from rnnlogic_amd import datasets
@@ -91,7 +129,7 @@ def test_sample_shapes_and_dedupe_cpu():
     torch.manual_seed(0)
     g = Generator(KnowledgeGraph(datasets.materialize("umls")), num_layers=1, embedding_dim=16, hidden_dim=16)
     solver = TrainerGenerator(g, gpu=None)
-    out = solver.sample(20, 3)
+    out = solver.sample(20, 3, batched=batched)
     seen = set()
     for rule in out:
         body = rule[1:-1]
@@ -108,9 +146,13 @@ def test_sample_shapes_and_dedupe_cpu():
 
 @pytest.mark.gpu
 def test_em_iteration_gpu():
-    """run_rnnlogic.py:45-91 on cuda:0 through the package vs the reference run."""
-    z, got = em_chain.run(torch.device("cuda:0"), em=True)
+    """run_rnnlogic.py:45-91 through the package vs the reference run: the
+    generator on the CPU (its sample() must draw the fixture's rules), the
+    EM iteration's Predictor on cuda:0."""
+    z, got = em_chain.run(torch.device("cuda:0"), em=True, gen_device=torch.device("cpu"))
     _check_generator_part(z, got)
+    _check_sample(got["em/sampled"], z["em/sampled"])
+    assert np.array_equal(got["probe/sample"], z["probe/sample"])
     _check_states(got["pred_init"], em_chain.state(z, "pred_init"), 0.0)
     _close(got["em/train_loss"], z["em/train_loss"], W_TOL + 1e-6)
     assert np.array_equal(got["probe/em_train"], z["probe/em_train"])

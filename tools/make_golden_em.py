@@ -10,12 +10,13 @@ run_rnnlogic.py calls them, from set_seed(1):
   2. generator pre-training on a RuleDataset of the UMLS mined rules (weights
      below): logged mean losses, state_dict after, log_probability of every
      rule, next_relation_log_probability of a few prefixes, beam_search;
-  3. one EM iteration with a FIXED rule list (sample() draws from the device
-     RNG, so it is not pinned): Predictor(bias) + Adam, TrainerPredictor
-     train (logged losses) / evaluate valid + test / compute_H -> likelihood,
-     posterior = likelihood + prior_weight * prior, then the M-step
-     generator.train on the posterior-weighted rules (logged losses, final
-     log_probability).
+  3. one EM iteration as run_rnnlogic.py:67-91 runs it: sampled_rules =
+     TrainerGenerator.sample(num_rules, max_length) on the CPU (its rules,
+     in the reference's own order, and their log-probabilities), prior =
+     rule[-1]; Predictor(bias) + Adam, TrainerPredictor train (logged losses)
+     / evaluate valid + test / compute_H -> likelihood, posterior =
+     likelihood + prior_weight * prior, then the M-step generator.train on
+     the posterior-weighted rules (logged losses, final log_probability).
   After each stage the global torch RNG is probed (4 int draws), so a
   drop-in whose DataLoaders consume the RNG differently is caught.
 
@@ -42,7 +43,7 @@ import generators as R_gen  # noqa: E402  (reference src/generators.py)
 
 CFG = dict(seed=1, gen=dict(num_layers=1, embedding_dim=32, hidden_dim=32),
            pre_train=dict(num_epoch=60, lr=1e-3, print_every=20, batch_size=256),
-           beam=dict(num_samples=8, max_len=2), rules_per_relation=30, prior_weight=0.001,
+           beam=dict(num_samples=8, max_len=2), sample=dict(num_samples=20, max_len=3), prior_weight=0.001,
            predictor_train=dict(batch_per_epoch=40, smoothing=0.2, print_every=10),
            m_step=dict(num_epoch=30, lr=1e-3, print_every=10, batch_size=256))
 
@@ -111,16 +112,12 @@ def main():
     out["pre/beam"] = np.array(json.dumps(beam))
     out["probe/beam"] = probe()
 
-    # ---- one EM iteration on a fixed rule list (run_rnnlogic.py:61-91)
-    per_rel = {}
-    chosen = []
-    for i, r in enumerate(mined):
-        if per_rel.get(r[0], 0) < CFG["rules_per_relation"]:
-            per_rel[r[0]] = per_rel.get(r[0], 0) + 1
-            chosen.append(i)
-    rules = [list(mined[i]) for i in chosen]
-    prior = [rule_weight(i) for i in chosen]
-    out["em/rule_index"] = np.asarray(chosen, np.int64)
+    # ---- one EM iteration (run_rnnlogic.py:67-91), starting from sample()
+    sampled = solver_g.sample(**CFG["sample"])
+    out["em/sampled"] = np.array(json.dumps(sampled))
+    out["probe/sample"] = probe()
+    prior = [rule[-1] for rule in sampled]
+    rules = [rule[0:-1] for rule in sampled]
     predictor = MG.R_pred.Predictor(graph, entity_feature="bias")
     predictor.set_rules([list(r) for r in rules])
     for k, v in predictor.state_dict().items():
@@ -147,7 +144,7 @@ def main():
         solver_g.train(dataset, **CFG["m_step"])
     out["m_step/loss"] = lg.numbers(2)
     out["probe/m_step"] = probe()
-    out["m_step/log_prob"] = np.asarray(solver_g.log_probability([list(mined[i]) for i in chosen]), np.float64)
+    out["m_step/log_prob"] = np.asarray(solver_g.log_probability([list(r[:-1]) for r in rules]), np.float64)
     for k, v in gen.state_dict().items():
         out["gen_m/" + k] = v.numpy().copy()
 
