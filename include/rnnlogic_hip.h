@@ -240,7 +240,15 @@ int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t poo
  * index node - root < ld, ld >= max_head_nodes): pos[q*ld + k] = path count
  * of node k at all_t[q], tot[q*ld + k] = its sum over all candidates.  The
  * caller zero-fills pos.  compute_H's pos_score / neg_score
- * (predictors.py:106-113) are w x pos and w x tot / n_cand. */
+ * (predictors.py:106-113) are w x pos and w x tot / n_cand.
+ *
+ * rnnl_predictor_backward: after rnnl_predictor_forward on the same
+ * workspace, the gradient of the scores with respect to the per-node weight
+ * sums: grad_node[n] += sum over every (q, t) of count_n(q, t) x
+ * grad_score[q * n_entities + t] (fp64; caller zero-fills n_nodes values).
+ * A rule's weight gradient is its node's (rules ending at one node share their
+ * counts) — the backward of `score += x * rule_weights[index]`
+ * (predictors.py:62-66) that trainer.py:90's loss.backward() takes. */
 int rnnl_linear_node_weights_size(rnnl_rules r, size_t *bytes);
 int rnnl_linear_node_weights(rnnl_rules r, const float *rule_weights, int32_t n_rules, void *node_w, void *stream);
 int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32_t feature, const int64_t *all_h,
@@ -250,6 +258,9 @@ int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32
 int rnnl_predictor_rule_stats(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
                               rnnl_rules r, const int64_t *all_r, const int64_t *all_t, int32_t ld, int64_t *pos,
                               int64_t *tot, void *stream);
+int rnnl_predictor_backward(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
+                            rnnl_rules r, const int64_t *all_r, int32_t n_entities, const float *grad_score,
+                            int32_t ld, double *grad_node, void *stream);
 
 /* --------------------------------------------------------- entity feature --
  * Base-score fills (reference src/predictors.py:260-269). */

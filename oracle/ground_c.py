@@ -30,6 +30,7 @@ def _lib():
     lib = ctypes.CDLL(LIB)
     lib.oracle_digests.restype = ctypes.c_int
     lib.oracle_query_candidates.restype = ctypes.c_int
+    lib.oracle_query_stats.restype = ctypes.c_int
     lib.oracle_mix64.restype = ctypes.c_uint64
     lib.oracle_mix64.argtypes = [ctypes.c_uint64]
     return lib
@@ -109,6 +110,42 @@ class Oracle:
                                      ctypes.c_int(threads or os.cpu_count() or 1), _ptr(d), _ptr(c), _ptr(w))
         assert rc == 0
         return (d, c, w) if work else (d, c)
+
+
+    def query_stats(self, h, r, t, rm_src=None, rm_dst=None, weights=None, threads=None):
+        """The EM Predictor's integer work per query (oracle_query_stats):
+        returns (rq_ptr (n+1,), pos, tot) — for query q and the k-th rule of
+        its relation (file order), pos[rq_ptr[q] + k] = paths h -> t and
+        tot[...] = paths h -> any entity — and, with `weights` (per global
+        rule id), also (cand_ptr (n+1,), cand (entity, sorted per query),
+        score = sum_rho count_rho * w_rho in float64)."""
+        h = np.ascontiguousarray(h, dtype=np.int32)
+        r = np.ascontiguousarray(r, dtype=np.int32)
+        t = np.ascontiguousarray(t, dtype=np.int32)
+        rs = np.ascontiguousarray(rm_src, dtype=np.int32) if rm_src is not None else None
+        rd = np.ascontiguousarray(rm_dst, dtype=np.int32) if rm_dst is not None else None
+        n = len(h)
+        nrq = np.diff(self.rules.rh_ptr).astype(np.int64)[r]
+        rq_ptr = np.zeros(n + 1, np.int64)
+        np.cumsum(nrq, out=rq_ptr[1:])
+        pos = np.zeros(max(int(rq_ptr[-1]), 1), np.int64)
+        tot = np.zeros_like(pos)
+        threads = threads or os.cpu_count() or 1
+        cand_ptr = out_t = out_s = w = None
+        if weights is not None:
+            _, nc = self.digests(h, r, rs, rd, threads=threads)
+            cand_ptr = np.zeros(n + 1, np.int64)
+            np.cumsum(nc.astype(np.int64), out=cand_ptr[1:])
+            out_t = np.zeros(max(int(cand_ptr[-1]), 1), np.int32)
+            out_s = np.zeros(len(out_t), np.float64)
+            w = np.ascontiguousarray(weights, dtype=np.float64)
+        rc = self.lib.oracle_query_stats(*self._args(), _ptr(h), _ptr(r), _ptr(rs), _ptr(rd), _ptr(t), ctypes.c_int(n),
+                                         ctypes.c_int(threads), _ptr(w), _ptr(rq_ptr), _ptr(pos), _ptr(tot),
+                                         _ptr(cand_ptr), _ptr(out_t), _ptr(out_s))
+        assert rc == 0
+        if weights is None:
+            return rq_ptr, pos, tot
+        return rq_ptr, pos, tot, cand_ptr, out_t[:cand_ptr[-1]], out_s[:cand_ptr[-1]]
 
 
 class RefMiner:

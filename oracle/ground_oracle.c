@@ -72,8 +72,28 @@ static void scratch_free(scratch_t *s) {
   free(s->sum); free(s->fp); free(s->cand);
 }
 
-/* Ground every rule of head r from h; accumulate sum/fp per candidate. */
+/* Per-rule statistics of one query (Predictor, reference predictors.py:53-119):
+ * for rule position k of the head's list, pos[k] = count at the true tail t,
+ * tot[k] = sum of counts over all destinations; wsum[t] += count * w[rule id]
+ * accumulates the EM Predictor's score in double. */
+typedef struct {
+  int t;
+  int64_t *pos, *tot;
+  const double *w;
+  double *wsum;             /* |E|, cleared by the caller */
+} rule_stats_t;
+
+/* Ground every rule of head r from h; accumulate sum/fp per candidate
+ * (and, when st != NULL, the per-rule statistics). */
+static void ground_query_st(const graph_t *g, scratch_t *s, int h, int r, int rm_src, int rm_dst,
+                            rule_stats_t *st);
+
 static void ground_query(const graph_t *g, scratch_t *s, int h, int r, int rm_src, int rm_dst) {
+  ground_query_st(g, s, h, r, rm_src, rm_dst, NULL);
+}
+
+static void ground_query_st(const graph_t *g, scratch_t *s, int h, int r, int rm_src, int rm_dst,
+                            rule_stats_t *st) {
   const int R = g->R;
   s->n_cand = 0;
   for (int rule = g->rh_ptr[r]; rule < g->rh_ptr[r + 1]; ++rule) {
@@ -103,11 +123,20 @@ static void ground_query(const graph_t *g, scratch_t *s, int h, int r, int rm_sr
       ncur = nnxt;
     }
     const uint64_t m = mix64((uint64_t)g->rid[rule]);
+    const int k = rule - g->rh_ptr[r];
+    if (st) {
+      st->pos[k] = s->cur_c[st->t];
+      st->tot[k] = 0;
+    }
     for (int i = 0; i < ncur; ++i) {
       const int t = s->cur_v[i];
       const int64_t c = s->cur_c[t];
       s->cur_c[t] = 0;
       if (c == 0) continue;
+      if (st) {
+        st->tot[k] += c;
+        if (st->w) st->wsum[t] += (double)c * st->w[g->rid[rule]];
+      }
       s->P += 1;
       if (s->sum[t] == 0) s->cand[s->n_cand++] = t;
       s->sum[t] += c;
@@ -201,6 +230,78 @@ int oracle_digests(const int64_t *off, const int32_t *col, int R, int E, const i
   for (int i = 0; i < nthreads; ++i) {
     jobs[i] = (job_t){&g, qh, qr, rm_src, rm_dst, nq, nthreads, i, digest, ncand, work, 0};
     pthread_create(&th[i], NULL, worker, &jobs[i]);
+  }
+  int ok = 1;
+  for (int i = 0; i < nthreads; ++i) {
+    pthread_join(th[i], NULL);
+    ok &= jobs[i].ok;
+  }
+  free(th);
+  free(jobs);
+  return ok ? 0 : 1;
+}
+
+typedef struct {
+  const graph_t *g;
+  const int32_t *qh, *qr, *qrs, *qrd, *qt;
+  int nq, nthreads, tid;
+  const double *w;
+  const int64_t *rq_ptr, *cand_ptr;
+  int64_t *pos, *tot;
+  int32_t *out_t;
+  double *out_score;
+  int ok;
+} stats_job_t;
+
+static void *stats_worker(void *arg) {
+  stats_job_t *j = (stats_job_t *)arg;
+  scratch_t s;
+  double *wsum = calloc(j->g->E, sizeof(double));
+  if (!scratch_init(&s, j->g->E) || !wsum) { scratch_free(&s); free(wsum); j->ok = 0; return NULL; }
+  j->ok = 1;
+  for (int q = j->tid; q < j->nq; q += j->nthreads) {
+    rule_stats_t st = {j->qt[q], j->pos + j->rq_ptr[q], j->tot + j->rq_ptr[q], j->w, wsum};
+    ground_query_st(j->g, &s, j->qh[q], j->qr[q], j->qrs ? j->qrs[q] : -1, j->qrd ? j->qrd[q] : -1, &st);
+    const int n = s.n_cand;
+    if (j->out_t && j->cand_ptr[q + 1] - j->cand_ptr[q] != n) { j->ok = 0; }
+    qsort(s.cand, n, sizeof(int32_t), cmp_int);
+    for (int i = 0; i < n; ++i) {
+      const int t = s.cand[i];
+      if (j->ok && j->out_t) {
+        j->out_t[j->cand_ptr[q] + i] = t;
+        j->out_score[j->cand_ptr[q] + i] = wsum[t];
+      }
+      wsum[t] = 0.0;
+      s.sum[t] = 0;
+      s.fp[t] = 0;
+    }
+  }
+  scratch_free(&s);
+  free(wsum);
+  return NULL;
+}
+
+/* The EM Predictor's integer work per query, over `nthreads` pthreads:
+ * per rule position k of the query relation's rules (file order),
+ * pos[rq_ptr[q] + k] = paths h -> t along the rule, tot[...] = paths h -> any
+ * destination (compute_H's inputs, predictors.py:82-119); and, when out_t is
+ * not NULL, the candidates sorted by entity with their score
+ * sum_rho count_rho * w[rho] in double (predictors.py:53-80) at cand_ptr[q]
+ * (cand_ptr from the candidate counts of oracle_digests).  Returns 0 on
+ * success. */
+int oracle_query_stats(const int64_t *off, const int32_t *col, int R, int E, const int32_t *rh_ptr,
+                       const int32_t *bptr, const int32_t *body, const int32_t *rid, const int32_t *qh,
+                       const int32_t *qr, const int32_t *rm_src, const int32_t *rm_dst, const int32_t *qt,
+                       int nq, int nthreads, const double *w, const int64_t *rq_ptr, int64_t *pos,
+                       int64_t *tot, const int64_t *cand_ptr, int32_t *out_t, double *out_score) {
+  graph_t g = {off, col, R, E, rh_ptr, bptr, body, rid};
+  if (nthreads < 1) nthreads = 1;
+  pthread_t *th = malloc(sizeof(pthread_t) * nthreads);
+  stats_job_t *jobs = malloc(sizeof(stats_job_t) * nthreads);
+  for (int i = 0; i < nthreads; ++i) {
+    jobs[i] = (stats_job_t){&g, qh, qr, rm_src, rm_dst, qt, nq, nthreads, i, w, rq_ptr, cand_ptr, pos, tot,
+                            out_t, out_score, 0};
+    pthread_create(&th[i], NULL, stats_worker, &jobs[i]);
   }
   int ok = 1;
   for (int i = 0; i < nthreads; ++i) {

@@ -380,6 +380,18 @@ def predictor_compute_H(sd, g, rules, h, r, t, edges_to_remove):
     return (e / e.sum(-1, keepdims=True)).sum(0).astype(np.float32), np.asarray(index, dtype=np.int64)
 
 
+def predictor_H_rows(w, pos, tot, ncand):
+    """Per-row compute_H terms (predictors.py:109-117) from integer path
+    statistics of one row's rules: pos = count at t, tot = sum of counts over
+    candidates, ncand = #candidates, w = the rules' weights.  Returns the
+    row's softmax over its rules (float64): pos_score = w * pos (one-hot
+    divided by 1), neg_score = w * tot / max(ncand, 1)."""
+    w = np.asarray(w, np.float64)
+    h = w * np.asarray(pos, np.float64) - w * np.asarray(tot, np.float64) / max(int(ncand), 1)
+    h = np.exp(h - h.max())
+    return h / h.sum()
+
+
 # --------------------------------------------------------------------------- evaluation
 def query_ranks(logits, mask, flag, t):
     """(L, H) per query (trainer.py:190-201)."""

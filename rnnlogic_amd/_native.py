@@ -57,6 +57,7 @@ SIGNATURES = [
     ("rnnl_predictor_forward", ctypes.c_int,
      [_P, _P, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_predictor_rule_stats", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
+    ("rnnl_predictor_backward", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _I32, _P, _I32, _P, _P]),
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_debug_clock", ctypes.c_int, [_P]),
     ("rnnl_debug_capacity", ctypes.c_int, [_I64, _I64, _I64]),

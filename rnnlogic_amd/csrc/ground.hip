@@ -2478,6 +2478,41 @@ __global__ __launch_bounds__(BS) void rule_stats_kernel(KParams p, const int64_t
   }
 }
 
+// Predictor.forward's gradient (the backward of predictors.py:62-66 under
+// trainer.py:86-90): d score[q, t] / d rule_weights[rho] = count_rho(q, t), and
+// rules ending at one trie node share the count, so per node
+// grad_node[n] = sum over (q, t) of count_n(q, t) x grad_score[q, t].  One
+// workgroup per row (grid-stride): the row's contributions are summed in LDS
+// (fp64, one slot per node of the head's trie), then one global fp64 atomic
+// per (row, touched node).  The caller zero-fills grad_node.
+__global__ __launch_bounds__(BS) void predictor_backward_kernel(KParams p, const float *__restrict__ grad, int ld,
+                                                                double *__restrict__ grad_node) {
+  extern __shared__ double s_g[];
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    const int nc = p.n_cand[q];
+    if (nc <= 0) continue;
+    const int r = (int)p.all_r[q];
+    const int root = p.rl.head_root[r], nh = min(p.rl.head_nodes[r], ld);
+    for (int i = threadIdx.x; i < nh; i += BS) s_g[i] = 0.0;
+    __syncthreads();
+    const int64_t qb = p.q_base[q];
+    const float *__restrict__ gq = grad + (int64_t)q * p.g.E;
+    for (int s = threadIdx.x; s < nc; s += BS) {
+      const int4 cr = p.cand[qb + s];
+      const double g = (double)gq[cr.x];
+      if (g == 0.0) continue;
+      for (int e = cr.y; e < cr.y + cr.z; ++e) {
+        const int2 be = p.bent[e];
+        atomicAdd(&s_g[be.x - root], (double)(uint32_t)be.y * g);
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nh; i += BS)
+      if (s_g[i] != 0.0) atomicAdd(&grad_node[root + i], s_g[i]);
+    __syncthreads();
+  }
+}
+
 }  // namespace rnnl
 
 using namespace rnnl;
@@ -2910,6 +2945,29 @@ int rnnl_predictor_rule_stats(void *ws, int32_t nq, int32_t scale, const int32_t
   hipLaunchKernelGGL(rule_stats_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(BS), (size_t)ld * 8,
                      (hipStream_t)stream, p, all_t, ld, reinterpret_cast<long long *>(pos),
                      reinterpret_cast<long long *>(tot));
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictor_backward(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand, rnnl_rules r,
+                            const int64_t *all_r, int32_t n_entities, const float *grad_score, int32_t ld,
+                            double *grad_node, void *stream) {
+  if (!ws || nq < 0 || scale < 1 || !n_cand || !r || !all_r || !grad_score || !grad_node || n_entities <= 0 ||
+      ld < r->d.max_head_nodes || ld < 1) {
+    set_error("rnnl_predictor_backward: bad arguments (ld >= max_head_nodes)");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  if ((int64_t)ld * 8 > 64 * 1024) {
+    set_error("rnnl_predictor_backward: head trie too large for the LDS table");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p = export_params(ws, nq, scale, n_cand);
+  p.rl = r->d;
+  p.all_r = all_r;
+  p.g.E = n_entities;
+  hipLaunchKernelGGL(predictor_backward_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(BS),
+                     (size_t)ld * 8, (hipStream_t)stream, p, grad_score, ld, grad_node);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

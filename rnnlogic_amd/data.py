@@ -215,11 +215,45 @@ class _DeviceLists(object):
         return out
 
 
-def _batch_rows(batches, indices, device):
-    """(all_h, all_r, all_t) of the concatenated batches[indices], on device."""
-    flat = [x for i in indices for x in batches[i]]
-    hrt = torch.tensor(flat, dtype=torch.int64).view(-1, 3).to(device, non_blocking=True)
-    return hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
+class _RowTable(object):
+    """A dataset's batches as one (n, 3) int64 (h, r, t) table on the device
+    with per-batch offsets, uploaded once and rebuilt when the batch list
+    changes: another list object (make_batches) or a batch object replaced or
+    moved inside it (one identity check per batch; the table keeps references
+    to the batches it was built from, so a recycled id cannot alias).  A
+    single batch is then a slice of the table (no host->device copy per step)
+    and many batches one gather."""
+
+    def __init__(self, device):
+        self.device = device
+        self._src = None
+        self._refs = ()
+
+    def get(self, batches):
+        if self._src is not batches or len(self._refs) != len(batches) or \
+                any(a is not b for a, b in zip(self._refs, batches)):
+            lens = np.fromiter((len(b) for b in batches), dtype=np.int64, count=len(batches))
+            off = np.zeros(len(batches) + 1, dtype=np.int64)
+            np.cumsum(lens, out=off[1:])
+            flat = np.asarray([x for b in batches for x in b], dtype=np.int64).reshape(-1, 3)
+            self.tab = torch.from_numpy(flat).to(self.device)
+            self.lens, self.off = lens, off
+            self._src, self._refs = batches, tuple(batches)
+        return self.tab, self.lens, self.off
+
+    def batch(self, batches, i):
+        tab, _, off = self.get(batches)
+        hrt = tab[int(off[i]):int(off[i + 1])]
+        return hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
+
+    def rows(self, batches, indices):
+        tab, lens, off = self.get(batches)
+        idx = np.asarray(list(indices), dtype=np.int64)
+        n = lens[idx]
+        # positions of the selected batches' rows, in the order of `indices`
+        sel = np.repeat(off[idx] - (np.cumsum(n) - n), n) + np.arange(int(n.sum()), dtype=np.int64)
+        hrt = tab[torch.from_numpy(sel).to(self.device, non_blocking=True)]
+        return hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
 
 
 class DeviceTrainBatches(object):
@@ -229,7 +263,8 @@ class DeviceTrainBatches(object):
     multi-hot target comes from rnnl_multi_hot over a CSR of hr2o (keys
     r * |E| + h, built once); the row's own relation-local edge id
     (relation2ht2index) from a sorted key table of all train edges.  Follows
-    `train_set.batches`, so a make_batches() reshuffle is seen."""
+    `train_set.batches` (a device table of its rows, rebuilt when
+    make_batches() reshuffles them)."""
 
     def __init__(self, train_set, device):
         self.train_set = train_set
@@ -249,6 +284,7 @@ class DeviceTrainBatches(object):
         o = np.argsort(ek, kind="stable")
         self.edge_keys = torch.from_numpy(ek[o]).to(self.device)
         self.edge_ids = torch.from_numpy(ev[o]).to(self.device)
+        self.table = _RowTable(self.device)
 
     def __len__(self):
         return len(self.train_set)
@@ -256,7 +292,7 @@ class DeviceTrainBatches(object):
     def __getitem__(self, idx):
         g = self.train_set.graph
         E = g.entity_size
-        all_h, all_r, all_t = _batch_rows(self.train_set.batches, [idx], self.device)
+        all_h, all_r, all_t = self.table.batch(self.train_set.batches, idx)
         B = all_h.numel()
         target = torch.empty((B, E), dtype=torch.float32, device=self.device)
         self.hr2o.rows("rnnl_multi_hot", (all_r * E + all_h).contiguous(), E, target)
@@ -271,7 +307,7 @@ class DeviceTrainBatches(object):
         (their concatenation, in `idx` order), without the dense targets."""
         g = self.train_set.graph
         E = g.entity_size
-        all_h, all_r, all_t = _batch_rows(self.train_set.batches, list(idx), self.device)
+        all_h, all_r, all_t = self.table.rows(self.train_set.batches, idx)
         ekey = (all_r * E + all_t) * E + all_h
         pos = torch.searchsorted(self.edge_keys, ekey).clamp(max=max(self.edge_keys.numel() - 1, 0))
         return all_h, all_r, all_t, self.edge_ids[pos]
@@ -288,35 +324,14 @@ class DeviceEvalBatches(object):
         self.eval_set = eval_set
         self.device = torch.device(device)
         self.lists = _DeviceLists(getattr(eval_set.graph, eval_set.filter_attr), self.device)
+        self.table = _RowTable(self.device)  # the split's rows, gathered per call
 
     def __len__(self):
         return len(self.eval_set)
 
-    def _table(self):
-        """All batches' (h, r, t) rows on the device once, with per-batch
-        offsets, so `rows` gathers a whole split without a Python pass over
-        its triples (an eval set's batches are fixed at construction,
-        reference src/data.py:230-240; rebuilt if the list is replaced)."""
-        batches = self.eval_set.batches
-        key = (id(batches), len(batches))
-        if getattr(self, "_tab_key", None) != key:
-            lens = np.fromiter((len(b) for b in batches), dtype=np.int64, count=len(batches))
-            off = np.zeros(len(batches) + 1, dtype=np.int64)
-            np.cumsum(lens, out=off[1:])
-            flat = np.asarray([x for b in batches for x in b], dtype=np.int64).reshape(-1, 3)
-            self._tab = (torch.from_numpy(flat).to(self.device), lens, off)
-            self._tab_key = key
-        return self._tab
-
     def rows(self, indices):
         E = self.eval_set.graph.entity_size
-        tab, lens, off = self._table()
-        idx = np.asarray(list(indices), dtype=np.int64)
-        n = lens[idx]
-        # positions of the selected batches' rows, in the order of `indices`
-        sel = np.repeat(off[idx] - (np.cumsum(n) - n), n) + np.arange(int(n.sum()), dtype=np.int64)
-        hrt = tab[torch.from_numpy(sel).to(self.device, non_blocking=True)]
-        all_h, all_r, all_t = hrt[:, 0].contiguous(), hrt[:, 1].contiguous(), hrt[:, 2].contiguous()
+        all_h, all_r, all_t = self.table.rows(self.eval_set.batches, indices)
         flag = torch.empty((all_h.numel(), E), dtype=torch.bool, device=self.device)
         if all_h.numel():
             self.lists.rows("rnnl_filter_flags", (all_r * E + all_h).contiguous(), E, flag.view(torch.uint8))

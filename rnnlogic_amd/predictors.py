@@ -33,6 +33,10 @@ from .embedding import RotatE
 from .layers import MLP, FuncToNode, FuncToNodeSum
 
 
+# training-path LSTM input padded to one shape (RNNL_TRAIN_LSTM_PAD=0: per-relation shapes, for A/B)
+_PAD_TRAIN_LSTM = os.environ.get("RNNL_TRAIN_LSTM_PAD", "1") != "0"
+
+
 def _read_rules(input):
     """Rule list/file -> [(head, [body...])] (predictors.py:27-41, 166-182)."""
     rules = []
@@ -134,6 +138,8 @@ class _HipGrounding(object):
                              self.capacity_scale)
                 continue
             _native.check(rc)
+            # launch generation: a saved workspace is stale once this moves on
+            self._ws_gen[device] = self._ws_gen.get(device, 0) + 1
             return ws, scale
 
     def ground(self, all_h, all_r, edges_to_remove=None, totals=None):
@@ -191,6 +197,49 @@ class _HipGrounding(object):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
 
+class _PredictorLinear(torch.autograd.Function):
+    """Predictor.forward under autograd (predictors.py:53-80): the HIP forward
+    (rnnl_predictor_forward) and its backward (rnnl_predictor_backward: per
+    trie node the sum of count x incoming gradient, shared by the node's
+    rules; the bias gradient is the column sum).  The grounding stays in the
+    model's workspace between the two; if another launch has reused it by
+    the time backward runs, the rows are grounded again (same COO)."""
+
+    @staticmethod
+    def forward(ctx, rule_weights, bias, model, all_h, all_r, edges_to_remove):
+        score, mask, n_cand, ws, scale = model._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
+        device = score.device
+        ctx.model, ctx.ws, ctx.scale, ctx.n_cand = model, ws, scale, n_cand
+        ctx.gen = model._ws_gen.get(device)
+        ctx.rows = model._rows(all_h, all_r, edges_to_remove)[1:]
+        ctx.has_bias = bias is not None
+        ctx.mark_non_differentiable(mask)
+        return score, mask
+
+    @staticmethod
+    def backward(ctx, grad_score, grad_mask):
+        model = ctx.model
+        all_h, all_r, etr = ctx.rows
+        device = all_h.device
+        nq = all_h.numel()
+        gw = gb = None
+        if nq and ctx.needs_input_grad[0]:
+            ws, scale, n_cand = ctx.ws, ctx.scale, ctx.n_cand
+            if model._ws_gen.get(device) != ctx.gen:  # the workspace was reused: ground again
+                ws, scale, n_cand = model.ground(all_h, all_r, etr)
+            nr = model.native_rules(device)
+            _, ld = model.head_roots(device)
+            g = grad_score.contiguous().float()
+            grad_node = torch.zeros(max(nr.n_nodes, 1), dtype=torch.float64, device=device)
+            _native.call("rnnl_predictor_backward", ws.data_ptr(), nq, scale, n_cand.data_ptr(), nr.ptr,
+                         all_r.data_ptr(), model.num_entities, g.data_ptr(), ld, grad_node.data_ptr(),
+                         torch.cuda.current_stream(device).cuda_stream)
+            gw = grad_node.index_select(0, nr.node_of_rule).to(model.rule_weights.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[1]:
+            gb = grad_score.sum(0)
+        return gw, gb, None, None, None, None
+
+
 class Predictor(_HipGrounding, torch.nn.Module):
     """Rule-weight predictor of the EM loop (reference src/predictors.py:17-119).
 
@@ -212,6 +261,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         self._ws = {}
         self._lin_cache = {}
         self._roots = {}
+        self._ws_gen = {}  # per device: launches on the workspace so far
         self.capacity_scale = 1
 
     def set_rules(self, input):
@@ -258,12 +308,25 @@ class Predictor(_HipGrounding, torch.nn.Module):
     def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False):
         """Forward for any rows (one or many reference batches, mixed
         relations): (score (n, |E|) f32, mask (n, |E|) bool[, n_cand])."""
+        score, mask, n_cand, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
+        return (score, mask, n_cand) if return_ncand else (score, mask)
+
+    def _forward_launch(self, all_h, all_r, edges_to_remove, single_relation=False):
+        """rnnl_predictor_forward over the rows -> (score, mask, n_cand, ws,
+        scale); the workspace keeps the grounding for a backward.  With
+        `single_relation` the reference's one-relation-per-batch check
+        (predictors.py:54-55) is read back with the launch status (no extra
+        host sync)."""
         device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
         nq, E = all_h.numel(), self.num_entities
         if nq == 0:  # no rows: empty outputs, no launch
-            out = (torch.empty((0, E), dtype=torch.float32, device=device),
-                   torch.empty((0, E), dtype=torch.bool, device=device))
-            return out + (torch.empty(0, dtype=torch.int32, device=device),) if return_ncand else out
+            return (torch.empty((0, E), dtype=torch.float32, device=device),
+                    torch.empty((0, E), dtype=torch.bool, device=device),
+                    torch.empty(0, dtype=torch.int32, device=device), None, None)
+        mixed = None
+        if single_relation:
+            mixed = torch.empty((), dtype=torch.bool, pin_memory=True)
+            mixed.copy_((all_r != all_r[0]).any(), non_blocking=True)
         g, nr = self.graph.device_graph(device), self.native_rules(device)
         node_w = self.node_weights(device)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -284,22 +347,31 @@ class Predictor(_HipGrounding, torch.nn.Module):
                          all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
                          mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(), ws.data_ptr(),
                          ws.numel(), scale, stream)
-        self._launch(device, nq, run)
+        ws, scale = self._launch(device, nq, run)
+        if mixed is not None:
+            assert not bool(mixed), "a batch must hold one relation (predictors.py:54-55)"
         mask = torch.ones((nq, E), dtype=torch.bool, device=device) if bias_mode else mask8.bool()
-        return (score, mask, n_cand) if return_ncand else (score, mask)
+        return score, mask, n_cand, ws, scale
 
     # ------------------------------------------------------------------ reference API
+    # every entity is scored (the reference's mask is all True) with the bias feature
+    @property
+    def mask_all_true(self):
+        return self.entity_feature == "bias"
+
     def forward(self, all_h, all_r, edges_to_remove):
-        """predictors.py:53-80: one single-relation batch -> (score, mask)."""
-        # the reference's single-relation check (predictors.py:54-55) in one host read
-        query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
-        assert n_other == 0
+        """predictors.py:53-80: one single-relation batch -> (score, mask).
+        With autograd (training) the same HIP forward runs inside
+        _PredictorLinear, whose backward is rnnl_predictor_backward."""
         if self._needs_grad():
-            return self.forward_autograd(all_h, all_r, edges_to_remove)
-        score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
-        if self.entity_feature != "bias" and int(n_cand.sum().item()) == 0:
-            # early return `mask - float('-inf')` (predictors.py:68-72): +inf, mask all False
-            score.fill_(float("inf"))
+            bias = self.bias if self.entity_feature == "bias" else None
+            score, mask = _PredictorLinear.apply(self.rule_weights, bias, self, all_h, all_r, edges_to_remove)
+        else:
+            score, mask, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
+        if self.entity_feature != "bias":
+            # early return `mask - float('-inf')` (predictors.py:68-72): +inf where the
+            # batch has no candidate at all (mask all False), without a host read
+            score = torch.where(mask.any(), score, torch.full_like(score, float("inf")))
         return score, mask
 
     def forward_autograd(self, all_h, all_r, edges_to_remove):
@@ -468,6 +540,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._ws = {}
         self._ws_chunks = {}
         self._side = {}
+        self._ws_gen = {}
         self.capacity_scale = 1
         # RotatE base score: the grounding runs on a side stream beside the
         # RotatE kernel; rows may be split into chunks so that each chunk's
@@ -503,6 +576,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self.relation2rules[rule[0]].append([index, rule])
         self.rule_features = torch.tensor(
             [[h] + b + [self.padding_index] * (self.max_length - len(b)) for h, b in self.rules], dtype=torch.long)
+        self._max_rules_per_relation = max(len(x) for x in self.relation2rules)
         if self.type == "emb":
             self.rule_emb = nn.parameter.Parameter(torch.zeros(self.num_rules, self.hidden_dim))
             nn.init.kaiming_uniform_(self.rule_emb, a=math.sqrt(5), mode="fan_in")
@@ -835,11 +909,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         C = ent.numel()
         nr = self.native_rules(device)
         rels = [rels] if isinstance(rels, int) else torch.unique(all_r).tolist()
-        ridx = torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
+        ridx = self._rule_ids(rels, device)
         if self.type == "emb":
             x_f = self.rule_emb.index_select(0, ridx)
         else:
-            x_f = self.encode_rules(self.rule_features.to(device)[ridx])
+            x_f = self._encode_rules_padded(ridx, device)
         nodes = nr.node_of_rule[ridx]
         H = self.hidden_dim
         # gathers of differentiable tables use index_select: its backward is an
@@ -877,6 +951,41 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             return score + rot, torch.ones((nq, E), dtype=torch.bool, device=device)
         mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
         return score.masked_fill(~mask, float("-inf")), mask
+
+    def _rule_ids(self, rels, device):
+        """Device int64 ids of the rules of relations `rels` (relation order,
+        then file order); one relation's list is uploaded once and cached."""
+        if len(rels) == 1:
+            key = ("rids", self._device_index(device), rels[0])
+            hit = self._tok_cache.get(key)
+            if hit is None:
+                hit = torch.tensor([i for i, _ in self.relation2rules[rels[0]]], dtype=torch.long, device=device)
+                self._tok_cache[key] = hit
+            return hit
+        return torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
+
+    def _encode_rules_padded(self, ridx, device):
+        """encode_rules over the rules `ridx` with autograd (the training
+        path).  The token table lives on the device (uploaded once), and the
+        LSTM input is padded to a fixed row count — the largest per-relation
+        rule list, or a multiple of 512 beyond it — so the recurrent kernels
+        see one shape, not one per relation (a new RNN shape costs a kernel
+        selection on its first use).  The padding rows repeat rule 0; their
+        outputs are dropped, so they add nothing to the gradients."""
+        key = ("tok64", self._device_index(device))
+        tok = self._tok_cache.get(key)
+        if tok is None:
+            tok = self.rule_features.to(device)
+            self._tok_cache[key] = tok
+        n = ridx.numel()
+        rows = max(self._max_rules_per_relation, 1)
+        if n > rows:
+            rows = (n + 511) // 512 * 512
+        if not _PAD_TRAIN_LSTM:  # A/B: one LSTM shape per relation
+            rows = n
+        if rows > n:
+            ridx = torch.cat([ridx, ridx.new_zeros(rows - n)])
+        return self.encode_rules(tok.index_select(0, ridx))[:n]
 
     def forward(self, all_h, all_r, edges_to_remove):
         """predictors.py:210-271: one single-relation batch -> (score, mask).

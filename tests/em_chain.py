@@ -23,6 +23,18 @@ def fixture():
     return z, json.loads(str(z["cfg"]))
 
 
+def cpu_model():
+    """model name of /proc/cpuinfo (tools/make_golden_em.py stores the fixture's)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def rule_weight(i):
     return 0.25 * ((i * 37) % 11) - 1.0
 

@@ -203,3 +203,46 @@ def test_predictor_trainer_hip(case):
                 np.testing.assert_allclose(prm.grad.detach().cpu().numpy(), want_g, atol=atol, rtol=1e-5)
         optim.step()
         optim.zero_grad()
+
+
+# ----------------------------------------------------------------------------- CPU: the C oracle's EM statistics
+@pytest.mark.parametrize("case", PRED_CASES)
+def test_c_oracle_predictor_stats(case):
+    """oracle_query_stats (per-rule path counts at the true tail and in
+    total, and the Predictor score per candidate) against the reference's
+    compute_H and forward outputs (tests/golden/pred_*.npz) — the checker the
+    FB15k-237 EM test uses at full size."""
+    from oracle import ground_c
+    fx, g, rules = _fixture(case)
+    cg = ground_c.CGraph(g.entity_size, g.relation_size, g.train_facts)
+    orc = ground_c.Oracle(cg, [(hd, list(b)) for hd, b in rules.rules], g.relation_size)
+    w = fx.sd["rule_weights"].astype(np.float64)
+    heads = np.asarray([hd for hd, _ in rules.rules])
+    for k in range(fx.nH):
+        c = fx.hcall(k)
+        if c["index"].size == 0:
+            continue
+        q = int(c["r"][0])
+        rm_src, rm_dst = g.adj[q][0][c["etr"]], g.adj[q][1][c["etr"]]
+        rq_ptr, pos, tot = orc.query_stats(c["h"], c["r"], c["t"], rm_src, rm_dst)
+        # candidates per row (over all the relation's rules)
+        _, ncand = orc.digests(c["h"], c["r"], rm_src, rm_dst)
+        ids = np.nonzero(heads == q)[0]
+        np.testing.assert_array_equal(ids, c["index"])
+        H = sum(ref.predictor_H_rows(w[ids], pos[rq_ptr[i]:rq_ptr[i + 1]], tot[rq_ptr[i]:rq_ptr[i + 1]], ncand[i])
+                for i in range(len(c["h"])))
+        np.testing.assert_allclose(H, c["H"], atol=1e-5, rtol=0)
+    for k in range(0, fx.ncalls, 3):
+        c = fx.call(k)
+        if not c["mask"].any() and fx.cfg["feature"] != "bias":
+            continue
+        q = int(c["r"][0])
+        rm = (g.adj[q][0][c["etr"]], g.adj[q][1][c["etr"]]) if c["etr"] is not None else (None, None)
+        rq_ptr, pos, tot, cptr, cand, sc = orc.query_stats(c["h"], c["r"], c["t"], rm[0], rm[1], weights=w)
+        for i in range(len(c["h"])):
+            e, v = cand[cptr[i]:cptr[i + 1]], sc[cptr[i]:cptr[i + 1]]
+            if fx.cfg["feature"] == "bias":
+                v = v + fx.sd["bias"][e]
+            else:
+                np.testing.assert_array_equal(np.nonzero(c["mask"][i])[0], e)
+            np.testing.assert_allclose(c["score"][i, e], v, atol=1e-5, rtol=1e-6)

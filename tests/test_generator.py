@@ -73,13 +73,16 @@ def _check_sample(got, want_json):
 
 def test_generator_chain_cpu():
     z, got = em_chain.run(torch.device("cpu"))
-    # on the CPU the pre-training reproduces the reference's weights bitwise
-    # (same batches, same gathered loss sums, same Adam), hence sample()'s
-    # log-probabilities and its set order too
-    _check_generator_part(z, got, w_tol=0.0)
+    # on the CPU model the fixture was made on, the pre-training reproduces the
+    # reference's weights bitwise (same batches, same gathered loss sums, same
+    # Adam), hence sample()'s log-probabilities and its set order too; another
+    # CPU's vector code rounds the LSTM GEMMs differently (W_TOL then)
+    same_cpu = "cpu" in z.files and str(z["cpu"]) == em_chain.cpu_model()
+    _check_generator_part(z, got, w_tol=0.0 if same_cpu else W_TOL)
     exact = _check_sample(got["em/sampled"], z["em/sampled"])
-    print("sample(): %d rules, bitwise log p and order: %s" % (len(got["em/sampled"]), exact))
-    assert exact
+    print("sample(): %d rules, bitwise log p and order: %s (fixture CPU: %s)" % (len(got["em/sampled"]), exact,
+                                                                               "same" if same_cpu else "other"))
+    assert exact or not same_cpu
     assert np.array_equal(got["probe/sample"], z["probe/sample"])
 
 

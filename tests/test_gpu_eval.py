@@ -7,10 +7,20 @@
   through TrainerPredictor.filtered_ranks on the device and rank_metrics give
   the reference's evaluate() metrics to 1e-12.
 * Per-query ranks of the HIP forward against the reference's per-query
-  (L, H) (tests/golden/eval_<case>.npz, tools/make_golden_eval.py): a query's
-  bounds may differ only by the number of flagged competitors whose reference
-  score lies within 1e-4 (the forward's score tolerance) of the target's,
-  and MRR / Hits deltas are logged.
+  (L, H) (tests/golden/eval_<case>.npz, tools/make_golden_eval.py), held to
+  the score error actually measured, not to a fixed window:
+    - per reference batch, eps = max |HIP - reference| over the targets and
+      16 probe entities per row (the 12 flagged competitors closest to the
+      target's score and 4 random entities; the fixture stores their
+      reference scores); eps <= 2e-5 is required;
+    - a competitor can change sides only if |s_e - s_t| <= 2 eps, so a row's
+      (L, H) may differ from the reference's by at most the number of flagged
+      competitors within the smallest stored window >= 2 eps;
+    - where that window holds no more competitors than the probes, the
+      difference is accounted exactly: dL (dH) = the number of probe
+      competitors that moved above (to at-or-above) the target minus those
+      that moved below;
+  MRR / Hits deltas are logged and |dMRR| is bounded.
 """
 import os
 
@@ -110,16 +120,54 @@ def test_per_query_ranks_vs_reference(case, dev):
         logits, mask = model.forward_rows(h, r, None)
     L, H = TrainerPredictor.filtered_ranks(logits, mask, flag, t, graph.entity_size)
     L, H = L.cpu().numpy(), H.cpu().numpy()
-    dL, dH = np.abs(L - want[:, 3]), np.abs(H - want[:, 4])
-    near = want[:, 5]
-    diff = (dL > 0) | (dH > 0)
-    bad = np.nonzero((dL > near) | (dH > near))[0]
+    n = len(want)
+    # HIP scores at the fixture's target and probe entities
+    pe = z["probe_ent"].astype(np.int64)
+    rows_i = torch.arange(n, device=dev)
+    hip_t = logits[rows_i, t].cpu().numpy().astype(np.float64)
+    hip_p = logits.gather(1, torch.from_numpy(np.maximum(pe, 0)).to(dev)).cpu().numpy().astype(np.float64)
+    hit = mask[rows_i, t].cpu().numpy()
+    ref_t = z["s_t"].astype(np.float64)
+    ref_p = z["probe_score"].astype(np.float64)
+    valid_p = pe >= 0
+    # the target is a candidate in both or in neither (exact mask parity)
+    assert np.array_equal(hit, ~np.isnan(ref_t))
+    err = np.where(valid_p, np.abs(hip_p - ref_p), 0.0).max(1)
+    err = np.maximum(err, np.where(hit, np.abs(hip_t - np.nan_to_num(ref_t)), 0.0))
+    bp = z["batch_ptr"]
+    eps = np.zeros(n)
+    for b in range(nb):
+        eps[bp[b]:bp[b + 1]] = err[bp[b]:bp[b + 1]].max()
+    assert eps.max() <= 2e-5, "score error %g above 2e-5" % eps.max()
+    windows = z["windows"]
+    wi = np.searchsorted(windows, 2 * eps)  # smallest stored window >= 2 eps
+    assert (wi < len(windows)).all()
+    allowed = z["near_w"][np.arange(n), wi]
+    dL, dH = L - want[:, 3], H - want[:, 4]
+    diff = (dL != 0) | (dH != 0)
+    bad = np.nonzero((np.abs(dL) > allowed) | (np.abs(dH) > allowed))[0]
+    assert len(bad) == 0, (bad[:10], L[bad[:10]], H[bad[:10]], want[bad[:10]], allowed[bad[:10]])
+    # exact accounting where the window's competitors are all probes
+    nclose = pe.shape[1] - 4
+    close = valid_p[:, :nclose]
+    exact_rows = np.nonzero(hit & (allowed <= nclose))[0]
+    above_h = (hip_p[:, :nclose] > hip_t[:, None]) & close
+    above_r = (ref_p[:, :nclose] > ref_t[:, None]) & close
+    atleast_h = (hip_p[:, :nclose] >= hip_t[:, None]) & close
+    atleast_r = (ref_p[:, :nclose] >= ref_t[:, None]) & close
+    exp_dL = above_h.sum(1) - above_r.sum(1)
+    exp_dH = atleast_h.sum(1) - atleast_r.sum(1)
+    mism = exact_rows[(dL[exact_rows] != exp_dL[exact_rows]) | (dH[exact_rows] != exp_dH[exact_rows])]
+    assert len(mism) == 0, (mism[:10], dL[mism[:10]], exp_dL[mism[:10]], dH[mism[:10]], exp_dH[mism[:10]])
     got_m = TrainerPredictor.rank_metrics(np.stack([want[:, 0], want[:, 1], want[:, 2], L, H], 1).tolist(), True)
-    msg = "%s: %d rows, %d with differing (L, H) (all within their near-tie counts: %s); " % (
-        case, len(want), int(diff.sum()), "yes" if len(bad) == 0 else "NO")
+    msg = "%s: %d rows / %d batches, score error max %.3g (median batch %.3g); %d rows with differing (L, H), " \
+          "all within their window (%d accounted exactly, %d bounded); " % (
+              case, n, nb, eps.max(), float(np.median(eps[bp[:-1]])), int(diff.sum()),
+              int(diff[exact_rows].sum()), int(diff.sum() - diff[exact_rows].sum()))
     msg += ", ".join("%s delta %.3g" % (k, got_m[k] - float(z["metric/" + k]))
                      for k in ("MRR", "Hit1", "Hit3", "Hit10", "MR"))
     print(msg)
-    assert len(bad) == 0, (bad[:10], L[bad[:10]], H[bad[:10]], want[bad[:10]])
     if not diff.any():
         assert abs(got_m["MRR"] - float(z["metric/MRR"])) <= 1e-12
+    # each differing row moves its reciprocal-rank expectation by < 1 / L
+    assert abs(got_m["MRR"] - float(z["metric/MRR"])) <= max(1e-6, float(diff.sum()) / n)

@@ -54,6 +54,19 @@ def rule_weight(i):
     return 0.25 * ((i * 37) % 11) - 1.0
 
 
+def cpu_model():
+    """The CPU the fixture was made on: CPU float results (LSTM GEMMs) are
+    bitwise reproducible on the same CPU model only."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def probe():
     return torch.randint(0, 2 ** 31 - 1, (4,)).numpy()
 
@@ -84,7 +97,7 @@ def main():
     path = MG.datasets.materialize("umls")
     rule_path = MG.datasets.rule_file("umls")
     mined = [[int(x) for x in line.split()] for line in open(rule_path)]
-    out = dict(cfg=np.array(json.dumps(CFG)))
+    out = dict(cfg=np.array(json.dumps(CFG)), cpu=np.array(cpu_model()))
 
     MG.R_utils.set_seed(CFG["seed"])
     graph = MG.R_data.KnowledgeGraph(path)
