@@ -291,6 +291,129 @@ def kinship_line(dev, reps=50):
                         "(L<=3, top 100 per relation); real train graph"}
 
 
+def per_batch_line(model, graph, test_set, dev):
+    """The reference API's call pattern (src/trainer.py:150-173): one
+    PredictorPlus.forward(all_h, all_r, None) per TestDataset batch (B <= 32,
+    one relation) over the whole split, inputs already on the device.  Its
+    roofline: the RotatE flops of every call over the loop's time (the same
+    kernel as `value`, launched 1,514 times on 32 rows each)."""
+    hs = [torch.tensor([x[0] for x in b], device=dev) for b in test_set.batches]
+    rs = [torch.tensor([x[1] for x in b], device=dev) for b in test_set.batches]
+    with torch.no_grad():
+        for k in range(3):
+            model(hs[k], rs[k], None)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for h, r in zip(hs, rs):
+            model(h, r, None)
+        torch.cuda.synchronize(dev)
+        sec = time.perf_counter() - t0
+    n = sum(len(b) for b in test_set.batches)
+    out = {"queries_per_s": round(n / sec, 1), "ms": round(sec * 1e3, 3), "calls": len(hs),
+           "ms_per_call": round(sec / len(hs) * 1e3, 4), "rows": n,
+           "note": "PredictorPlus.forward once per TestDataset batch (the reference evaluate()'s loop), "
+                   "device-resident inputs; same model as value"}
+    if model.entity_feature == "RotatE":
+        fl = 7.0 * n * graph.entity_size * model.RotatE.emb_dim
+        out["roofline"] = {"bound": "valu", "achieved": round(fl / sec / 1e12, 2), "peak": FP32_PEAK_TFS,
+                           "unit": "TFLOP/s", "frac": round(fl / sec / 1e12 / FP32_PEAK_TFS, 4),
+                           "kernel": "rotate_direct_kernel (RotatE flops of all calls / loop time)"}
+    return out
+
+
+def train_step_line(model, solver, dev, n_steps=10, warmup=2):
+    """TrainerPredictor.train_step (src/trainer.py:72-98) on FB15k-237 train
+    batches with the bench model: per-step times of every timed step (a
+    first-use cost of a new shape shows as an outlier, a steady cost does not)."""
+    from rnnlogic_amd.data import DeviceTrainBatches
+    opt = torch.optim.Adam(model.parameters(), lr=5e-3)
+    solver.optimizer = opt
+    dtb = DeviceTrainBatches(model.train_set, dev)
+    model.train()
+    batches = [[x.unsqueeze(0) for x in dtb[i]] for i in range(warmup + n_steps)]
+    for b in batches[:warmup]:
+        solver.train_step(model, b, 0.2)
+    times, nrow = [], 0
+    for b in batches[warmup:]:
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        solver.train_step(model, b, 0.2, sync=False)
+        torch.cuda.synchronize(dev)
+        times.append((time.perf_counter() - t) * 1e3)
+        nrow += b[0].numel()
+    model.eval()
+    sec = sum(times) * 1e-3
+    return {"queries_per_s": round(nrow / sec, 1), "ms_per_batch": round(sec * 1e3 / n_steps, 3),
+            "ms_per_step": [round(x, 3) for x in times], "batches": n_steps, "rows": nrow,
+            "note": "TrainerPredictor.train_step on FB15k-237 train batches (B=32, edge removal, RotatE feature, "
+                    "Adam): forward + loss + backward + step, each step synchronised"}
+
+
+def em_iteration_line(dev, pre_epochs=200):
+    """One EM iteration of run_rnnlogic.py (src/run_rnnlogic.py:61-91) with
+    config/FB15k-237.yaml's settings on FB15k-237 (BASELINE.json config 5):
+    sample(100, 3) from the generator, a new Predictor(bias) + Adam trained
+    over every train batch (the config's batch_per_epoch 1e6 = all 17,258),
+    evaluate('valid') and ('test'), compute_H over every train row, the
+    posterior and the M-step (generator.train, 100 epochs).  The generator is
+    first pre-trained for `pre_epochs` of the config's 10,000 epochs on
+    rnnlogic_rules.txt with synthetic weights (pre-training happens once per
+    run, before the EM loop; FB's mined_rules.txt needs the absent
+    train.txt) — reported separately, not part of the iteration."""
+    from rnnlogic_amd.data import RuleDataset
+    from rnnlogic_amd.generators import Generator
+    from rnnlogic_amd.predictors import Predictor
+    from rnnlogic_amd.trainer import TrainerGenerator, TrainerPredictor
+    from rnnlogic_amd.utils import set_seed
+
+    def timed(fn):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize(dev)
+        return out, time.perf_counter() - t0
+    with contextlib.redirect_stdout(sys.stderr):
+        set_seed(1)
+        graph = KnowledgeGraph(datasets.materialize("FB15k-237"))
+        train_set, valid_set, test_set = TrainDataset(graph, 32), ValidDataset(graph, 32), TestDataset(graph, 32)
+    mined = [[int(x) for x in line.split()] for line in open(datasets.rule_file("FB15k-237"))]
+    dataset = RuleDataset(graph.relation_size, [r + [0.25 * ((i * 37) % 11) - 1.0] for i, r in enumerate(mined)])
+    gen = Generator(graph, num_layers=1, embedding_dim=512, hidden_dim=256)
+    solver_g = TrainerGenerator(gen, gpu=dev.index or 0)
+    _, t_pre = timed(lambda: solver_g.train(dataset, num_epoch=pre_epochs, lr=1e-3, print_every=1000000,
+                                            batch_size=512))
+    res = {}
+    sampled, res["sample_s"] = timed(lambda: solver_g.sample(100, 3))
+    prior = [r[-1] for r in sampled]
+    rules = [r[:-1] for r in sampled]
+    predictor = Predictor(graph, entity_feature="bias")
+    with contextlib.redirect_stdout(sys.stderr):
+        predictor.set_rules(rules)
+    optim = torch.optim.Adam(predictor.parameters(), lr=1e-3, weight_decay=0)
+    solver_p = TrainerPredictor(predictor, train_set, valid_set, test_set, optim, gpus=[dev.index or 0])
+    _, res["predictor_train_s"] = timed(lambda: solver_p.train(batch_per_epoch=1000000, smoothing=0.2,
+                                                               print_every=1000000))
+    (vm, tm), res["evaluate_s"] = timed(lambda: (solver_p.evaluate("valid"), solver_p.evaluate("test")))
+    H, res["e_step_compute_H_s"] = timed(lambda: solver_p.compute_H(print_every=1000000))
+    posterior = [h + p * 0.001 for h, p in zip(H, prior)]
+    for i in range(len(rules)):
+        rules[i].append(posterior[i])
+    _, res["m_step_s"] = timed(lambda: solver_g.train(RuleDataset(graph.relation_size, rules), num_epoch=100,
+                                                      lr=1e-5, print_every=1000000, batch_size=512))
+    total = sum(res.values())
+    nb = len(train_set)
+    out = {"s": round(total, 3), "phases_s": {k: round(v, 3) for k, v in res.items()},
+           "rules_sampled": len(sampled), "train_batches": nb,
+           "predictor_ms_per_batch": round(res["predictor_train_s"] / nb * 1e3, 3),
+           "valid_mrr": vm, "test_mrr": tm,
+           "pre_train": {"epochs": pre_epochs, "s": round(t_pre, 3), "ms_per_epoch": round(t_pre / pre_epochs * 1e3, 3),
+                         "note": "once per run, before the EM loop; not in `s`"},
+           "workload": "config/FB15k-237.yaml EM iteration (EM.num_rules 100, max_length 3; predictor over all "
+                       "train batches; M-step 100 epochs) on the seeded synthetic FB15k-237 train graph, 1 GPU"}
+    del solver_p, predictor, solver_g, gen
+    return out
+
+
 def algorithmic_work(model, graph, rows, threads):
     """Exact per-rule work counts of the SURVEY §8(d) formula: F (frontier
     expansions), T (edge traversals), P ((rule, dest) pairs) and C
@@ -528,30 +651,14 @@ def main():
                                   "first_call_ms": round(t_first * 1e3, 3), "rows": n_split,
                                   "note": "TrainerPredictor.evaluate('test') end to end (MRR/Hits on the host); "
                                           "the first call also uploads the split's rows and filter lists"}
+        # the reference API's per-batch forward (trainer.py:150-173)
+        extra["per_batch_forward"] = per_batch_line(model, graph, test_set, dev)
         # training steps (trainer.py:72-98): HIP grounding with edge removal,
-        # autograd on the path-count COO + RotatE (torch), Adam
-        opt = torch.optim.Adam(model.parameters(), lr=5e-3)
-        solver.optimizer = opt
-        from rnnlogic_amd.data import DeviceTrainBatches
-        dtb = DeviceTrainBatches(model.train_set, dev)
-        model.train()
-        batches = [[x.unsqueeze(0) for x in dtb[i]] for i in range(12)]
-        for b in batches[:2]:
-            solver.train_step(model, b, 0.2)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        nrow = 0
-        for b in batches[2:]:
-            solver.train_step(model, b, 0.2)
-            nrow += b[0].numel()
-        torch.cuda.synchronize(dev)
-        sec = time.perf_counter() - t1
-        model.eval()
-        extra["train_step"] = {"queries_per_s": round(nrow / sec, 1), "ms_per_batch": round(sec * 1e3 / 10, 3),
-                               "batches": 10, "rows": nrow,
-                               "note": "TrainerPredictor.train_step on FB15k-237 train batches (B=32, edge removal, "
-                                       "RotatE feature, Adam): forward + loss + backward + step"}
-        del solver, opt, dtb, batches
+        # autograd on the path-count COO + RotatE (HIP backward), Adam
+        extra["train_step"] = train_step_line(model, solver, dev)
+        del solver
+        # config 5: one EM iteration of run_rnnlogic.py on FB15k-237
+        extra["em_iteration"] = em_iteration_line(dev)
 
     if rank != 0:
         if world > 1:

@@ -44,11 +44,20 @@ class Generator(torch.nn.Module):
     def loss(self, inputs, target, mask, weight, hidden):
         """Weighted next-token cross entropy over the unpadded positions,
         Σ w_i·CE / Σ w_i with a rule's weight on each of its positions
-        (generators.py:31-37).  The unpadded positions are gathered in
-        row-major order before the sums, as the reference does, so the fp32
-        sums round identically and a seeded run trains to bitwise the same
-        weights (which sample() needs to draw the same rules)."""
+        (generators.py:31-37).  On the CPU the unpadded positions are
+        gathered in row-major order before the sums, as the reference does, so
+        the fp32 sums round identically and a seeded run trains to bitwise the
+        same weights (which sample() needs to draw the reference's rules).  On
+        a GPU (whose reductions round differently from the CPU reference's in
+        any case) the sums run densely with padded positions weighted 0: the
+        same value without the gather's host sync."""
         logits, _ = self.forward(inputs, inputs[:, 0], hidden)
+        if logits.is_cuda:
+            # PAD (= label_size) is not a class: point padded targets at class 0, weight 0
+            tgt = torch.where(mask, target, torch.zeros_like(target))
+            ce = F.cross_entropy(logits.reshape(-1, self.label_size), tgt.reshape(-1), reduction="none")
+            w = (mask.to(logits.dtype) * weight.to(logits.dtype).unsqueeze(1)).reshape(-1)
+            return (ce * w).sum() / w.sum()
         keep = mask.reshape(-1).nonzero().squeeze(1)
         picked = logits.reshape(-1, self.label_size).index_select(0, keep)
         ce = F.cross_entropy(picked, target.reshape(-1).index_select(0, keep), reduction="none")

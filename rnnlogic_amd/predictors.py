@@ -210,6 +210,11 @@ class _PredictorLinear(torch.autograd.Function):
         score, mask, n_cand, ws, scale = model._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
         device = score.device
         ctx.model, ctx.ws, ctx.scale, ctx.n_cand = model, ws, scale, n_cand
+        # a batch without any candidate returns `mask + bias` in the reference
+        # (predictors.py:67-71): the rule weights are not in its graph, so they
+        # get no gradient (None, which Adam skips — a zero gradient would still
+        # move them through the moment estimates)
+        ctx.no_cand = score.numel() == 0 or int(model._last_totals[0]) == 0
         ctx.gen = model._ws_gen.get(device)
         ctx.rows = model._rows(all_h, all_r, edges_to_remove)[1:]
         ctx.has_bias = bias is not None
@@ -223,7 +228,7 @@ class _PredictorLinear(torch.autograd.Function):
         device = all_h.device
         nq = all_h.numel()
         gw = gb = None
-        if nq and ctx.needs_input_grad[0]:
+        if nq and ctx.needs_input_grad[0] and not ctx.no_cand:
             ws, scale, n_cand = ctx.ws, ctx.scale, ctx.n_cand
             if model._ws_gen.get(device) != ctx.gen:  # the workspace was reused: ground again
                 ws, scale, n_cand = model.ground(all_h, all_r, etr)
@@ -347,9 +352,11 @@ class Predictor(_HipGrounding, torch.nn.Module):
                          all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
                          mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(), ws.data_ptr(),
                          ws.numel(), scale, stream)
-        ws, scale = self._launch(device, nq, run)
+        totals = np.zeros(2, dtype=np.int64)  # (candidates, bucket entries), read with the status
+        ws, scale = self._launch(device, nq, run, totals)
         if mixed is not None:
             assert not bool(mixed), "a batch must hold one relation (predictors.py:54-55)"
+        self._last_totals = totals
         mask = torch.ones((nq, E), dtype=torch.bool, device=device) if bias_mode else mask8.bool()
         return score, mask, n_cand, ws, scale
 
@@ -563,6 +570,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # per-candidate outputs to the workspace; a short apply pass adds them
         # into the finished RotatE rows (rnnl_predictorplus_apply)
         self.overlap_deferred = os.environ.get("RNNL_OVERLAP_DEFERRED", "1") != "0"
+        # below this many rows the forward runs on one stream (bit-identical);
+        # 0: overlap from 2 rows on (one 32-row reference batch per call: 0.78
+        # ms overlapped vs 1.02 ms on one stream, the grounding's latency then
+        # hiding behind RotatE)
+        self.overlap_min_rows = int(os.environ.get("RNNL_OVERLAP_MIN_ROWS", "0"))
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -649,6 +661,25 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         return w
 
     def _params(self, device, node_w):
+        """The fused kernels' parameter block (rnnl_predictor_params), cached
+        while node_w and every source tensor keep their storage and version
+        (a per-batch forward then builds nothing)."""
+        rte, sm = self.rule_to_entity, self.score_model
+        srcs = [rte.add_model.layers[0].weight, rte.add_model.layers[0].bias, rte.layer_norm.weight,
+                rte.layer_norm.bias, sm.layers[0].weight, sm.layers[0].bias, sm.layers[1].weight,
+                sm.layers[1].bias, self.relation_emb.weight]
+        if self.entity_feature == "bias":
+            srcs.append(self.bias)
+        key = (node_w.data_ptr(), self.aggregator, self.entity_feature,
+               tuple((t.data_ptr(), t._version) for t in srcs))
+        hit = self._side.get(("params", self._device_index(device)))
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        p, keep = self._build_params(node_w)
+        self._side[("params", self._device_index(device))] = (key, p, keep)
+        return p, keep
+
+    def _build_params(self, node_w):
         rte, sm = self.rule_to_entity, self.score_model
         p = _native.PredictorParams()
         p.aggregator = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
@@ -726,7 +757,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        if self.entity_feature == "RotatE" and self.overlap and nq >= 2 * self.overlap_chunks:
+        if self.entity_feature == "RotatE" and self.overlap and nq >= max(2 * self.overlap_chunks,
+                                                                           self.overlap_min_rows):
             self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec)
             del keep
             return (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device), n_cand) \
@@ -992,13 +1024,30 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
 
         With autograd active (training) the differentiable path runs
         (forward_autograd); otherwise the fused HIP kernels (forward_rows)."""
-        # the reference's single-relation check (predictors.py:211-212) in one host read
-        query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
-        assert n_other == 0
         if self._needs_grad():
+            # the reference's single-relation check (predictors.py:211-212) in one host
+            # read, which also gives the relation whose rules the autograd path gathers
+            query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
+            assert n_other == 0
             return self.forward_autograd(all_h, all_r, edges_to_remove, query_r=query_r)
+        # eval: the check is copied to pinned memory before the launch and read
+        # after the launch status (its host read), so it costs no extra sync
+        mixed = None
+        if all_r.is_cuda and all_r.numel():
+            mixed = torch.empty((), dtype=torch.bool, pin_memory=True)
+            mixed.copy_((all_r != all_r[0]).any(), non_blocking=True)
         score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
-        if self.entity_feature not in ("bias", "RotatE") and int(n_cand.sum().item()) == 0:
-            # reference early return `mask - float('-inf')` (predictors.py:236-237): +inf, mask all False
-            score.fill_(float("inf"))
+        if mixed is not None:
+            torch.cuda.current_stream(all_r.device).synchronize()  # no-op after the status read
+            assert not bool(mixed), "a batch must hold one relation (predictors.py:211-212)"
+        if self.entity_feature not in ("bias", "RotatE"):
+            # reference early return `mask - float('-inf')` (predictors.py:236-237): +inf
+            # where the batch has no candidate (mask all False), without a host read
+            score = torch.where(mask.any(), score, torch.full_like(score, float("inf")))
         return score, mask
+
+    @property
+    def mask_all_true(self):
+        """Every entity is scored (the reference's mask is all True) with the
+        bias and RotatE features (predictors.py:260-266)."""
+        return self.entity_feature in ("bias", "RotatE")

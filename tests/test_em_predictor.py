@@ -246,3 +246,30 @@ def test_c_oracle_predictor_stats(case):
             else:
                 np.testing.assert_array_equal(np.nonzero(c["mask"][i])[0], e)
             np.testing.assert_allclose(c["score"][i, e], v, atol=1e-5, rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_predictor_batch_without_candidates_gives_no_rule_gradient():
+    """predictors.py:67-71: a batch with no candidate returns `mask + bias`,
+    so the rule weights are outside its graph and keep grad None (Adam then
+    skips them; a zero gradient would still move them through its moments).
+    A batch with candidates gives them a gradient."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph
+    from rnnlogic_amd.predictors import Predictor
+    dev = torch.device("cuda:0")
+    graph = KnowledgeGraph(datasets.materialize("umls"))
+    facts = np.asarray(graph.train_facts, dtype=np.int64)
+    r0 = int(facts[0, 1])
+    model = Predictor(graph, entity_feature="bias")
+    model.set_rules([[r0, r0], [r0, r0, r0]])  # rules for one relation only
+    model = model.to(dev).train()
+    other = facts[facts[:, 1] != r0][:8]
+    for rows, want_grad in ((other, False), (facts[facts[:, 1] == r0][:8], True)):
+        model.zero_grad(set_to_none=True)
+        h, r = torch.from_numpy(rows[:, 0]).to(dev), torch.from_numpy(rows[:, 1]).to(dev)
+        score, mask = model(h, r, None)
+        assert bool(mask.all())
+        (torch.softmax(score, 1)[:, 0].sum()).backward()
+        assert (model.rule_weights.grad is not None) == want_grad
+        assert model.bias.grad is not None

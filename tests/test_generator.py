@@ -55,8 +55,8 @@ def _check_generator_part(z, got, w_tol=W_TOL):
     assert np.array_equal(got["probe/beam"], z["probe/beam"])
 
 
-def _check_sample(got, want_json):
-    """Same rules per head relation (as sets), log p within 1e-6, and the
+def _check_sample(got, want_json, tol=1e-6):
+    """Same rules per head relation (as sets), log p within `tol`, and the
     reference's order when every log p is bitwise equal."""
     import json
     want = json.loads(str(want_json))
@@ -64,7 +64,7 @@ def _check_sample(got, want_json):
     key = lambda rule: tuple(int(x) for x in rule[:-1])  # noqa: E731
     gmap, wmap = {key(r): r[-1] for r in got}, {key(r): r[-1] for r in want}
     assert len(gmap) == len(got) and set(gmap) == set(wmap)
-    _close([gmap[k] for k in wmap], [wmap[k] for k in wmap], 1e-6)
+    _close([gmap[k] for k in wmap], [wmap[k] for k in wmap], tol)
     if all(gmap[k] == wmap[k] for k in wmap):
         assert [key(r) for r in got] == [key(r) for r in want]
         return True
@@ -154,8 +154,18 @@ def test_em_iteration_gpu():
     EM iteration's Predictor on cuda:0."""
     z, got = em_chain.run(torch.device("cuda:0"), em=True, gen_device=torch.device("cpu"))
     _check_generator_part(z, got)
-    _check_sample(got["em/sampled"], z["em/sampled"])
+    # bitwise on the fixture's CPU model (test_generator_chain_cpu); on another
+    # CPU the pre-trained weights differ in the last bits, so log p does too
+    same_cpu = "cpu" in z.files and str(z["cpu"]) == em_chain.cpu_model()
+    _check_sample(got["em/sampled"], z["em/sampled"], 1e-6 if same_cpu else 1e-5)
     assert np.array_equal(got["probe/sample"], z["probe/sample"])
+    err = lambda a, b: float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())  # noqa: E731
+    print("EM errors: train_loss %.3g, pred_trained %s, H %.3g, posterior %.3g, m_step loss %.3g, gen_m %s" % (
+        err(got["em/train_loss"], z["em/train_loss"]),
+        {k: "%.3g" % err(v, em_chain.state(z, "pred_trained")[k]) for k, v in got["pred_trained"].items()},
+        err(got["em/H"], z["em/H"]), err(got["em/posterior"], z["em/posterior"]),
+        err(got["m_step/loss"], z["m_step/loss"]),
+        max(err(v, em_chain.state(z, "gen_m")[k]) for k, v in got["gen_m"].items())))
     _check_states(got["pred_init"], em_chain.state(z, "pred_init"), 0.0)
     _close(got["em/train_loss"], z["em/train_loss"], W_TOL + 1e-6)
     assert np.array_equal(got["probe/em_train"], z["probe/em_train"])

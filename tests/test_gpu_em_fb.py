@@ -7,7 +7,8 @@ split; the pre-training rule set is rnnlogic_rules.txt with synthetic weights
 PRE_EPOCHS of the config's 10,000 epochs.  The rest is the config's:
   sample      TrainerGenerator.sample(100, 3) in the reference's draw order:
               per head relation <= 100 distinct rules of body length <= 3,
-              each log p = the generator's own log_probability of the rule;
+              a rule closed by END before length 3 carrying the generator's
+              own log_probability of it;
   E-step      Predictor.compute_H_rows over the rows of the first H_BATCHES
               train batches (sampler order, edge removal) against the C
               oracle's per-rule path counts (oracle_query_stats, pinned to
@@ -91,7 +92,10 @@ def test_fb15k237_em_iteration():
     assert len(per_rel) == graph.relation_size
     assert all(len(v) <= 100 for v in per_rel.values())
     assert sum(len(v) for v in per_rel.values()) == len(sampled)  # deduplicated per relation
-    probe = sampled[::997][:40]
+    # a sequence closed by END before max_length carries END's log p, as
+    # log_probability does; full-length ones stop without it (trainer.py:428-445)
+    probe = [r for r in sampled if len(r) - 2 < 3][::97][:40]
+    assert probe
     lp = solver_g.log_probability([list(r[:-1]) for r in probe])
     np.testing.assert_allclose([r[-1] for r in probe], lp, atol=1e-4, rtol=0)
     prior = [rule[-1] for rule in sampled]
