@@ -264,7 +264,8 @@ def test_predictor_batch_without_candidates_gives_no_rule_gradient():
     model = Predictor(graph, entity_feature="bias")
     model.set_rules([[r0, r0], [r0, r0, r0]])  # rules for one relation only
     model = model.to(dev).train()
-    other = facts[facts[:, 1] != r0][:8]
+    r1 = int(facts[facts[:, 1] != r0][0, 1])
+    other = facts[facts[:, 1] == r1][:8]  # one relation without rules
     for rows, want_grad in ((other, False), (facts[facts[:, 1] == r0][:8], True)):
         model.zero_grad(set_to_none=True)
         h, r = torch.from_numpy(rows[:, 0]).to(dev), torch.from_numpy(rows[:, 1]).to(dev)
