@@ -502,11 +502,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     rows_per_rank = [nq]
+    shards = None
     if world > 1:
         cnt = torch.tensor([nq], dtype=torch.int64, device=dev)
         parts = [torch.empty_like(cnt) for _ in range(world)]
         dist.all_gather(parts, cnt)
         rows_per_rank = [int(x.item()) for x in parts]
+        # every rank's batch indices: their union must be the split, the
+        # surplus the sampler's padding (repeated batches, trainer.py:150)
+        idx_all = [None] * world
+        dist.all_gather_object(idx_all, list(shard))
+        flat = [i for part in idx_all for i in part]
+        shards = {"batches_per_rank": [len(x) for x in idx_all],
+                  "union_is_split": sorted(set(flat)) == list(range(len(test_set))),
+                  "padding_batches": len(flat) - len(test_set),
+                  "rows_total_with_padding": int(sum(rows_per_rank)), "rows_counted": n_split}
 
     # secondary at N > 1: every rank on the whole split (replicated, weak scaling)
     weak = None
@@ -741,7 +751,7 @@ def main():
                                   "RotatE(D=1000,gamma=9)" if args.feature == "RotatE" else "bias",
                                   model.num_rules, " and RotatE tables" if args.feature == "RotatE" else ""),
                    "batch_size": 32, "parallelism": "dp%d (test batches sharded, KG replicated)" % world,
-                   "rows_per_rank": rows_per_rank, "batches_per_rank": len(shard)},
+                   "rows_per_rank": rows_per_rank, "batches_per_rank": len(shard), "shards": shards},
         "roofline": dominant,
         "kernels_ms": {"rule_encoder+node_weights": round(nodes_ms, 3), "base_score": round(base_ms, 3),
                        "tail_after_base": round(tail_ms, 3), "ground+score_isolated": round(ground_ms, 3)},

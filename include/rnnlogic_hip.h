@@ -285,7 +285,9 @@ int rnnl_fill_value(float value, int64_t n, float *score, void *stream);
  *                   (rnnl_rotate_relation_table, from remb (n_rel_total x dim)).
  * rnnl_rotate_score replaces RotatE.forward (embedding.py:45-70); it needs a
  * per-call workspace of rnnl_rotate_workspace_size bytes (h o r of every
- * query in DIRECT mode; 0 for MFMA).  accumulate != 0 adds into score. */
+ * query in DIRECT mode, plus per-32-dim chunk sums when a launch has few rows
+ * — the split form, bitwise equal to the one-pass kernel; 0 for MFMA).
+ * accumulate != 0 adds into score. */
 #define RNNL_ROTATE_DIRECT 0
 #define RNNL_ROTATE_MFMA 1
 int rnnl_rotate_table_sizes(int32_t n_entities, int32_t dim, int32_t n_rel_total, int32_t mode,
@@ -294,7 +296,7 @@ int rnnl_rotate_entity_table(const float *eemb, int32_t n_entities, int32_t dim,
                              void *stream);
 int rnnl_rotate_relation_table(const float *remb, int32_t n_rel_total, int32_t dim, float gamma,
                                float *relation_table, void *stream);
-int rnnl_rotate_workspace_size(int32_t n_queries, int32_t dim, int32_t mode, size_t *bytes);
+int rnnl_rotate_workspace_size(int32_t n_queries, int32_t n_entities, int32_t dim, int32_t mode, size_t *bytes);
 int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *relation_table, int32_t dim,
                       float gamma, const int64_t *all_h, const int64_t *all_r, int32_t n_queries,
                       int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
@@ -305,6 +307,7 @@ int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *
  * (n_queries x 2 dim: re | im, as torch forms it) and the entity planes
  * (dim x 2 x ld: planes[(2 d + part) * ld + e], ld >= E), writes
  *   d_tail (dim x 2 x E, same plane order) = dL/d(tail entity embedding)
+ *   (d_tail may be NULL when the entity table is frozen)
  * and accumulates (atomically; zero it first) d_hr (n_queries x 2 dim) +=
  * dL/d(h o r).  torch.norm's convention: zero gradient where |hr - t| = 0. */
 int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const float *grad, int32_t n_queries,

@@ -66,7 +66,7 @@ SIGNATURES = [
     ("rnnl_rotate_table_sizes", ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P]),
     ("rnnl_rotate_entity_table", ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     ("rnnl_rotate_relation_table", ctypes.c_int, [_P, _I32, _I32, _F32, _P, _P]),
-    ("rnnl_rotate_workspace_size", ctypes.c_int, [_I32, _I32, _I32, _P]),
+    ("rnnl_rotate_workspace_size", ctypes.c_int, [_I32, _I32, _I32, _I32, _P]),
     ("rnnl_multi_hot", ctypes.c_int, [_P, _P, _P, _I64, _P, _I32, _I32, _P, _P]),
     ("rnnl_filter_flags", ctypes.c_int, [_P, _P, _P, _I64, _P, _I32, _I32, _P, _P]),
     ("rnnl_filtered_ranks", ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _P, _P, _P]),

@@ -132,7 +132,10 @@ def reduce(obj, op="sum", dst=None):
 
 def stack(obj, dst=None):
     """All-gather every tensor of `obj` and stack along a new dim 0
-    (comm.py:178-211); every rank must pass equal shapes."""
+    (comm.py:178-211); every rank must pass equal shapes.  `dst` is accepted
+    for the reference's signature only: the result is returned on every rank
+    (the reference's reduce leaves it valid on dst alone, so this is a
+    superset)."""
     world = get_world_size()
     if world == 1:
         return _rebuild(obj, iter([t.unsqueeze(0) for t in _leaves(obj, [])]))
@@ -151,7 +154,8 @@ def stack(obj, dst=None):
 def cat(obj, dst=None):
     """All-gather every tensor of `obj` and concatenate along dim 0
     (comm.py:214-256); dim 0 may differ across ranks (sizes are exchanged
-    first, payloads padded to the largest rank)."""
+    first, payloads padded to the largest rank).  `dst` is accepted for the
+    reference's signature only: the result is returned on every rank."""
     world = get_world_size()
     if world == 1:
         return obj

@@ -1899,6 +1899,10 @@ __device__ __forceinline__ void fold_relation_bias(const KParams &p, float *s_re
   }
 }
 
+// Launches with at most this many rows compute the memo only for the
+// relations their rows hold (a scan of all_r per workgroup).
+constexpr int MEMO_SCAN_ROWS = 2048;
+
 // One workgroup per head relation with rules: memo[n] for its leaf nodes.
 __global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__restrict__ W) {
   using L = WL<RNNL_AGG_SUM>;
@@ -1907,6 +1911,12 @@ __global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__
   const int r = blockIdx.x;
   const int lp = p.rl.head_leaf_ptr[r], nl = p.rl.head_leaf_ptr[r + 1] - lp;
   if (nl <= 0) return;  // uniform
+  if (p.nq <= MEMO_SCAN_ROWS) {
+    // few rows (e.g. one reference batch): only the relations present need a memo
+    bool any = false;
+    for (int q = threadIdx.x; q < p.nq; q += BS) any |= (int)p.all_r[q] == r;
+    if (!__syncthreads_or(any)) return;  // block-uniform
+  }
   load_sum_weights(s_w, W);
   fold_relation_bias(p, s_relb, r);
   __syncthreads();

@@ -470,6 +470,110 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
 }
 
 // ---------------------------------------------------------------------------
+// Split-dimension form of rotate_direct_kernel for launches with few rows
+// (e.g. one 32-row reference batch per call, trainer.py:150-173): there the
+// (query group x entity tile) grid has ~100 blocks and each wave walks all D
+// dims alone — latency-bound (525 us for 32 rows x 14,541 entities x 1000
+// dims on FB15k-237, vs 64 us at the full-split rate).  Here the DCH-dim
+// chunks are dealt to `groups` blocks per tile: each wave computes, for its
+// DQ queries and 64 entities, every chunk sum of its chunk range exactly as
+// rotate_direct_kernel does (the same sub, sub, mul, fma, sqrt per term, the
+// same sequential adds within a chunk, the sqrt of a dim added in the next
+// dim's step) and stores it; rotate_combine_kernel then folds the chunk sums
+// into the row total in chunk order and adds the last dim's sqrt — the same
+// fp32 operations in the same order, so the scores are bitwise those of
+// rotate_direct_kernel.  parts layout: [nchunks + 1][nq][E].
+__global__ __launch_bounds__(RB) void rotate_split_kernel(const float *__restrict__ ptab,
+                                                          const float *__restrict__ hr, int D, int nq, int E,
+                                                          int chunks_per_group, float *__restrict__ parts) {
+  const int64_t Ep = ent_pad(E);
+  const int n_et = (int)(Ep / RB);
+  const int ngroups_q = (nq + DQ - 1) / DQ;
+  const int nchunks = (D + DCH - 1) / DCH;
+  // block -> (chunk group, query group, entity tile): entity tiles fastest,
+  // so the blocks of one dim range share their slice of the entity planes
+  int b = blockIdx.x;
+  const int et = b % n_et;
+  b /= n_et;
+  const int qt = __builtin_amdgcn_readfirstlane(b % ngroups_q);
+  const int cg = __builtin_amdgcn_readfirstlane(b / ngroups_q);
+  const int c0 = cg * chunks_per_group, c1 = min(nchunks, c0 + chunks_per_group);
+  if (c0 >= nchunks) return;  // block-uniform; no barrier in the kernel
+  const int e = et * RB + (int)threadIdx.x;  // < Ep: the table is padded
+  const int q0 = qt * DQ;
+  const float *hp = hr + (int64_t)qt * D * 2 * DQ;
+  const float *ap = ptab + e;
+  float sq[DQ];
+#pragma unroll
+  for (int k = 0; k < DQ; ++k) sq[k] = 0.f;
+  if (c0 > 0) {  // the pipeline's carried value: the previous chunk's last dim
+    const int d = c0 * DCH - 1;
+    const float a = ap[(int64_t)d * 2 * Ep], bb = ap[(int64_t)d * 2 * Ep + Ep];
+    const float *h = hp + (int64_t)d * 2 * DQ;
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) {
+      const float x = h[k] - a;
+      const float y = h[DQ + k] - bb;
+      sq[k] = fmaf(x, x, y * y);
+    }
+  }
+  const int64_t plane = (int64_t)nq * E;
+  for (int c = c0; c < c1; ++c) {
+    float part[DQ];
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) part[k] = 0.f;
+    for (int d = c * DCH; d < min(c * DCH + DCH, D); ++d) {
+      const float a = ap[(int64_t)d * 2 * Ep], bb = ap[(int64_t)d * 2 * Ep + Ep];
+      const float *h = hp + (int64_t)d * 2 * DQ;  // wave-uniform: s_load
+#pragma unroll
+      for (int k = 0; k < DQ; ++k) {
+        part[k] += __builtin_amdgcn_sqrtf(sq[k]);
+        const float x = h[k] - a;
+        const float y = h[DQ + k] - bb;
+        sq[k] = fmaf(x, x, y * y);
+      }
+    }
+    if (e < E) {
+#pragma unroll
+      for (int k = 0; k < DQ; ++k)
+        if (q0 + k < nq) parts[(int64_t)c * plane + (int64_t)(q0 + k) * E + e] = part[k];
+    }
+  }
+  if (c1 == nchunks && e < E) {  // the last dim's sqrt, added after the chunk sums
+#pragma unroll
+    for (int k = 0; k < DQ; ++k)
+      if (q0 + k < nq) parts[(int64_t)nchunks * plane + (int64_t)(q0 + k) * E + e] = __builtin_amdgcn_sqrtf(sq[k]);
+  }
+}
+
+__global__ __launch_bounds__(256) void rotate_combine_kernel(const float *__restrict__ parts, int nchunks, int nq,
+                                                             int E, float gamma, float *__restrict__ score,
+                                                             int accumulate) {
+  const int64_t n = (int64_t)nq * E;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int c = 0; c < nchunks; ++c) acc += parts[(int64_t)c * n + i];
+    acc += parts[(int64_t)nchunks * n + i];
+    const float v = gamma - acc;
+    score[i] = accumulate ? score[i] + v : v;
+  }
+}
+
+// Chunk groups of the split form for a launch (1: the one-pass direct kernel):
+// when the (query group x entity tile) grid is below ~1,024 blocks, deal the
+// chunks to enough groups for ~2,048 blocks, capped so the chunk sums stay
+// within 512 MB.
+static int split_groups(int64_t nq, int64_t E, int D) {
+  const int64_t base = (ent_pad(E) / RB) * ((nq + DQ - 1) / DQ);
+  const int nchunks = (D + DCH - 1) / DCH;
+  if (base >= 1024 || nchunks < 2) return 1;
+  if ((int64_t)(nchunks + 1) * nq * E * 4 > (int64_t)512 << 20) return 1;
+  int groups = (int)std::min<int64_t>(nchunks, (2048 + base - 1) / base);
+  const int cpg = (nchunks + groups - 1) / groups;
+  return (nchunks + cpg - 1) / cpg;
+}
+
+// ---------------------------------------------------------------------------
 // Table builders (once per weight version)
 
 // etab[d][kg][e] from eemb[e][2D]: 32 entities x 32 dims per tile through
@@ -631,7 +735,7 @@ __global__ __launch_bounds__(BW_BS) void rotate_backward_kernel(const float *__r
 #pragma unroll
   for (int k = 0; k < BW_EPT; ++k) {
     const int e = e0 + k * BW_BS;
-    if (e < E) {
+    if (d_tail && e < E) {  // d_tail == nullptr: the entity table is frozen
       d_tail[(int64_t)(2 * d) * E + e] = ta[k];
       d_tail[(int64_t)(2 * d + 1) * E + e] = tb[k];
     }
@@ -709,12 +813,21 @@ int rnnl_rotate_relation_table(const float *remb, int32_t n_rel_total, int32_t D
   return RNNL_OK;
 }
 
-int rnnl_rotate_workspace_size(int32_t nq, int32_t D, int32_t mode, size_t *bytes) {
-  if (nq < 0 || D <= 0 || !valid_mode(mode) || !bytes) {
+// hr slabs, then (split form only) the chunk sums, 256-byte aligned
+static size_t hr_bytes(int64_t nq, int D) { return (size_t)((nq + DQ - 1) / DQ) * D * 2 * DQ * sizeof(float); }
+
+int rnnl_rotate_workspace_size(int32_t nq, int32_t E, int32_t D, int32_t mode, size_t *bytes) {
+  if (nq < 0 || E <= 0 || D <= 0 || !valid_mode(mode) || !bytes) {
     set_error("rnnl_rotate_workspace_size: bad arguments");
     return RNNL_ERR_INVALID;
   }
-  *bytes = mode == RNNL_ROTATE_DIRECT ? (size_t)((nq + DQ - 1) / DQ) * D * 2 * DQ * sizeof(float) : 0;
+  if (mode != RNNL_ROTATE_DIRECT) {
+    *bytes = 0;
+    return RNNL_OK;
+  }
+  size_t b = (hr_bytes(nq, D) + 255) / 256 * 256;
+  if (split_groups(nq, E, D) > 1) b += (size_t)((D + DCH - 1) / DCH + 1) * nq * E * sizeof(float);
+  *bytes = b;
   return RNNL_OK;
 }
 
@@ -728,7 +841,7 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
   if (nq == 0) return RNNL_OK;
   if (mode == RNNL_ROTATE_DIRECT) {
     size_t need = 0;
-    rnnl_rotate_workspace_size(nq, D, mode, &need);
+    rnnl_rotate_workspace_size(nq, E, D, mode, &need);
     if (!workspace || ws_bytes < need) {
       set_error("rnnl_rotate_score: workspace too small (see rnnl_rotate_workspace_size)");
       return RNNL_ERR_INVALID;
@@ -737,6 +850,19 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
                        (hipStream_t)stream, eemb,
                        (const float2 *)rtab, D, all_h, all_r, nq, (float *)workspace);
     RNNL_HIP_CHECK(hipGetLastError());
+    const int groups = split_groups(nq, E, D);
+    if (groups > 1) {  // few rows: chunk sums over more blocks, then the in-order fold
+      const int nchunks = (D + DCH - 1) / DCH, cpg = (nchunks + groups - 1) / groups;
+      float *parts = reinterpret_cast<float *>(static_cast<unsigned char *>(workspace) +
+                                               (hr_bytes(nq, D) + 255) / 256 * 256);
+      const int64_t nblk = (ent_pad(E) / RB) * ((nq + DQ - 1) / DQ) * groups;
+      hipLaunchKernelGGL(rotate_split_kernel, dim3((unsigned)nblk), dim3(RB), 0, (hipStream_t)stream,
+                         (const float *)etab, (const float *)workspace, D, nq, E, cpg, parts);
+      hipLaunchKernelGGL(rotate_combine_kernel, dim3(grid_for((int64_t)nq * E)), dim3(256), 0, (hipStream_t)stream,
+                         (const float *)parts, nchunks, nq, E, gamma, score, accumulate);
+      RNNL_HIP_CHECK(hipGetLastError());
+      return RNNL_OK;
+    }
     hipLaunchKernelGGL(rotate_direct_kernel,
                        dim3(xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW)), dim3(RB), 0,
                        (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E, score,
@@ -752,7 +878,7 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
 
 int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const float *grad, int32_t nq,
                          int32_t E, int32_t D, float *d_hr, float *d_tail, void *stream) {
-  if (!planes || !hr || !grad || !d_hr || !d_tail || nq < 0 || E <= 0 || D <= 0 || ld < E) {
+  if (!planes || !hr || !grad || !d_hr || nq < 0 || E <= 0 || D <= 0 || ld < E) {
     set_error("rnnl_rotate_backward: bad arguments");
     return RNNL_ERR_INVALID;
   }

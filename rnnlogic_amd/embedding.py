@@ -40,10 +40,14 @@ class _RotatEScore(torch.autograd.Function):
         hr = torch.cat([hr_re, hr_im], dim=1).detach().float().contiguous()
         grad = grad.detach().float().contiguous()
         d_hr = torch.zeros((nq, 2 * D), dtype=torch.float32, device=eemb.device)
-        d_tail = torch.empty((D, 2, E), dtype=torch.float32, device=eemb.device)
+        # the tail gradient only when eemb is trained (a frozen table with a
+        # trained remb still needs d(h o r))
+        need_tail = ctx.needs_input_grad[0]
+        d_tail = torch.empty((D, 2, E), dtype=torch.float32, device=eemb.device) if need_tail else None
         _native.call("rnnl_rotate_backward", planes.data_ptr(), E, hr.data_ptr(), grad.data_ptr(), nq, E, D,
-                     d_hr.data_ptr(), d_tail.data_ptr(), torch.cuda.current_stream(eemb.device).cuda_stream)
-        d_eemb = d_tail.permute(2, 1, 0).reshape(E, 2 * D)
+                     d_hr.data_ptr(), d_tail.data_ptr() if need_tail else None,
+                     torch.cuda.current_stream(eemb.device).cuda_stream)
+        d_eemb = d_tail.permute(2, 1, 0).reshape(E, 2 * D) if need_tail else None
         return d_eemb, d_hr[:, :D], d_hr[:, D:], None, None, None
 
 
@@ -91,7 +95,8 @@ class RotatE(torch.nn.Module):
 
     def _workspace(self, nq):
         need = ctypes.c_size_t()
-        _native.call("rnnl_rotate_workspace_size", nq, self.emb_dim, int(self.mode), ctypes.byref(need))
+        _native.call("rnnl_rotate_workspace_size", nq, self.num_entities, self.emb_dim, int(self.mode),
+                     ctypes.byref(need))
         if need.value == 0:
             return None, 0
         if self._ws is None or self._ws.numel() * 4 < need.value or self._ws.device != self.eemb.device:

@@ -458,12 +458,14 @@ class Predictor(_HipGrounding, torch.nn.Module):
         return out
 
     @torch.no_grad()
-    def compute_H_rows(self, all_h, all_r, all_t, edges_to_remove, chunk=32768):
+    def compute_H_rows(self, all_h, all_r, all_t, edges_to_remove, chunk=8192):
         """Σ over rows of compute_H's per-row softmax (predictors.py:82-119),
         for rows of any relations in a few launches: the per-row terms are
         independent, so the sum over the reference's batches equals the sum
         over all their rows.  Returns (num_rules,) (rules of relations that
-        have none get 0)."""
+        have none get 0).  `chunk` rows per launch bound the grounding
+        workspace (8,192 rows: ~1.9 GB at capacity_scale 1; the result does
+        not depend on it)."""
         device = all_h.device
         n = all_h.numel()
         H = torch.zeros(self.num_rules, device=device)
@@ -904,8 +906,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             if self.entity_feature == "bias":
                 return zero + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
             if self.entity_feature == "RotatE":
-                return zero + self.RotatE.forward_grad(all_h, all_r), torch.ones((nq, E), dtype=torch.bool,
-                                                                                 device=device)
+                return zero + self.RotatE(all_h, all_r), torch.ones((nq, E), dtype=torch.bool, device=device)
             return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
         return self._score_coo(all_h, all_r, row, ent, ce, node, count, rels=query_r)
 
@@ -979,7 +980,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if self.entity_feature == "bias":
             return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
         if self.entity_feature == "RotatE":
-            rot = self.RotatE.forward_grad(all_h, all_r) if self._needs_grad() else self.RotatE(all_h, all_r)
+            # RotatE.forward takes its HIP backward only when eemb / remb are trained
+            rot = self.RotatE(all_h, all_r)
             return score + rot, torch.ones((nq, E), dtype=torch.bool, device=device)
         mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
         return score.masked_fill(~mask, float("-inf")), mask

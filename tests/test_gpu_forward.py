@@ -307,3 +307,28 @@ def test_lstm_encoder_matches_torch(data, dev):
         got = model._encode_rules_hip(dev)
     err = float((got - want).abs().max())
     assert err <= 2e-6, err
+
+
+@pytest.mark.parametrize("data", ["FB15k-237", "umls"])
+def test_rotate_split_form_is_bitwise(data, dev):
+    """A launch with few rows (one 32-row reference batch) runs RotatE in the
+    split-dimension form (rotate_split_kernel + rotate_combine_kernel); its
+    scores equal the one-pass direct kernel's bitwise for the same rows —
+    including ragged row counts and the accumulate mode."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.embedding import RotatE
+    path = datasets.rotate_path(data) if data == "FB15k-237" else datasets.rotate_path(data, 200)
+    rot = RotatE(path).to(dev)
+    E = rot.num_entities
+    g = torch.Generator().manual_seed(3)
+    n_big = 4096 if data == "FB15k-237" else 40000  # enough rows for the one-pass grid
+    h = torch.randint(0, E, (n_big,), generator=g).to(dev)
+    r = torch.randint(0, rot.remb.shape[0], (n_big,), generator=g).to(dev)
+    with torch.no_grad():
+        big = rot(h, r)
+        for n in (32, 7, 45):
+            small = rot(h[:n], r[:n])
+            assert torch.equal(small, big[:n]), (n, float((small - big[:n]).abs().max()))
+        base = torch.randn(5, E, device=dev)
+        acc = rot.score_into(h[:5], r[:5], base.clone(), accumulate=True)
+        assert torch.equal(acc, base + big[:5])

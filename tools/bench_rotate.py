@@ -1,5 +1,5 @@
 """A/B timing of rnnl_rotate_score across the compile variants built by
-tools/rotate_variants.sh (rnnlogic_amd/_build/variants/*.so), at the bench
+tools/build_variants.sh rotate.hip (rnnlogic_amd/_build/variants/*.so), at the bench
 workload's shape (FB15k-237 test split: 40,932 queries x 14,541 entities x
 D = 1000).  Prints one line per variant: mean ms per launch (HIP events) and
 the max |diff| against the main library's RNNL_ROTATE_DIRECT result.
@@ -55,7 +55,7 @@ def main():
     rtab = torch.empty(rb.value // 4, device=dev)
     _native.call("rnnl_rotate_relation_table", remb.data_ptr(), R2, D, 9.0, rtab.data_ptr(), st)
     wsb = ctypes.c_size_t()
-    _native.call("rnnl_rotate_workspace_size", nq, D, _native.ROTATE_DIRECT, ctypes.byref(wsb))
+    _native.call("rnnl_rotate_workspace_size", nq, E, D, _native.ROTATE_DIRECT, ctypes.byref(wsb))
     ws = torch.empty(wsb.value // 2 + 1024, device=dev)  # 2x: variants may pad the query groups differently
     out = torch.empty(nq, E, device=dev)
     ref = torch.empty(nq, E, device=dev)
