@@ -10,7 +10,7 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
-# diagnostic A/B builds (tools/*_variants.sh) may be selected with RNNL_LIB
+# diagnostic A/B builds (tools/build_variants.sh) may be selected with RNNL_LIB
 LIB_PATH = os.environ.get("RNNL_LIB") or LIB_PATH
 
 RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL, RNNL_ERR_RANGE = \

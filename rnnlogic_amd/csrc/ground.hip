@@ -1250,6 +1250,165 @@ __device__ __forceinline__ float score_one_2walk(const KParams &p, const float *
   return out + wl[L::S1B];
 }
 
+// One walk over a candidate's bucket entries for 8 dims (d0 .. d0 + 7) of
+// one half of the node records: the exact sums of count x record word
+// (fp64, exact below a total count of 2^23, else the int64 fallback) and the
+// min (half 0) / max (half 1) of the float words.
+// STATS (the first walk): also the degree sum, the digest fingerprint and
+// the count total.
+template <int HALF, bool STATS>
+__device__ __forceinline__ void pna_walk8(const KParams &p, int beg, int cnt, int d0, uint64_t &csum, long long &deg,
+                                          uint64_t &fp, bool want_fp, double (&a)[8], float (&m)[8]) {
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    a[d] = 0;
+    m[d] = HALF == 0 ? __builtin_huge_valf() : -__builtin_huge_valf();
+  }
+#pragma unroll 1
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const double cd = (double)(uint32_t)be.y;
+    if constexpr (STATS) {
+      const long long c = (uint32_t)be.y;
+      csum += (uint64_t)c;
+      deg += c * p.rl.node_nrules[be.x];
+      if (want_fp) fp += (uint64_t)c * p.rl.node_fp[be.x];
+    }
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna) + HALF * 16 + d0;
+    const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      a[d] = fma(cd, (double)rec[d], a[d]);
+      m[d] = HALF == 0 ? fminf(m[d], fr[d]) : fmaxf(m[d], fr[d]);
+    }
+  }
+  if (csum >> 23) {  // exact int64 sums one dim at a time (rare)
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      long long acc = 0;
+#pragma unroll 1
+      for (int e = beg; e < beg + cnt; ++e) {
+        const int2 be = p.bent[e];
+        acc += (long long)(uint32_t)be.y *
+               reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna)[HALF * 16 + d0 + d];
+      }
+      a[d] = (double)acc;
+    }
+  }
+}
+
+__device__ __forceinline__ void pin8(float (&x)[8]) {
+  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+               :
+               : "memory");
+}
+
+// score_one_2walk with each walk split in two 8-dim walks (four walks over
+// the entries): only 8 fp64 sums and 8 min / max are live at a time, which
+// takes the PNA scoring pass from 168 to ~100 VGPRs (more waves beside
+// RotatE).  The 192 Linear inputs are folded into the 16 outputs in the
+// same order as score_one_2walk (mean, min of dims 0..15, then max, std of
+// dims 0..15), so the scores are bitwise the same.
+__device__ __forceinline__ float score_one_4walk(const KParams &p, const float *wl, const float *relb, int beg,
+                                                 int cnt, float mean_scale, uint64_t *dig_out, int t) {
+  using L = WL<RNNL_AGG_PNA>;
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  long long deg = 0;
+  uint64_t fp = 0, csum = 0;
+  double a[8];
+  float m[8];
+  // walk 1 also sums the degree, the digest fingerprint and the count total
+  pna_walk8<0, true>(p, beg, cnt, 0, csum, deg, fp, dig_out != nullptr, a, m);
+  if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+  if (csum >> 33) flag_acc_range(p);
+  const double inv1 = ldexp(1.0, -(int)trailer[1]), inv2 = ldexp(1.0, -(int)trailer[4]);
+  const float degf = (float)(deg + 1);
+  const float dcl = fmaxf(degf, 1e-6f);
+  const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
+  const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
+  float x1[16], mean[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] = 0.f;
+  // walks 1-2: sums of x (means) and min, dims 0..7 then 8..15
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) pna_walk8<0, false>(p, beg, cnt, 8, csum, deg, fp, false, a, m);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = h * 8 + j;
+      mean[d] = (float)(a[j] * inv1) / dcl;
+      const float fv[2] = {mean[d], m[j]};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+          pin16(x1);
+          const float v = fv[b] * sc[s3];
+          const float *w = wl + L::ADDW + ((b * 16 + d) * 3 + s3) * 16;
+#pragma unroll
+          for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
+        }
+      }
+    }
+  }
+  // walks 3-4: sums of x^2 (std) and max, dims 0..7 then 8..15
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    pna_walk8<1, false>(p, beg, cnt, h * 8, csum, deg, fp, false, a, m);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = h * 8 + j;
+      const float sqm = (float)(a[j] * inv2) / dcl;
+      const float fv[2] = {m[j], sqrtf(fmaxf(sqm - mean[d] * mean[d], 1e-6f))};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+          pin16(x1);
+          const float v = fv[b] * sc[s3];
+          const float *w = wl + L::ADDW + (((b + 2) * 16 + d) * 3 + s3) * 16;
+#pragma unroll
+          for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] += wl[L::ADDB + o];
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+  float out = 0.f;
+#pragma unroll 2
+  for (int o = 0; o < 128; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(x1[i], wl[L::S0X + o * 16 + i], acc);
+    acc = fmaxf(acc + relb[o], 0.f);
+    out = fmaf(acc, wl[L::S1W + o], out);
+  }
+  return out + wl[L::S1B];
+}
+
+// Measured on WN18RR (config 3, round 3): the four-walk form at 4 waves/SIMD
+// 22.4 ms/step, at 3 waves 22.0, the two-walk form (190 VGPRs, 2 waves) 21.1
+// — the extra entry walks cost more than the occupancy gains beside RotatE.
+// Kept for A/B (RNNL_PNA_4WALK=1); bitwise the same scores.
+#ifndef RNNL_PNA_4WALK
+#define RNNL_PNA_4WALK 0
+#endif
+
 #ifndef RNNL_PNA_SPLIT
 #define RNNL_PNA_SPLIT 0
 #endif
@@ -1453,7 +1612,12 @@ __device__ __forceinline__ void next_chunks(unsigned int *ctr, long long nchunks
 #endif
 constexpr int PNA_CK = RNNL_PNA_CK;  // chunks per dequeue
 
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAVES, 8))) void score_pna_chunk_kernel(
+// 4 waves/SIMD for the four-walk scoring (128 VGPRs, no spills; 138 unforced
+// = 3 waves)
+#ifndef RNNL_PNA_CHUNK_WAVES
+#define RNNL_PNA_CHUNK_WAVES (RNNL_PNA_4WALK ? 4 : RNNL_PNA_WAVES)
+#endif
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_CHUNK_WAVES, 8))) void score_pna_chunk_kernel(
     KParams p, const float *__restrict__ W) {
   using L = WL<RNNL_AGG_PNA>;
   __shared__ __attribute__((aligned(16))) float s_w[L::N];
@@ -1509,7 +1673,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
     const int t = cr.x;
     uint64_t dg = 0;
     asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop (see score_kernel)
+#if RNNL_PNA_4WALK
+    const float out = score_one_4walk(p, s_w, relb, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t);
+#else
     const float out = score_one_2walk<RNNL_AGG_PNA>(p, s_w, relb, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t);
+#endif
     if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
     if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
       p.cand_out[qb + s] = out;

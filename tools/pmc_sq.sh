@@ -8,4 +8,4 @@ C=${COUNTERS:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ
 timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_$tag -o run -- \
     python3 bench.py --feature bias --steps 2 --warmup 1 --profile-only > gpurun_out/pmc_$tag.json 2> gpurun_out/pmc_$tag.err \
     || { tail -5 gpurun_out/pmc_$tag.err; exit 1; }
-python3 tools/pmc_summary.py gpurun_out/pmc_$tag rnnl:: | grep -E "ground_kernel|score_sum|score_linear" | tail -6
+python3 tools/pmc_summary.py gpurun_out/pmc_$tag rnnl:: | grep -E "ground_kernel|score_sum|score_linear|memo_sum|chunk_" | tail -6
