@@ -247,8 +247,11 @@ def wn18rr_line(dev, reps=10):
         del tmp
     ground_ms = isolated_ground_ms(model, graph, h, r, dev)
     flops = 7.0 * nq * E * D
+    groof = grounding_roofline(algorithmic_work(model, graph, rows, name="wn18rr"), nq, E, ground_ms,
+                               "ground_kernel<PNA> + score_pna_chunk_kernel",
+                               measured="one untimed one-stream launch over all rows (isolated from RotatE)")
     return {"queries_per_s": round(nq / sec, 1), "ms_per_step": round(sec * 1e3, 3), "rows": nq,
-            "batches": len(test_set), "rules": model.num_rules,
+            "batches": len(test_set), "rules": model.num_rules, "roofline_grounding": groof,
             "kernels_ms": {"rotate_alone": round(rot_ms, 3), "ground+score_isolated": round(ground_ms, 3)},
             "roofline_rotate": {"bound": "valu", "achieved": round(flops / (rot_ms * 1e-3) / 1e12, 2),
                                 "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
@@ -285,8 +288,11 @@ def kinship_line(dev, reps=50):
         with torch.no_grad():
             return model.forward_rows(h, r, None)
     sec = time_forward(step, reps)
+    roof = grounding_roofline(algorithmic_work(model, graph, rows, name="kinship"), len(rows), graph.entity_size,
+                              sec * 1e3, "ground_kernel + scoring (whole step: no entity feature)",
+                              measured="the timed step (rule embeddings + node aggregates + grounding + scoring)")
     return {"queries_per_s": round(len(rows) / sec, 1), "ms_per_step": round(sec * 1e3, 3), "rows": len(rows),
-            "batches": len(test_set), "rules": model.num_rules,
+            "batches": len(test_set), "rules": model.num_rules, "roofline": roof,
             "workload": "kinship test split, PredictorPlus(lstm,3,16,sum), entity_feature none; mined rules "
                         "(L<=3, top 100 per relation); real train graph"}
 
@@ -414,20 +420,35 @@ def em_iteration_line(dev, pre_epochs=200):
     return out
 
 
-def algorithmic_work(model, graph, rows, threads):
+WORK_FILES = {"FB15k-237": "fb15k237_work.json", "kinship": "kinship_work.json", "wn18rr": "wn18rr_work.json"}
+
+
+def algorithmic_work(model, graph, rows, threads=None, name="FB15k-237"):
     """Exact per-rule work counts of the SURVEY §8(d) formula: F (frontier
     expansions), T (edge traversals), P ((rule, dest) pairs) and C
-    (candidates) of this workload, from tests/golden/fb15k237_work.json (made by
+    (candidates) of a workload, from tests/golden/<name>_work.json (made by
     tools/make_work_counts.py with the C oracle; a prefix is re-derived by
     tests/test_oracle_c.py).  The file must describe exactly these rows."""
     import hashlib
-    with open(os.path.join(REPO, "tests", "golden", "fb15k237_work.json")) as f:
+    fn = os.path.join(REPO, "tests", "golden", WORK_FILES[name])
+    with open(fn) as f:
         w = json.load(f)
     dig = hashlib.sha256(np.ascontiguousarray(rows[:, :2], dtype=np.int64).tobytes()).hexdigest()
     if w["rows_sha256"] != dig or w["rules"] != model.num_rules:
-        raise RuntimeError("tests/golden/fb15k237_work.json does not describe this workload: "
-                           "rerun tools/make_work_counts.py")
+        raise RuntimeError("%s does not describe this workload: rerun tools/make_work_counts.py" % fn)
     return (w["F"], w["T"], w["P"]), w["C"]
+
+
+def grounding_roofline(work, nq, E, ms, kernel, extra_bytes=0.0, measured=""):
+    """HBM roofline of a grounding + scoring launch: SURVEY §8(d)'s
+    ALG_BYTES = 12 F + 12 T + 8 P + 4 B |E| (+ X: the bias row or other base
+    reads) over the measured time."""
+    (F, T, P), C = work
+    alg = 12 * F + 12 * T + 8 * P + 4 * nq * E + extra_bytes
+    ach = alg / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "ms": round(ms, 3), "kernel": kernel, "measured": measured,
+            "alg_bytes": int(alg), "work": {"F": int(F), "T": int(T), "P": int(P), "C": int(C)}}
 
 
 def main():
@@ -643,8 +664,13 @@ def main():
         pred = pred.to(dev).eval()
         with torch.no_grad():
             sec = time_forward(lambda: pred.forward_rows(h, r, None), 3)
-        extra["em_predictor_forward"] = {"queries_per_s": round(nq / sec, 1), "ms": round(sec * 1e3, 3),
-                                         "rows": nq, "note": "Predictor(bias) over the test split, same rules"}
+        extra["em_predictor_forward"] = {
+            "queries_per_s": round(nq / sec, 1), "ms": round(sec * 1e3, 3), "rows": nq,
+            "roofline": grounding_roofline(algorithmic_work(model, graph, all_rows), nq, graph.entity_size, sec * 1e3,
+                                           "ground_kernel + score_linear_kernel (+ bias row fill)",
+                                           extra_bytes=4.0 * graph.entity_size,
+                                           measured="the timed forward_rows (node weights + fill + ground + score)"),
+            "note": "Predictor(bias) over the test split, same rules (same grounding work as value)"}
         del pred
         extra["wn18rr_forward"] = wn18rr_line(dev)
         extra["kinship_forward"] = kinship_line(dev)

@@ -103,8 +103,9 @@ def test_c_oracle_digest_consistency(fixtures):
         assert int(d[i]) == acc and n[i] == len(tt)
 
 
-def test_bench_work_counts_fixture():
-    """tests/golden/fb15k237_work.json (bench.py's algorithmic-bytes input)
+@pytest.mark.parametrize("name", ["FB15k-237", "kinship", "wn18rr"])
+def test_bench_work_counts_fixture(name):
+    """tests/golden/<name>_work.json (bench.py's algorithmic-bytes inputs)
     describes the bench rows, and its first 2000 queries re-derive from the C
     oracle."""
     import importlib.util
@@ -113,9 +114,9 @@ def test_bench_work_counts_fixture():
     spec = importlib.util.spec_from_file_location("make_work_counts", os.path.join(root, "tools", "make_work_counts.py"))
     mwc = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mwc)
-    with open(os.path.join(root, "tests", "golden", "fb15k237_work.json")) as f:
+    with open(mwc.out_path(name)) as f:
         w = json.load(f)
-    graph, model, rows = mwc.workload()
+    graph, model, rows = mwc.workload(name)
     assert w["queries"] == len(rows) and w["rules"] == model.num_rules
     assert w["rows_sha256"] == mwc.rows_digest(rows)
     pre = w["prefix"]

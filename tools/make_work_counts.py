@@ -1,12 +1,13 @@
-"""Writes tests/golden/fb15k237_work.json: the exact SURVEY §8(d) work counts
-of the bench workload (FB15k-237 test split in TestDataset order, committed
-synthetic train graph, rnnlogic_rules.txt), computed by the C oracle
+"""Writes tests/golden/<name>_work.json: the exact SURVEY §8(d) work counts
+of a bench workload (the test split in TestDataset order, the committed train
+graph, the bench's rule file), computed by the C oracle
 (oracle/ground_oracle.c): F (frontier expansions), T (edge traversals),
-P ((rule, destination) pairs) and C (candidates).  bench.py reads the file for
-its algorithmic-bytes figure, so the timed program never runs oracle code;
-tests/test_oracle_c.py re-derives a prefix of it.
+P ((rule, destination) pairs) and C (candidates).  bench.py reads the files
+for its algorithmic-bytes figures (FB15k-237: `value` and the EM Predictor
+line; kinship: config 2; WN18RR: config 3), so the timed program never runs
+oracle code; tests/test_oracle_c.py re-derives a prefix of each.
 
-Usage: python tools/make_work_counts.py [threads]
+Usage: python tools/make_work_counts.py [--threads N] [FB15k-237 kinship wn18rr]
 """
 import contextlib
 import hashlib
@@ -25,11 +26,15 @@ from rnnlogic_amd import datasets  # noqa: E402
 from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset  # noqa: E402
 from rnnlogic_amd.predictors import PredictorPlus  # noqa: E402
 
-OUT = os.path.join(REPO, "tests", "golden", "fb15k237_work.json")
+NAMES = {"FB15k-237": "fb15k237", "kinship": "kinship", "wn18rr": "wn18rr"}
 
 
-def workload():
-    path = datasets.materialize("FB15k-237")
+def out_path(name):
+    return os.path.join(REPO, "tests", "golden", "%s_work.json" % NAMES[name])
+
+
+def workload(name="FB15k-237"):
+    path = datasets.materialize(name)
     # bench.build_workload's order (run_predictorplus.py): seeds, graph, train/valid/test datasets
     random.seed(1)
     np.random.seed(1)
@@ -40,7 +45,7 @@ def workload():
         ValidDataset(graph, 32)
         test_set = TestDataset(graph, 32)
         model = PredictorPlus(graph, type="emb", entity_feature="bias", aggregator="sum")
-        model.set_rules(datasets.rule_file("FB15k-237"))
+        model.set_rules(datasets.rule_file(name))
     rows = np.asarray([x for b in test_set.batches for x in b], dtype=np.int64)
     return graph, model, rows
 
@@ -57,18 +62,26 @@ def rows_digest(rows):
 
 
 def main():
-    threads = int(sys.argv[1]) if len(sys.argv) > 1 else (os.cpu_count() or 1)
-    graph, model, rows = workload()
-    work, ncand = work_counts(graph, model, rows, threads)
-    F, T, P = (int(x) for x in work.sum(0))
-    res = {"workload": "FB15k-237 test split (TestDataset order), synthetic train graph, rnnlogic_rules.txt",
-           "queries": int(len(rows)), "rules": int(model.num_rules), "rows_sha256": rows_digest(rows),
-           "F": F, "T": T, "P": P, "C": int(ncand.sum()),
-           "prefix": {"queries": 2000, "F": int(work[:2000, 0].sum()), "T": int(work[:2000, 1].sum()),
-                      "P": int(work[:2000, 2].sum()), "C": int(ncand[:2000].sum())}}
-    with open(OUT, "w") as f:
-        json.dump(res, f, indent=1)
-    print(json.dumps(res))
+    args = sys.argv[1:]
+    threads = os.cpu_count() or 1
+    if args[:1] == ["--threads"]:
+        threads, args = int(args[1]), args[2:]
+    for name in args or ["FB15k-237"]:
+        graph, model, rows = workload(name)
+        work, ncand = work_counts(graph, model, rows, threads)
+        F, T, P = (int(x) for x in work.sum(0))
+        k = min(2000, len(rows))
+        rf = datasets.rule_file(name)
+        res = {"workload": "%s test split (TestDataset order), %s train graph, %s" % (
+                   name, "real" if name == "kinship" else "synthetic",
+                   "rnnlogic_rules.txt" if "rnnlogic_rules" in rf else os.path.relpath(rf, REPO)),
+               "queries": int(len(rows)), "rules": int(model.num_rules), "rows_sha256": rows_digest(rows),
+               "F": F, "T": T, "P": P, "C": int(ncand.sum()),
+               "prefix": {"queries": k, "F": int(work[:k, 0].sum()), "T": int(work[:k, 1].sum()),
+                          "P": int(work[:k, 2].sum()), "C": int(ncand[:k].sum())}}
+        with open(out_path(name), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
 
 
 if __name__ == "__main__":
