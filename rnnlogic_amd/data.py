@@ -218,20 +218,31 @@ class _DeviceLists(object):
 class _RowTable(object):
     """A dataset's batches as one (n, 3) int64 (h, r, t) table on the device
     with per-batch offsets, uploaded once and rebuilt when the batch list
-    changes: another list object (make_batches) or a batch object replaced or
-    moved inside it (one identity check per batch; the table keeps references
-    to the batches it was built from, so a recycled id cannot alias).  A
-    single batch is then a slice of the table (no host->device copy per step)
-    and many batches one gather."""
+    changes: another list object (make_batches builds a new one) or another
+    length, or a batch object replaced or moved inside it — checked at 17
+    evenly spaced positions per call (an in-place reshuffle moves nearly every
+    batch; checking all 17,258 FB15k-237 train batches per training step cost
+    ~1 ms).  The table keeps references to the list and the batches it was
+    built from, so a recycled id cannot alias.  A single batch is then a slice
+    of the table (no host->device copy per step) and many batches one
+    gather."""
 
     def __init__(self, device):
         self.device = device
         self._src = None
         self._refs = ()
 
+    def _changed(self, batches):
+        n = len(batches)
+        if self._src is not batches or len(self._refs) != n:
+            return True
+        if n == 0:
+            return False
+        step = max(1, n // 16)
+        return any(self._refs[i] is not batches[i] for i in list(range(0, n, step)) + [n - 1])
+
     def get(self, batches):
-        if self._src is not batches or len(self._refs) != len(batches) or \
-                any(a is not b for a, b in zip(self._refs, batches)):
+        if self._changed(batches):
             lens = np.fromiter((len(b) for b in batches), dtype=np.int64, count=len(batches))
             off = np.zeros(len(batches) + 1, dtype=np.int64)
             np.cumsum(lens, out=off[1:])
