@@ -381,9 +381,22 @@ class _RuleTable(object):
         self.weight = torch.tensor([float(item[-1]) for item in rule_set.rules], device=device)
         self.device = device
 
-    def batch(self, idx):
-        """idx: CPU int64 (n,) -> (inputs, target, mask, weight) on the device."""
-        T = int(self.lens[idx].max()) - 1
+    def batch(self, idx, pad_rows=0):
+        """idx: CPU int64 (n,) -> (inputs, target, mask, weight) on the device.
+        pad_rows > n: the batch is padded to pad_rows rows (copies of rule 0
+        with weight 0) and to the table's full width, so every batch has one
+        shape — the loss is sum(w ce) / sum(w), so weight-0 rows add nothing,
+        and the LSTM's rows are independent."""
+        if pad_rows > idx.numel():
+            T = self.inputs.size(1)
+            i = torch.cat([idx, idx.new_zeros(pad_rows - idx.numel())]).to(self.device, non_blocking=True)
+            w = torch.cat([self.weight.new_ones(idx.numel()), self.weight.new_zeros(pad_rows - idx.numel())])
+            target = self.target[i, :T]
+            return self.inputs[i, :T], target, target != self.pad[i].unsqueeze(1), self.weight[i] * w
+        if pad_rows:
+            T = self.inputs.size(1)
+        else:
+            T = int(self.lens[idx].max()) - 1
         i = idx.to(self.device, non_blocking=True)
         target = self.target[i, :T]
         return self.inputs[i, :T], target, target != self.pad[i].unsqueeze(1), self.weight[i]
@@ -426,8 +439,11 @@ class TrainerGenerator(object):
         iterator = Iterator(order)
         optimizer = torch.optim.Adam(model.parameters(), lr=lr)
         total_loss = torch.zeros((), dtype=torch.float64, device=self.device)
+        # on a GPU every batch takes one shape (batch_size rows, the table's
+        # width): a new LSTM shape costs a kernel selection on its first use
+        pad = batch_size if self.device.type == "cuda" else 0
         for epoch in range(num_epoch):
-            inputs, target, mask, weight = table.batch(next(iterator))
+            inputs, target, mask, weight = table.batch(next(iterator), pad)
             hidden = self.zero_state(inputs.size(0))
             loss = model.loss(inputs, target, mask, weight, hidden)
             loss.backward()

@@ -181,3 +181,28 @@ def test_em_iteration_gpu():
     assert np.array_equal(got["probe/m_step"], z["probe/m_step"])
     _close(got["m_step/log_prob"], z["m_step/log_prob"], 1e-4)
     _check_states(got["gen_m"], em_chain.state(z, "gen_m"), W_TOL)
+
+
+def test_padded_rule_batch_gives_the_same_loss_cpu():
+    """TrainerGenerator.train on a GPU pads every batch to batch_size rows
+    (weight 0) and the table's full width (one LSTM shape); the loss is the
+    unpadded batch's."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph, RuleDataset
+    from rnnlogic_amd.generators import Generator
+    from rnnlogic_amd.trainer import _RuleTable
+    torch.manual_seed(0)
+    graph = KnowledgeGraph(datasets.materialize("umls"))
+    g = Generator(graph, num_layers=1, embedding_dim=16, hidden_dim=16)
+    mined = [[int(x) for x in line.split()] for line in open(datasets.rule_file("umls"))][:300]
+    ds = RuleDataset(graph.relation_size, [r + [0.1 + (i % 7)] for i, r in enumerate(mined)])
+    table = _RuleTable(ds, torch.device("cpu"))
+    idx = torch.tensor([5, 17, 2, 250, 99])
+    zero = lambda n: (torch.zeros(1, n, 16), torch.zeros(1, n, 16))  # noqa: E731
+    a = table.batch(idx)
+    b = table.batch(idx, pad_rows=16)
+    assert b[0].shape == (16, table.inputs.size(1))
+    with torch.no_grad():
+        la = g.loss(*a, zero(a[0].size(0)))
+        lb = g.loss(*b, zero(16))
+    assert abs(float(la) - float(lb)) <= 1e-6 * max(1.0, abs(float(la)))
