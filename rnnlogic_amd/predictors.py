@@ -207,14 +207,15 @@ class _PredictorLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, rule_weights, bias, model, all_h, all_r, edges_to_remove):
-        score, mask, n_cand, ws, scale = model._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
+        score, mask, n_cand, ws, scale, n_total = model._forward_launch(all_h, all_r, edges_to_remove,
+                                                                        single_relation=True)
         device = score.device
         ctx.model, ctx.ws, ctx.scale, ctx.n_cand = model, ws, scale, n_cand
         # a batch without any candidate returns `mask + bias` in the reference
         # (predictors.py:67-71): the rule weights are not in its graph, so they
         # get no gradient (None, which Adam skips — a zero gradient would still
         # move them through the moment estimates)
-        ctx.no_cand = score.numel() == 0 or int(model._last_totals[0]) == 0
+        ctx.no_cand = n_total == 0
         ctx.gen = model._ws_gen.get(device)
         ctx.rows = model._rows(all_h, all_r, edges_to_remove)[1:]
         ctx.has_bias = bias is not None
@@ -313,12 +314,13 @@ class Predictor(_HipGrounding, torch.nn.Module):
     def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False):
         """Forward for any rows (one or many reference batches, mixed
         relations): (score (n, |E|) f32, mask (n, |E|) bool[, n_cand])."""
-        score, mask, n_cand, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
+        score, mask, n_cand, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
     def _forward_launch(self, all_h, all_r, edges_to_remove, single_relation=False):
         """rnnl_predictor_forward over the rows -> (score, mask, n_cand, ws,
-        scale); the workspace keeps the grounding for a backward.  With
+        scale, candidate total); the workspace keeps the grounding for a
+        backward.  With
         `single_relation` the reference's one-relation-per-batch check
         (predictors.py:54-55) is read back with the launch status (no extra
         host sync)."""
@@ -327,7 +329,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         if nq == 0:  # no rows: empty outputs, no launch
             return (torch.empty((0, E), dtype=torch.float32, device=device),
                     torch.empty((0, E), dtype=torch.bool, device=device),
-                    torch.empty(0, dtype=torch.int32, device=device), None, None)
+                    torch.empty(0, dtype=torch.int32, device=device), None, None, 0)
         mixed = None
         if single_relation:
             mixed = torch.empty((), dtype=torch.bool, pin_memory=True)
@@ -356,9 +358,8 @@ class Predictor(_HipGrounding, torch.nn.Module):
         ws, scale = self._launch(device, nq, run, totals)
         if mixed is not None:
             assert not bool(mixed), "a batch must hold one relation (predictors.py:54-55)"
-        self._last_totals = totals
         mask = torch.ones((nq, E), dtype=torch.bool, device=device) if bias_mode else mask8.bool()
-        return score, mask, n_cand, ws, scale
+        return score, mask, n_cand, ws, scale, int(totals[0])
 
     # ------------------------------------------------------------------ reference API
     # every entity is scored (the reference's mask is all True) with the bias feature
@@ -374,7 +375,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
             bias = self.bias if self.entity_feature == "bias" else None
             score, mask = _PredictorLinear.apply(self.rule_weights, bias, self, all_h, all_r, edges_to_remove)
         else:
-            score, mask, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
+            score, mask, _, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
         if self.entity_feature != "bias":
             # early return `mask - float('-inf')` (predictors.py:68-72): +inf where the
             # batch has no candidate at all (mask all False), without a host read
