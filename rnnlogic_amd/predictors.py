@@ -573,6 +573,9 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # per-candidate outputs to the workspace; a short apply pass adds them
         # into the finished RotatE rows (rnnl_predictorplus_apply)
         self.overlap_deferred = os.environ.get("RNNL_OVERLAP_DEFERRED", "1") != "0"
+        # with several chunks, chunk k's deferred scoring on side stream B
+        # beside chunk k + 1's grounding on A (RNNL_OVERLAP_PIPELINE=1)
+        self.overlap_pipeline = os.environ.get("RNNL_OVERLAP_PIPELINE", "0") == "1"
         # below this many rows the forward runs on one stream (bit-identical);
         # 0: overlap from 2 rows on (one 32-row reference batch per call: 0.78
         # ms overlapped vs 1.02 ms on one stream, the grounding's latency then
@@ -810,14 +813,17 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         key = (self._device_index(device), "ev")
         evs = self._side.get(key)
         if evs is None or len(evs[0]) < K:
-            evs = ([torch.cuda.Event() for _ in range(K)], [torch.cuda.Event() for _ in range(K)])
+            evs = tuple([torch.cuda.Event() for _ in range(K)] for _ in range(3))
             self._side[key] = evs
         return evs
 
     def _side_streams(self, device):
         key = self._device_index(device)
         if key not in self._side:
-            self._side[key] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+            # RNNL_SIDE_PRIORITY=-1: the side streams on a high-priority queue
+            # (their workgroups dispatched first as RotatE's retire; A/B)
+            prio = int(os.environ.get("RNNL_SIDE_PRIORITY", "0"))
+            self._side[key] = (torch.cuda.Stream(device, priority=prio), torch.cuda.Stream(device, priority=prio))
         return self._side[key]
 
     def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec):
@@ -841,20 +847,29 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             side_g.wait_stream(main)  # inputs, node aggregates, workspaces
             side_s.wait_stream(main)
             rec("base")
-            ev_g, ev_r = self._overlap_events(device, K)
+            ev_g, ev_r, ev_s = self._overlap_events(device, K)
+            pipeline = deferred and self.overlap_pipeline and K > 1
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
                 _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h[lo:].data_ptr(),
                              all_r[lo:].data_ptr(), etr[lo:].data_ptr() if etr is not None else None, hi - lo,
                              n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_ground_wg,
                              side_g.cuda_stream)
+                if deferred and pipeline:
+                    # chunk k's scoring on side stream B, beside chunk k + 1's grounding
+                    ev_g[k].record(side_g)
+                    side_s.wait_event(ev_g[k])
                 if deferred:  # the score pass does not touch `score`: it runs beside RotatE too
+                    ss = side_s if pipeline else side_g
                     _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
                                  all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None,
                                  n_cand[lo:].data_ptr(), digest[lo:].data_ptr() if digest is not None else None,
                                  wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_score_wg, 1,
-                                 side_g.cuda_stream)
-                ev_g[k].record(side_g)
+                                 ss.cuda_stream)
+                    if pipeline:
+                        ev_s[k].record(side_s)
+                if not pipeline:
+                    ev_g[k].record(side_g)
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
                 self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=False)
@@ -862,7 +877,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             rec("ground")
             for k in range(K if deferred else 0):
                 lo, hi = bounds[k], bounds[k + 1]
-                main.wait_event(ev_g[k])
+                main.wait_event(ev_s[k] if pipeline else ev_g[k])
                 _native.call("rnnl_predictorplus_apply", wss[k].data_ptr(), hi - lo, scale, n_cand[lo:].data_ptr(),
                              params.feature, score[lo:].data_ptr(), None, self.num_entities, main.cuda_stream)
             for k in range(0 if deferred else K):
