@@ -139,6 +139,11 @@ struct KParams {
                      // (the first n_cand entries of a query's run)
   int2 *bent;        // bucket entries: (trie node, path count bits)
   float *memo;       // SUM: score_model output of a candidate reached by one path of one leaf node
+  // SUM: score_model outputs keyed by a candidate's bucket entries when it has
+  // one or two (pair memo, score_sum_chunk_kernel); nullptr = off
+  unsigned long long *ptab, *ptab_region;
+  int32_t psbits, pbr, pbo, pbc, pbc3;  // slots 2^psbits; key field bits: relation, node offset, count (pair,
+                                       // triple; 0: no triple keys)
   int2 *chunks;      // PNA: scoring work units (query, first candidate) of <= 64 candidates each
   int64_t chunk_cap;
   unsigned long long *prof;  // diagnostic phase cycle counters (nullable)
@@ -188,7 +193,8 @@ __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, in
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
-  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, off_chunk, chunk_cap, off_memo, total;
+  int64_t off_qbase, off_qscale, off_cand, off_bent, off_cout, off_slots, off_chunk, chunk_cap, off_memo, off_ptab,
+      ptab_bits, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -224,6 +230,11 @@ static Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   o += 8 * L.chunk_cap + 4 * (std::max<int64_t>(nq, 1) / 256 + 1);  // list | per-block chunk totals
   L.off_memo = o = align256(o);
   o += 4 * n_nodes;
+  // pair memo (SUM): 2^ptab_bits 8-B slots, ~128 per row, 2^16 .. 2^23
+  L.ptab_bits = 16;
+  while (L.ptab_bits < 23 && (1ll << L.ptab_bits) < 128 * std::max<int64_t>(nq, 1)) ++L.ptab_bits;
+  L.off_ptab = o = align256(o);
+  if (n_nodes > 0) o += 8ll << L.ptab_bits;
   L.total = o;
   return L;
 }
@@ -1856,6 +1867,9 @@ __device__ __forceinline__ void gather_sum_entry(const KParams &p, int n, uint32
 // FuncToNodeSum tail + score_model on the candidate's feature sums
 __device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const float *relb, const float f[16]) {
   using L = WL<RNNL_AGG_SUM>;
+#ifdef RNNL_DIAG_NOMLP  // diagnostic build: the MLP's cost bounded (every caller)
+  return f[0] + f[15];
+#endif
   float x1[16];
 #pragma unroll
   for (int o = 0; o < 16; ++o) {
@@ -2005,11 +2019,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
         // keep the loop-invariant LDS weight reads inside the loop (hoisted,
         // they would pin ~200 VGPRs and starve occupancy)
         asm volatile("" ::: "memory");
-#ifdef RNNL_DIAG_NOMLP  // diagnostic build: no MLP
-        const float out = f[0] + f[15];
-#else
         const float out = mlp_sum(s_w, s_relb, f);
-#endif
 #ifdef RNNL_DIAG_NOSCORE  // diagnostic build: no score/mask traffic
         if (out == 1234.5f) p.score[idx] = base;
         continue;
@@ -2216,6 +2226,82 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
   }
 }
 
+// Pair memo.  A candidate's feature is the exact sum of count x record over
+// its bucket entries, so candidates whose entries are equal get bit-identical
+// score_model outputs.  On an FB15k-237 test sample 57 % of the candidates
+// past the single-path memo hold one or two entries and 19 % three, and
+// within a 32-row relation batch only 7 % / 27 % of those entry lists are
+// distinct.  The key packs (relation, each entry's node offset and count, in
+// canonical order) exactly into K = 31 + psbits bits and is mixed by a
+// bijection of [0, 2^K): the low psbits bits pick the slot, the high 31 bits
+// are the tag, so (slot, tag) identifies the entries exactly.  A slot is one
+// 8-B word (tag + 1) << 32 | output bits, written and read whole: any word a
+// lane reads is some key's true output, and a lost or overwritten insert
+// only costs a recomputation.
+constexpr unsigned long long PAIR_NOKEY = ~0ull;
+
+__device__ __forceinline__ void entry_cswap(unsigned &oa, unsigned &ca, unsigned &ob, unsigned &cb) {
+  if (ob < oa || (ob == oa && cb < ca)) {
+    const unsigned to = oa, tc = ca;
+    oa = ob;
+    ca = cb;
+    ob = to;
+    cb = tc;
+  }
+}
+
+// z = 1..3 bucket entries (absent ones (0, 0): a node offset is never 0, the
+// root ends no rule).  Format bit 0: one or two entries, pbc-bit counts; 1:
+// three entries, pbc3-bit counts.
+__device__ __forceinline__ unsigned long long pair_key(const KParams &p, int r, int root, int z, int2 b0, int2 b1,
+                                                       int2 b2) {
+  unsigned o0 = (unsigned)(b0.x - root), c0 = (unsigned)b0.y;
+  unsigned o1 = z >= 2 ? (unsigned)(b1.x - root) : 0u, c1 = z >= 2 ? (unsigned)b1.y : 0u;
+  unsigned o2 = z >= 3 ? (unsigned)(b2.x - root) : 0u, c2 = z >= 3 ? (unsigned)b2.y : 0u;
+  if (z >= 2) entry_cswap(o0, c0, o1, c1);  // canonical order
+  if (z == 3) {
+    entry_cswap(o1, c1, o2, c2);
+    entry_cswap(o0, c0, o1, c1);
+  }
+  const int bc = z == 3 ? p.pbc3 : p.pbc;
+  if (bc <= 0 || ((c0 | c1 | c2) >> bc)) return PAIR_NOKEY;  // a count past the key's field
+  unsigned long long k = z == 3 ? 1ull : 0ull;
+  int sh = 1;
+  k |= (unsigned long long)r << sh;
+  sh += p.pbr;
+  k |= (unsigned long long)o0 << sh;
+  sh += p.pbo;
+  k |= (unsigned long long)o1 << sh;
+  sh += p.pbo;
+  if (z == 3) {
+    k |= (unsigned long long)o2 << sh;
+    sh += p.pbo;
+  }
+  k |= (unsigned long long)c0 << sh;
+  sh += bc;
+  k |= (unsigned long long)c1 << sh;
+  sh += bc;
+  if (z == 3) k |= (unsigned long long)c2 << sh;
+  const int K = 31 + p.psbits;
+  const unsigned long long mk = (1ull << K) - 1ull;
+  k = (k * 0x9E3779B97F4A7C15ull) & mk;  // odd multiplier mod 2^K, xor-shifts: a bijection of [0, 2^K)
+  k ^= k >> (K / 2);
+  k = (k * 0xBF58476D1CE4E5B9ull) & mk;
+  k ^= k >> (K / 2 + 1);
+  return k;
+}
+
+__device__ __forceinline__ bool pair_lookup(const KParams &p, unsigned long long m, float &out) {
+  const unsigned long long w = p.ptab[m & ((1ull << p.psbits) - 1ull)];
+  out = __uint_as_float((unsigned)w);
+  return (unsigned)(w >> 32) == (unsigned)(m >> p.psbits) + 1u;
+}
+
+__device__ __forceinline__ void pair_insert(const KParams &p, unsigned long long m, float out) {
+  p.ptab[m & ((1ull << p.psbits) - 1ull)] =
+      ((unsigned long long)((unsigned)(m >> p.psbits) + 1u) << 32) | (unsigned long long)__float_as_uint(out);
+}
+
 // SUM scoring over chunks (default; RNNL_SUM_CHUNKED=0 keeps
 // score_sum_memo_kernel): one wave x one 64-candidate chunk of one query at a
 // time (p.chunks, in row order), no
@@ -2228,7 +2314,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
 // score_sum_memo_kernel.
 template <bool DIGEST>
 __device__ __forceinline__ void sum_chunk_flush(const KParams &p, const float *s_w, const float *relb,
-                                                const int2 *queue, int m, float inv_scale) {
+                                                const int2 *queue, int m, float inv_scale, int r, int root) {
   const int lane = threadIdx.x & 63;
   if (lane < m) {
     const int2 it = queue[lane];
@@ -2243,7 +2329,14 @@ __device__ __forceinline__ void sum_chunk_flush(const KParams &p, const float *s
       atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + it.x),
                 (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
     asm volatile("" ::: "memory");  // keep the LDS weight reads inside (see score_sum_kernel)
-    sum_write_out(p, it.x, it.y, cr.x, mlp_sum(s_w, relb, f), base);
+    const float out = mlp_sum(s_w, relb, f);
+    sum_write_out(p, it.x, it.y, cr.x, out, base);
+    if (!DIGEST && p.ptab && cr.z <= 3) {
+      const int2 z0 = make_int2(0, 0);
+      const unsigned long long key = pair_key(p, r, root, cr.z, p.bent[cr.y], cr.z >= 2 ? p.bent[cr.y + 1] : z0,
+                                              cr.z >= 3 ? p.bent[cr.y + 2] : z0);
+      if (key != PAIR_NOKEY) pair_insert(p, key, out);
+    }
   }
 }
 
@@ -2275,7 +2368,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
   float *relb = s_relb[wv];
   int2 *queue = s_queue[wv];
-  int cur_r = -1, n = 0;  // wave-uniform: the queue's relation and length
+  int cur_r = -1, cur_root = 0, n = 0;  // wave-uniform: the queue's relation, its trie root, the queue length
   unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
   // chunks per dequeue: SUM_CK on large launches, fewer where that would leave
   // waves idle (at least 8 dequeues per wave)
@@ -2299,7 +2392,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
       const int m = drain ? min(n, 64) : (n >= 64 ? 64 : 0);
       if (m == 0) break;
       wave_lds_sync();
-      sum_chunk_flush<DIGEST>(p, s_w, relb, queue, m, inv_scale);
+      sum_chunk_flush<DIGEST>(p, s_w, relb, queue, m, inv_scale, cur_r, cur_root);
       n -= m;
       const int2 v = lane < n ? queue[m + lane] : make_int2(0, 0);
       wave_lds_sync();
@@ -2316,6 +2409,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
         relb[o] = acc;
       }
       cur_r = r;
+      cur_root = __builtin_amdgcn_readfirstlane(p.rl.head_root[r]);
     }
     const int nc = p.n_cand[q];
     const int64_t qb = p.q_base[q];
@@ -2324,6 +2418,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
     if (s < nc) {
       const int4 cr = p.cand[qb + s];
       queued = true;
+      unsigned long long key = PAIR_NOKEY;
       if (cr.z == 1) {
         const int2 be = p.bent[cr.y];
         if (be.y == 1) {  // one path of one leaf node: the memo
@@ -2334,7 +2429,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
                       (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)p.rl.node_nrules[be.x] ^
                                                                         mix64(p.rl.node_fp[be.x]))));
           sum_write_out(p, q, qb + s, cr.x, p.memo[be.x], base);
+        } else if (!DIGEST && p.ptab) {
+          key = pair_key(p, r, cur_root, 1, be, make_int2(0, 0), make_int2(0, 0));
         }
+      } else if (!DIGEST && p.ptab && cr.z <= 3) {
+        key = pair_key(p, r, cur_root, cr.z, p.bent[cr.y], p.bent[cr.y + 1],
+                       cr.z == 3 ? p.bent[cr.y + 2] : make_int2(0, 0));
+      }
+      float out;
+      if (key != PAIR_NOKEY && pair_lookup(p, key, out)) {  // the pair memo holds these entries' output
+        queued = false;
+        sum_write_out(p, q, qb + s, cr.x, out, sum_base(p, q, cr.x));
       }
     }
     const uint64_t bal = __ballot(queued);
@@ -2790,6 +2895,20 @@ static int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64
   p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
   p.bent = reinterpret_cast<int2 *>(base + Ly.off_bent);
   p.memo = reinterpret_cast<float *>(base + Ly.off_memo);
+  p.ptab = nullptr;  // set by launch_score where the pair memo applies
+  p.ptab_region = reinterpret_cast<unsigned long long *>(base + Ly.off_ptab);
+  p.psbits = (int32_t)Ly.ptab_bits;
+  {
+    auto bitlen = [](int64_t v) {
+      int b = 0;
+      while ((1ll << b) <= v) ++b;
+      return b;
+    };
+    p.pbr = bitlen(std::max<int64_t>(g->d.R - 1, 0));
+    p.pbo = bitlen(std::max<int64_t>(r->d.max_head_nodes - 1, 0));
+    p.pbc = std::min(20, (30 + p.psbits - p.pbr - 2 * p.pbo) / 2);  // K = 31 + psbits, one format bit
+    p.pbc3 = std::min(20, (30 + p.psbits - p.pbr - 3 * p.pbo) / 3);
+  }
   p.chunks = reinterpret_cast<int2 *>(base + Ly.off_chunk);
   p.chunk_cap = Ly.chunk_cap;
   p.prof = g_prof;
@@ -2836,6 +2955,12 @@ static bool score_memo_enabled() {
   return on;
 }
 
+// RNNL_SCORE_PAIRMEMO=0 turns the SUM pair memo off (A/B; bit-identical scores)
+static bool pair_memo_enabled() {  // read per launch: tests compare both settings in one process
+  const char *e = getenv("RNNL_SCORE_PAIRMEMO");
+  return !(e && e[0] == '0');
+}
+
 // RNNL_PNA_CHUNKED=0 selects the per-query PNA scoring kernel (A/B)
 static bool pna_chunked() {
   static const bool on = [] {
@@ -2854,7 +2979,8 @@ static bool sum_chunked() {
   return on;
 }
 
-static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int grid = 0) {
+static void launch_score(const KParams &p0, rnnl_rules r, hipStream_t st, int grid = 0) {
+  KParams p = p0;
   const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
@@ -2873,6 +2999,12 @@ static void launch_score(const KParams &p, rnnl_rules r, hipStream_t st, int gri
       if (sum_chunked()) {
         launch_chunk_list(p, st);
         if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);
+        // the pair memo (not with the test digest, which needs every candidate's entries); a key
+        // needs >= 2 count bits per entry
+        if (!p.digest && pair_memo_enabled() && p.pbc >= 2) {
+          p.ptab = p.ptab_region;
+          (void)hipMemsetAsync(p.ptab, 0, 8ull << p.psbits, st);
+        }
         const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * RNNL_SCORE_WG_PER_CU);
         if (p.digest)
           hipLaunchKernelGGL((score_sum_chunk_kernel<true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);

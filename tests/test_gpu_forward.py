@@ -164,6 +164,32 @@ def test_stream_overlap_is_bit_identical(case, dev):
     np.testing.assert_array_equal(outs[0][3].view(np.uint64), want_d)
 
 
+@pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "fb_lstm_sum_rotate", "kinship_lstm_sum_none",
+                                  "umls_lstm_sum_bias"])
+def test_pair_memo_is_bit_identical(case, dev, monkeypatch):
+    """The SUM pair memo (score_model outputs keyed by a candidate's one or
+    two bucket entries, ground.hip pair_key) reuses outputs of equal features:
+    scores, masks and candidate counts equal the launch without it, one stream
+    and overlapped, over many relation batches of the test split."""
+    fx = Fixture(case)
+    model = build_model(fx, dev)
+    test = np.asarray(graph_for(fx.dataset_path()).test_facts, dtype=np.int64)[:8000]
+    h = torch.from_numpy(test[:, 0]).to(dev)
+    r = torch.from_numpy(test[:, 1]).to(dev)
+    outs = []
+    for on, overlap in (("0", False), ("1", False), ("1", True)):
+        monkeypatch.setenv("RNNL_SCORE_PAIRMEMO", on)
+        model.overlap = overlap
+        with torch.no_grad():
+            out = model.forward_rows(h, r, None, return_ncand=True)
+        torch.cuda.synchronize()
+        outs.append([x.cpu().numpy() for x in out])
+    model.overlap = True
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "umls_emb_pna_rotate", "kinship_lstm_sum_none"])
 def test_dedupe_is_bit_identical(case, dev):
     """forward_rows(dedupe=True) computes each distinct (h, r) once: same
