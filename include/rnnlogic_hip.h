@@ -169,7 +169,12 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
  * score_model output into the workspace instead of adding it into `score`
  * (it then neither reads nor writes `score`, so it can run beside
  * rnnl_rotate_score); rnnl_predictorplus_apply adds the outputs into the
- * finished base score and sets mask (same fp32 sums as the direct pass). */
+ * finished base score and sets mask (same fp32 sums as the direct pass).
+ * deferred == 2 (feature add, mask NULL): the outputs are added atomically
+ * into `score`, which the caller zeroed and whose base score arrives by
+ * atomic adds too (rnnl_rotate_score accumulate == 2) — two addends on an
+ * exact zero round to fl(base + out) in either order, so no apply pass is
+ * needed and the result is the direct pass's bit for bit. */
 int rnnl_predictorplus_apply(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
                              int32_t feature, float *score, uint8_t *mask, int32_t n_entities, void *stream);
 /* After a forward: RNNL_OK, or RNNL_ERR_OVERFLOW if any query exceeded the
@@ -287,7 +292,8 @@ int rnnl_fill_value(float value, int64_t n, float *score, void *stream);
  * per-call workspace of rnnl_rotate_workspace_size bytes (h o r of every
  * query in DIRECT mode, plus per-32-dim chunk sums when a launch has few rows
  * — the split form, bitwise equal to the one-pass kernel; 0 for MFMA).
- * accumulate != 0 adds into score. */
+ * accumulate: 0 stores, 1 adds into score, 2 adds atomically (a zeroed score
+ * shared with rnnl_predictorplus_score deferred == 2 on another stream). */
 #define RNNL_ROTATE_DIRECT 0
 #define RNNL_ROTATE_MFMA 1
 int rnnl_rotate_table_sizes(int32_t n_entities, int32_t dim, int32_t n_rel_total, int32_t mode,

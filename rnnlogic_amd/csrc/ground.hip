@@ -135,6 +135,7 @@ struct KParams {
   int64_t *q_base;   // per query: first pool index of its run
   float *q_scale;    // per query: PNA mean log-degree
   float *cand_out;   // deferred scoring: score_model output per candidate record (nullable)
+  int32_t atomic_out;  // deferred scoring into a zeroed score matrix: atomic adds (no cand_out stores)
   int4 *cand;        // per pool index: candidate record (entity, bucket start, bucket length, 0)
                      // (the first n_cand entries of a query's run)
   int2 *bent;        // bucket entries: (trie node, path count bits)
@@ -159,6 +160,18 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 }
 
 __device__ __forceinline__ uint32_t hash32(uint32_t k) { return k * 2654435761u; }
+
+// Deferred scoring output of candidate record ci (entity t of row q): stored
+// for rnnl_predictorplus_apply, or (atomic_out) added into a score matrix that
+// starts at zero and receives the base score by atomic adds too — two addends
+// on an exact zero give fl(base + out) in either order, so the result is the
+// one-stream path's bit for bit.
+__device__ __forceinline__ void deferred_store(const KParams &p, int q, int64_t ci, int t, float out) {
+  if (p.atomic_out)
+    unsafeAtomicAdd(p.score + (int64_t)q * p.g.E + t, out);
+  else
+    p.cand_out[ci] = out;
+}
 
 
 // Per-slot scratch: two frontier buffers and the contribution list, each an
@@ -1491,8 +1504,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_WAV
                                        p.digest ? &dg : nullptr, t);
 #endif
       if (p.digest) atomicAdd(&s_dig, (unsigned long long)dg);
-      if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
-        p.cand_out[qb + s] = out;
+      if (p.cand_out) {  // deferred: added once the base score exists (deferred_store)
+        deferred_store(p, q, qb + s, t, out);
         continue;
       }
       const int64_t idx = (int64_t)q * p.g.E + t;
@@ -1690,8 +1703,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_CHU
     const float out = score_one_2walk<RNNL_AGG_PNA>(p, s_w, relb, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t);
 #endif
     if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
-    if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
-      p.cand_out[qb + s] = out;
+    if (p.cand_out) {  // deferred: added once the base score exists (deferred_store)
+      deferred_store(p, q, qb + s, t, out);
       continue;
     }
     const int64_t idx = (int64_t)q * p.g.E + t;
@@ -2024,8 +2037,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
         if (out == 1234.5f) p.score[idx] = base;
         continue;
 #endif
-        if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
-          p.cand_out[qb + s2] = out;
+        if (p.cand_out) {  // deferred: added once the base score exists (deferred_store)
+          deferred_store(p, q, qb + s2, t, out);
           continue;
         }
         p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + base;
@@ -2114,8 +2127,8 @@ __global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__
 }
 
 __device__ __forceinline__ void sum_write_out(const KParams &p, int q, int64_t ci, int t, float out, float base) {
-  if (p.cand_out) {  // deferred: rnnl_predictorplus_apply adds it once the base score exists
-    p.cand_out[ci] = out;
+  if (p.cand_out) {  // deferred: added once the base score exists (deferred_store)
+    deferred_store(p, q, ci, t, out);
     return;
   }
   const int64_t idx = (int64_t)q * p.g.E + t;
@@ -3087,7 +3100,8 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
                              const int64_t *all_r, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
                              uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t workgroups,
                              int32_t deferred, void *stream) {
-  if (bad_params(pp, score) || !n_cand) {
+  if (bad_params(pp, score) || !n_cand || deferred < 0 || deferred > 2 ||
+      (deferred == 2 && (mask || pp->feature != RNNL_FEATURE_ADD))) {
     set_error("rnnl_predictorplus_score: bad arguments");
     return RNNL_ERR_INVALID;
   }
@@ -3099,6 +3113,7 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
   set_score_params(p, pp, score, mask, digest);
   if (deferred) {
     p.cand_out = reinterpret_cast<float *>(static_cast<unsigned char *>(ws) + make_layout(nq, scale).off_cout);
+    p.atomic_out = deferred == 2;
   }
   hipStream_t st = (hipStream_t)stream;
   RNNL_HIP_CHECK(hipMemsetAsync(p.ws + 4 * H_DEQUEUE2, 0, 4, st));  // the scoring dequeue counter

@@ -277,7 +277,10 @@ __global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const f
         if (q < nq && e < E) {
           const int64_t idx = (int64_t)q * E + e;
           const float val = gamma - acc[qg][g][j];
-          score[idx] = accumulate ? score[idx] + val : val;
+          if (accumulate == 2)
+            unsafeAtomicAdd(score + idx, val);
+          else
+            score[idx] = accumulate ? score[idx] + val : val;
         }
       }
 }
@@ -463,7 +466,10 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
       if (q0 + k < nq) {
         const int64_t idx = (int64_t)(q0 + k) * E + e;
         const float v = gamma - acc[k];
-        score[idx] = accumulate ? score[idx] + v : v;
+        if (accumulate == 2)  // into a zeroed matrix beside deferred scoring adds (rnnl_rotate_score)
+          unsafeAtomicAdd(score + idx, v);
+        else
+          score[idx] = accumulate ? score[idx] + v : v;
       }
     }
   }
@@ -555,7 +561,10 @@ __global__ __launch_bounds__(256) void rotate_combine_kernel(const float *__rest
     for (int c = 0; c < nchunks; ++c) acc += parts[(int64_t)c * n + i];
     acc += parts[(int64_t)nchunks * n + i];
     const float v = gamma - acc;
-    score[i] = accumulate ? score[i] + v : v;
+    if (accumulate == 2)
+      unsafeAtomicAdd(score + i, v);
+    else
+      score[i] = accumulate ? score[i] + v : v;
   }
 }
 
@@ -834,7 +843,8 @@ int rnnl_rotate_workspace_size(int32_t nq, int32_t E, int32_t D, int32_t mode, s
 int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, int32_t D, float gamma,
                       const int64_t *all_h, const int64_t *all_r, int32_t nq, int32_t E, float *score,
                       int32_t accumulate, int32_t mode, void *workspace, size_t ws_bytes, void *stream) {
-  if (!eemb || !etab || !rtab || !all_h || !all_r || !score || D <= 0 || E <= 0 || nq < 0 || !valid_mode(mode)) {
+  if (!eemb || !etab || !rtab || !all_h || !all_r || !score || D <= 0 || E <= 0 || nq < 0 || !valid_mode(mode) ||
+      accumulate < 0 || accumulate > 2) {
     set_error("rnnl_rotate_score: bad arguments");
     return RNNL_ERR_INVALID;
   }

@@ -104,7 +104,8 @@ class RotatE(torch.nn.Module):
         return self._ws.data_ptr(), need.value
 
     def score_into(self, all_h, all_r, out, accumulate=False):
-        """out (B, |E|) (+)= gamma - dist(h o r, e) for every entity (HIP)."""
+        """out (B, |E|) (+)= gamma - dist(h o r, e) for every entity (HIP);
+        accumulate 2: atomic adds (rnnl_rotate_score)."""
         if not self.eemb.is_cuda:
             raise RuntimeError("RotatE.forward runs on the HIP path; move the module to a GPU")
         all_h = all_h.to(self.eemb.device, torch.int64).contiguous()
@@ -114,7 +115,7 @@ class RotatE(torch.nn.Module):
         ws, ws_bytes = self._workspace(all_h.numel())
         _native.call("rnnl_rotate_score", eemb.data_ptr(), etab.data_ptr(), rtab.data_ptr(),
                      self.emb_dim, float(self.gamma), all_h.data_ptr(), all_r.data_ptr(), all_h.numel(),
-                     self.num_entities, out.data_ptr(), 1 if accumulate else 0, int(self.mode), ws, ws_bytes,
+                     self.num_entities, out.data_ptr(), int(accumulate), int(self.mode), ws, ws_bytes,
                      torch.cuda.current_stream(self.eemb.device).cuda_stream)
         return out
 

@@ -573,6 +573,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # per-candidate outputs to the workspace; a short apply pass adds them
         # into the finished RotatE rows (rnnl_predictorplus_apply)
         self.overlap_deferred = os.environ.get("RNNL_OVERLAP_DEFERRED", "1") != "0"
+        # ... or, without the apply pass (default): the score rows are zeroed on
+        # side stream B beside the rule encoder, and RotatE and the deferred
+        # scoring pass both add into them atomically — fl(rotate + out) in either
+        # order, bit-identical (RNNL_OVERLAP_ATOMIC=0: the apply pass)
+        self.overlap_atomic = os.environ.get("RNNL_OVERLAP_ATOMIC", "1") != "0"
         # with several chunks, chunk k's deferred scoring on side stream B
         # beside chunk k + 1's grounding on A (RNNL_OVERLAP_PIPELINE=1)
         self.overlap_pipeline = os.environ.get("RNNL_OVERLAP_PIPELINE", "0") == "1"
@@ -757,15 +762,19 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         rec = (lambda k: events.setdefault(k, torch.cuda.Event(enable_timing=True)).record()) \
             if events is not None else (lambda k: None)
         rec("start")
+        score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
+        overlap = self.entity_feature == "RotatE" and self.overlap and nq >= max(2 * self.overlap_chunks,
+                                                                                  self.overlap_min_rows)
+        # atomic deferred overlap: zero the rows on side stream B beside the rule encoder
+        zero_ev = self._zero_rows(device, score) if overlap and self.overlap_deferred and self.overlap_atomic \
+            else None
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
-        score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        if self.entity_feature == "RotatE" and self.overlap and nq >= max(2 * self.overlap_chunks,
-                                                                           self.overlap_min_rows):
-            self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec)
+        if overlap:
+            self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec, zero_ev)
             del keep
             return (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device), n_cand) \
                 if return_ncand else (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device))
@@ -826,7 +835,22 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self._side[key] = (torch.cuda.Stream(device, priority=prio), torch.cuda.Stream(device, priority=prio))
         return self._side[key]
 
-    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec):
+    def _zero_rows(self, device, score):
+        """score.zero_() on side stream B (ordered after the current stream's
+        work so far); returns the event that marks it done."""
+        main = torch.cuda.current_stream(device)
+        side_s = self._side_streams(device)[1]
+        key = (self._device_index(device), "zev")
+        ev = self._side.get(key)
+        if ev is None:
+            ev = self._side[key] = torch.cuda.Event()
+        side_s.wait_stream(main)
+        with torch.cuda.stream(side_s):
+            score.zero_()
+        ev.record(side_s)
+        return ev
+
+    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec, zero_ev=None):
         """RotatE entity feature: the same kernels as the one-stream path, in
         row chunks over three streams — RotatE rows on the current stream,
         the grounding of every chunk on side stream A (it does not read the
@@ -841,7 +865,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         bounds = [nq * k // K for k in range(K + 1)]
         agg = params.aggregator
         deferred = self.overlap_deferred
+        atomic = deferred and zero_ev is not None  # RotatE and scoring add into zeroed rows: no apply pass
+        first = True
         while True:
+            if atomic and not first:  # a retried launch starts from zeroed rows again
+                score.zero_()
+                zero_ev.record(main)
+            first = False
             scale = self.capacity_scale
             wss = [self._chunk_workspace(device, k, bounds[k + 1] - bounds[k], scale) for k in range(K)]
             side_g.wait_stream(main)  # inputs, node aggregates, workspaces
@@ -859,23 +889,27 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                     # chunk k's scoring on side stream B, beside chunk k + 1's grounding
                     ev_g[k].record(side_g)
                     side_s.wait_event(ev_g[k])
-                if deferred:  # the score pass does not touch `score`: it runs beside RotatE too
+                if deferred:  # the score pass does not read `score`: it runs beside RotatE too
                     ss = side_s if pipeline else side_g
+                    if atomic:
+                        ss.wait_event(zero_ev)
                     _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
                                  all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None,
                                  n_cand[lo:].data_ptr(), digest[lo:].data_ptr() if digest is not None else None,
-                                 wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_score_wg, 1,
+                                 wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_score_wg, 2 if atomic else 1,
                                  ss.cuda_stream)
                     if pipeline:
                         ev_s[k].record(side_s)
                 if not pipeline:
                     ev_g[k].record(side_g)
+            if atomic:
+                main.wait_event(zero_ev)
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
-                self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=False)
+                self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=2 if atomic else 0)
                 ev_r[k].record(main)
             rec("ground")
-            for k in range(K if deferred else 0):
+            for k in range(K if deferred and not atomic else 0):
                 lo, hi = bounds[k], bounds[k + 1]
                 main.wait_event(ev_s[k] if pipeline else ev_g[k])
                 _native.call("rnnl_predictorplus_apply", wss[k].data_ptr(), hi - lo, scale, n_cand[lo:].data_ptr(),
