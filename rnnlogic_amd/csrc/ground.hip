@@ -2325,59 +2325,195 @@ __device__ __forceinline__ void pair_insert(const KParams &p, unsigned long long
 // early only when the next chunk's relation differs (the folded relation bias
 // is per wave) and at the end.  Same arithmetic per candidate as
 // score_sum_memo_kernel.
-template <bool DIGEST>
-__device__ __forceinline__ void sum_chunk_flush(const KParams &p, const float *s_w, const float *relb,
-                                                const int2 *queue, int m, float inv_scale, int r, int root) {
-  const int lane = threadIdx.x & 63;
-  if (lane < m) {
-    const int2 it = queue[lane];
-    const int4 cr = p.cand[it.y];
-    const float base = sum_base(p, it.x, cr.x);  // issued before the gather: its latency hides under it
-    float f[16];
-    long long deg;
-    uint64_t fp;
-    SumStage st{};
-    gather_sum<false, DIGEST>(p, st, 0, cr.y, cr.z, inv_scale, f, deg, fp);
-    if constexpr (DIGEST)
-      atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + it.x),
-                (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
-    asm volatile("" ::: "memory");  // keep the LDS weight reads inside (see score_sum_kernel)
-    const float out = mlp_sum(s_w, relb, f);
-    sum_write_out(p, it.x, it.y, cr.x, out, base);
-    if (!DIGEST && p.ptab && cr.z <= 3) {
-      const int2 z0 = make_int2(0, 0);
-      const unsigned long long key = pair_key(p, r, root, cr.z, p.bent[cr.y], cr.z >= 2 ? p.bent[cr.y + 1] : z0,
-                                              cr.z >= 3 ? p.bent[cr.y + 2] : z0);
-      if (key != PAIR_NOKEY) pair_insert(p, key, out);
-    }
-  }
-}
-
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// A candidate with more than BIG_ENTRIES bucket entries is gathered by the
+// whole wave (lane i takes entries i, i + 64, ...; a butterfly sums the 16
+// fp64 partials): its lane would otherwise walk the list alone, two dependent
+// loads per entry, while the wave waits — on a one-batch launch the scoring
+// time is the longest such walk.  The fp64 sums of exact count x record
+// products are exact in any order, so the feature is the per-lane walk's bit
+// for bit.  Up to BIG_SLOTS per round, their features staged in LDS.
+#ifndef RNNL_BIG_ENTRIES
+#define RNNL_BIG_ENTRIES 16
+#endif
+constexpr int BIG_ENTRIES = RNNL_BIG_ENTRIES;
+constexpr int BIG_SLOTS = 16;
+
+template <bool DIGEST>
+__device__ __forceinline__ void coop_gather(const KParams &p, int beg, int cnt, float inv_scale, float *fslot,
+                                            uint64_t &csum, long long &deg, uint64_t &fp) {
+  const int lane = threadIdx.x & 63;
+  double acc[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) acc[d] = 0.0;
+  csum = 0;
+  deg = 0;
+  fp = 0;
+  for (int e = beg + lane; e < beg + cnt; e += 64) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const uint32_t cu = (uint32_t)be.y;
+    csum += cu;
+    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const double cd = (double)cu;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) acc[d] = fma(cd, (double)x[d], acc[d]);
+    if constexpr (DIGEST) {
+      deg += (long long)cu * p.rl.node_nrules[n];
+      fp += (uint64_t)cu * p.rl.node_fp[n];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) acc[d] += __shfl_xor(acc[d], off, 64);
+    csum += __shfl_xor(csum, off, 64);
+    if constexpr (DIGEST) {
+      deg += __shfl_xor(deg, off, 64);
+      fp += __shfl_xor(fp, off, 64);
+    }
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d)
+    if (lane == d) v = (float)(acc[d] * (double)inv_scale);
+  if (lane < 16) fslot[lane] = v;
+}
+
+// COOP = false (large launches): each lane walks its own list — the
+// cooperative rounds' registers spill at the 64-VGPR cap, which costs the
+// throughput-bound launches more (RotatE step +0.8 ms) than the long walks.
+template <bool DIGEST, bool COOP>
+__device__ __forceinline__ void sum_chunk_flush(const KParams &p, const float *s_w, const float *relb,
+                                                const int2 *queue, int m, float inv_scale, int r, int root,
+                                                float *fbig) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (!COOP) {
+    if (lane < m) {
+      const int2 it = queue[lane];
+      const int4 cr = p.cand[it.y];
+      const float base = sum_base(p, it.x, cr.x);  // issued before the gather: its latency hides under it
+      float f[16];
+      long long deg;
+      uint64_t fp;
+      SumStage st{};
+      gather_sum<false, DIGEST>(p, st, 0, cr.y, cr.z, inv_scale, f, deg, fp);
+      if constexpr (DIGEST)
+        atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + it.x),
+                  (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
+      asm volatile("" ::: "memory");  // keep the LDS weight reads inside (see score_sum_kernel)
+      const float out = mlp_sum(s_w, relb, f);
+      sum_write_out(p, it.x, it.y, cr.x, out, base);
+      if (!DIGEST && p.ptab && cr.z <= 3) {
+        const int2 z0 = make_int2(0, 0);
+        const unsigned long long key = pair_key(p, r, root, cr.z, p.bent[cr.y], cr.z >= 2 ? p.bent[cr.y + 1] : z0,
+                                                cr.z >= 3 ? p.bent[cr.y + 2] : z0);
+        if (key != PAIR_NOKEY) pair_insert(p, key, out);
+      }
+    }
+    return;
+  }
+  int2 it = make_int2(0, 0);
+  int4 cr = make_int4(0, 0, 0, 0);
+  if (lane < m) {
+    it = queue[lane];
+    cr = p.cand[it.y];
+  }
+  bool todo = lane < m;
+#pragma unroll 1
+  while (true) {
+    // this round's long-list candidates, gathered by the whole wave
+    uint64_t big = __ballot(todo && cr.z > BIG_ENTRIES);
+    int slot = -1;  // >= 0: this lane's feature is in fbig[slot]; -2: walk it here (int64 range)
+    long long bdeg = 0;
+    uint64_t bfp = 0;
+#pragma unroll 1
+    for (int nb = 0; big && nb < BIG_SLOTS; ++nb) {
+      const int owner = __builtin_ctzll(big);
+      big &= big - 1;
+      const int beg = __builtin_amdgcn_readlane(cr.y, owner), cnt = __builtin_amdgcn_readlane(cr.z, owner);
+      uint64_t csum;
+      long long deg;
+      uint64_t fp;
+      coop_gather<DIGEST>(p, beg, cnt, inv_scale, fbig + nb * 16, csum, deg, fp);
+      if (lane == owner) {
+        slot = csum >= (1ull << 23) ? -2 : nb;  // past the exact fp64 range: the lane's int64 walk
+        bdeg = deg;
+        bfp = fp;
+      }
+    }
+    wave_lds_sync();
+    const bool go = todo && (cr.z <= BIG_ENTRIES || slot != -1);
+    if (go) {
+      const float base = sum_base(p, it.x, cr.x);  // issued before the gather: its latency hides under it
+      float f[16];
+      long long deg;
+      uint64_t fp;
+      if (slot >= 0) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) f[d] = fbig[slot * 16 + d];
+        deg = bdeg;
+        fp = bfp;
+      } else {
+        SumStage st{};
+        gather_sum<false, DIGEST>(p, st, 0, cr.y, cr.z, inv_scale, f, deg, fp);
+      }
+      if constexpr (DIGEST)
+        atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + it.x),
+                  (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
+      asm volatile("" ::: "memory");  // keep the LDS weight reads inside (see score_sum_kernel)
+      const float out = mlp_sum(s_w, relb, f);
+      sum_write_out(p, it.x, it.y, cr.x, out, base);
+      if (!DIGEST && p.ptab && cr.z <= 3) {
+        const int2 z0 = make_int2(0, 0);
+        const unsigned long long key = pair_key(p, r, root, cr.z, p.bent[cr.y], cr.z >= 2 ? p.bent[cr.y + 1] : z0,
+                                                cr.z >= 3 ? p.bent[cr.y + 2] : z0);
+        if (key != PAIR_NOKEY) pair_insert(p, key, out);
+      }
+      todo = false;
+    }
+    wave_lds_sync();  // fbig is reused by the next round
+    if (__ballot(todo) == 0ull) break;
+  }
+}
+
+
 #ifndef RNNL_SUM_CK
 #define RNNL_SUM_CK 8
 #endif
 constexpr int SUM_CK = RNNL_SUM_CK;  // chunks per dequeue
 
-template <bool DIGEST>
+#ifndef RNNL_SCORE_PROF
+#define RNNL_SCORE_PROF 0  // 1: phase clocks in score_sum_chunk_kernel (tools/score_phases.py)
+#endif
+constexpr bool kScoreProf = RNNL_SCORE_PROF;
+
+template <bool DIGEST, bool COOP>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_WAVES, 8))) void score_sum_chunk_kernel(
     KParams p, const float *__restrict__ W) {
   using L = WL<RNNL_AGG_SUM>;
   __shared__ __attribute__((aligned(16))) float s_w[L::N];
   __shared__ float s_relb[BS / 64][128];
   __shared__ int2 s_queue[BS / 64][128];
+  __shared__ float s_fbig[BS / 64][COOP ? BIG_SLOTS * 16 : 1];  // long-list candidates' features (COOP flush)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  // diagnostic phase clocks (-DRNNL_SCORE_PROF=1 builds, rnnl_debug_profile; prof[16..24]): per wave,
+  // setup / classify / flush / total cycles, the chunks taken and the max total
+  const unsigned long long t_start = kScoreProf && p.prof ? __builtin_amdgcn_s_memtime() : 0ull;
+  const unsigned long long rt_start = kScoreProf && p.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  unsigned long long t_cls = 0, t_fl = 0, n_ck = 0, t_ready = 0;
   load_sum_weights(s_w, W);
   check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum));
   const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
   const float inv_scale = ldexpf(1.f, -shift);
   __syncthreads();  // the only workgroup barrier: waves run independently from here
+  if (kScoreProf && p.prof) t_ready = __builtin_amdgcn_s_memtime();
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
   float *relb = s_relb[wv];
   int2 *queue = s_queue[wv];
@@ -2405,13 +2541,19 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
       const int m = drain ? min(n, 64) : (n >= 64 ? 64 : 0);
       if (m == 0) break;
       wave_lds_sync();
-      sum_chunk_flush<DIGEST>(p, s_w, relb, queue, m, inv_scale, cur_r, cur_root);
+      const unsigned long long tf = kScoreProf && p.prof ? __builtin_amdgcn_s_memtime() : 0ull;
+      sum_chunk_flush<DIGEST, COOP>(p, s_w, relb, queue, m, inv_scale, cur_r, cur_root, s_fbig[wv]);
+      if (kScoreProf && p.prof) {
+        __builtin_amdgcn_s_waitcnt(0);
+        t_fl += __builtin_amdgcn_s_memtime() - tf;
+      }
       n -= m;
       const int2 v = lane < n ? queue[m + lane] : make_int2(0, 0);
       wave_lds_sync();
       if (lane < n) queue[lane] = v;
     }
     if (done) break;
+    const unsigned long long tc = kScoreProf && p.prof ? __builtin_amdgcn_s_memtime() : 0ull;
     if (r != cur_r) {
       wave_lds_sync();  // every lane is done with the previous relation's bias
 #pragma unroll
@@ -2434,7 +2576,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
       unsigned long long key = PAIR_NOKEY;
       if (cr.z == 1) {
         const int2 be = p.bent[cr.y];
-        if (be.y == 1) {  // one path of one leaf node: the memo
+        if (be.y == 1 && p.memo) {  // one path of one leaf node: the memo
           queued = false;
           const float base = sum_base(p, q, cr.x);
           if constexpr (DIGEST)
@@ -2462,6 +2604,23 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_SCORE_W
     if (queued) queue[pos] = make_int2(q, (int)(qb + s));
     n += (int)__popcll(bal);  // < 128: the queue held < 64 before this chunk
     ++c;
+    if (kScoreProf && p.prof) {
+      __builtin_amdgcn_s_waitcnt(0);
+      t_cls += __builtin_amdgcn_s_memtime() - tc;
+      ++n_ck;
+    }
+  }
+  if (kScoreProf && p.prof && lane == 0 && n_ck) {  // waves that took a chunk
+    const unsigned long long tot = __builtin_amdgcn_s_memtime() - t_start;
+    atomicAdd(&p.prof[16], t_ready - t_start);
+    atomicAdd(&p.prof[17], t_cls);
+    atomicAdd(&p.prof[18], t_fl);
+    atomicAdd(&p.prof[19], tot);
+    atomicAdd(&p.prof[20], n_ck);
+    atomicAdd(&p.prof[21], n_ck ? 1ull : 0ull);
+    atomicMax(&p.prof[22], tot);
+    atomicMax(&p.prof[23], t_fl);
+    atomicAdd(&p.prof[24], __builtin_amdgcn_s_memrealtime() - rt_start);
   }
 }
 
@@ -2486,7 +2645,7 @@ __global__ __launch_bounds__(BS) void apply_kernel(KParams p) {
 // Packs the MLP weights behind the workspace header (layout W_* above).
 __global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
   const int kin = p.agg == RNNL_AGG_SUM ? 16 : 192;
-  for (int i = threadIdx.x; i < W_FLOATS; i += blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < W_FLOATS; i += gridDim.x * blockDim.x) {
     float v = 0.f;
     if (i < W_ADDB) {
       if (i < 16 * kin) v = p.add_w[i];
@@ -2996,7 +3155,7 @@ static void launch_score(const KParams &p0, rnnl_rules r, hipStream_t st, int gr
   KParams p = p0;
   const int nq = p.nq;
   float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
-  hipLaunchKernelGGL(pack_weights_kernel, dim3(1), dim3(256), 0, st, p, W);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3((W_FLOATS + 255) / 256), dim3(256), 0, st, p, W);
   if (p.agg == RNNL_AGG_SUM) {
     // staged path while the largest head's leaves fit the LDS budget
     const int64_t base_lds = (int64_t)(WL<RNNL_AGG_SUM>::N + 128) * 4;
@@ -3008,7 +3167,15 @@ static void launch_score(const KParams &p0, rnnl_rules r, hipStream_t st, int gr
 #endif
     const bool staged = base_lds + stage <= RNNL_STAGE_LIMIT;
     if (!staged && score_memo_enabled() && p.memo) {
-      hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, (const float *)W);
+      // few rows (e.g. one reference batch per call) with the pair memo on: no memo
+      // pass (one workgroup per relation, on the call's critical path); the
+      // single-path candidates take pair-memo keys instead — the same outputs
+      const bool small = sum_chunked() && !p.digest && pair_memo_enabled() && p.pbc >= 2 && nq <= MEMO_SCAN_ROWS;
+      if (small)
+        p.memo = nullptr;
+      else
+        hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p,
+                           (const float *)W);
       if (sum_chunked()) {
         launch_chunk_list(p, st);
         if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);
@@ -3019,10 +3186,17 @@ static void launch_score(const KParams &p0, rnnl_rules r, hipStream_t st, int gr
           (void)hipMemsetAsync(p.ptab, 0, 8ull << p.psbits, st);
         }
         const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * RNNL_SCORE_WG_PER_CU);
-        if (p.digest)
-          hipLaunchKernelGGL((score_sum_chunk_kernel<true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+        // one reference batch per call: the wave-cooperative walk of long entry lists
+        // (bit-identical features); large launches keep the per-lane walk
+        const bool coop = nq <= MEMO_SCAN_ROWS;
+        if (p.digest && coop)
+          hipLaunchKernelGGL((score_sum_chunk_kernel<true, true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+        else if (p.digest)
+          hipLaunchKernelGGL((score_sum_chunk_kernel<true, false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+        else if (coop)
+          hipLaunchKernelGGL((score_sum_chunk_kernel<false, true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
         else
-          hipLaunchKernelGGL((score_sum_chunk_kernel<false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+          hipLaunchKernelGGL((score_sum_chunk_kernel<false, false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
         return;
       }
       if (p.digest)

@@ -774,10 +774,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
         if overlap:
-            self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec, zero_ev)
+            mask = self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec,
+                                         zero_ev)
             del keep
-            return (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device), n_cand) \
-                if return_ncand else (score, torch.ones((nq, self.num_entities), dtype=torch.bool, device=device))
+            return (score, mask, n_cand) if return_ncand else (score, mask)
         while True:
             mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
             scale = self.capacity_scale
@@ -857,7 +857,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         base score, and it is latency-bound where RotatE is VALU-bound), and
         each chunk's scoring pass on side stream B once both its grounding and
         its RotatE rows are done.  Results are bit-identical to the
-        one-stream path (same kernels, same inputs per row)."""
+        one-stream path (same kernels, same inputs per row).  Returns the
+        (all-True) mask, filled on the current stream behind RotatE."""
         main = torch.cuda.current_stream(device)
         side_g, side_s = self._side_streams(device)
         nq = all_h.numel()
@@ -908,6 +909,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 lo, hi = bounds[k], bounds[k + 1]
                 self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=2 if atomic else 0)
                 ev_r[k].record(main)
+            # the all-True mask (RotatE feature) is filled behind RotatE, beside the side streams' work
+            mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
             rec("ground")
             for k in range(K if deferred and not atomic else 0):
                 lo, hi = bounds[k], bounds[k + 1]
@@ -937,7 +940,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 continue
             for rc in bad:
                 _native.check(rc)
-            break
+            return mask
 
     # ------------------------------------------------------------------ autograd (training) path
     def forward_autograd(self, all_h, all_r, edges_to_remove, query_r=None):

@@ -2,7 +2,7 @@
 once per TestDataset batch (B <= 32, one relation) over the FB15k-237 test
 split, the bench model (lstm/sum + RotatE D = 1000) — diagnostic timing of the
 per-call cost beside bench.py's one-launch forward_rows.
-Usage (GPU box): python tools/per_batch_forward.py [N_BATCHES]"""
+Usage (GPU box): python tools/per_batch_forward.py [N_BATCHES [FEATURE]]"""
 import contextlib
 import os
 import sys
@@ -15,9 +15,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+FEATURE = sys.argv[2] if len(sys.argv) > 2 else "RotatE"  # or "bias"
 dev = torch.device("cuda:0")
 with contextlib.redirect_stdout(sys.stderr):
-    graph, test_set, model, rows = bench.build_workload("RotatE")
+    graph, test_set, model, rows = bench.build_workload(FEATURE)
 model = model.to(dev).eval()
 batches = test_set.batches[:N] if N else test_set.batches
 hs = [torch.tensor([x[0] for x in b], device=dev) for b in batches]
