@@ -186,6 +186,12 @@ int rnnl_forward_status(void *workspace, void *stream);
  * (trie node, path count) entries of the COO), so a caller sizing the COO
  * export needs no further synchronisation.  Valid when RNNL_OK. */
 int rnnl_forward_status_totals(void *workspace, void *stream, int64_t *totals);
+/* The same status from a host copy of the workspace's first
+ * rnnl_forward_header_bytes bytes (copied by the caller on its stream, e.g.
+ * asynchronously into pinned memory): no synchronisation here.  totals as
+ * for rnnl_forward_status_totals (nullable). */
+int rnnl_forward_header_bytes(size_t *bytes);
+int rnnl_forward_status_host(const void *header, int64_t *totals);
 /* Grounding only (reference data.py:136-173 for every rule of every row,
  * predictors.py:221-244): fills the workspace's COO of the stacked rule_count
  * matrix and n_cand (per row candidate count, -1/-2 on overflow/error; check
@@ -260,6 +266,19 @@ int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32
                            const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries, float *score,
                            uint8_t *mask, int32_t *n_cand, void *workspace, size_t workspace_bytes,
                            int32_t capacity_scale, void *stream);
+/* rnnl_predictor_forward in two halves (training lookahead: the grounding of
+ * the next batches, which does not depend on the weights, runs on a second
+ * stream while the current batch scores and steps): rnnl_predictor_ground
+ * fills the workspace (grounding + the scoring chunk list) and n_cand;
+ * rnnl_predictor_score then scores from it (same rows, n_queries,
+ * capacity_scale; score pre-filled as for rnnl_predictor_forward).  The
+ * overflow status is the workspace's, read after the score half. */
+int rnnl_predictor_ground(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t *all_r,
+                          const int64_t *edges_to_remove, int32_t n_queries, int32_t *n_cand, void *workspace,
+                          size_t workspace_bytes, int32_t capacity_scale, void *stream);
+int rnnl_predictor_score(rnnl_graph g, rnnl_rules r, const void *node_w, int32_t feature, const int64_t *all_h,
+                         const int64_t *all_r, int32_t n_queries, float *score, uint8_t *mask, int32_t *n_cand,
+                         void *workspace, size_t workspace_bytes, int32_t capacity_scale, void *stream);
 int rnnl_predictor_rule_stats(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
                               rnnl_rules r, const int64_t *all_r, const int64_t *all_t, int32_t ld, int64_t *pos,
                               int64_t *tot, void *stream);

@@ -49,6 +49,8 @@ SIGNATURES = [
     ("rnnl_predictorplus_apply", ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _I32, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
+    ("rnnl_forward_header_bytes", ctypes.c_int, [_P]),
+    ("rnnl_forward_status_host", ctypes.c_int, [_P, _P]),
     ("rnnl_ground", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_ground_export_candidates", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_ground_export_entries", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
@@ -56,6 +58,9 @@ SIGNATURES = [
     ("rnnl_linear_node_weights", ctypes.c_int, [_P, _P, _I32, _P, _P]),
     ("rnnl_predictor_forward", ctypes.c_int,
      [_P, _P, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
+    ("rnnl_predictor_ground", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _P]),
+    ("rnnl_predictor_score", ctypes.c_int,
+     [_P, _P, _P, _I32, _P, _P, _I32, _P, _P, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_predictor_rule_stats", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     ("rnnl_predictor_backward", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _I32, _P, _I32, _P, _P]),
     ("rnnl_debug_profile", ctypes.c_int, [_P]),

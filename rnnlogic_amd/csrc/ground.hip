@@ -3425,6 +3425,42 @@ int rnnl_predictor_forward(rnnl_graph g, rnnl_rules r, const void *node_w, int32
   return RNNL_OK;
 }
 
+int rnnl_predictor_ground(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t *all_r, const int64_t *etr,
+                          int32_t nq, int32_t *n_cand, void *ws, size_t ws_bytes, int32_t scale, void *stream) {
+  KParams p;
+  if (int rc = setup_params("rnnl_predictor_ground", g, r, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale, p))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
+  if (nq == 0) return RNNL_OK;
+  p.agg = RNNL_AGG_SUM;
+  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
+  launch_chunk_list(p, st);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_predictor_score(rnnl_graph g, rnnl_rules r, const void *node_w, int32_t feature, const int64_t *all_h,
+                         const int64_t *all_r, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand, void *ws,
+                         size_t ws_bytes, int32_t scale, void *stream) {
+  if (!node_w || !score || (feature != RNNL_FEATURE_ADD && feature != RNNL_FEATURE_NONE)) {
+    set_error("rnnl_predictor_score: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p;
+  if (int rc = setup_params("rnnl_predictor_score", g, r, all_h, all_r, nullptr, nq, n_cand, ws, ws_bytes, scale, p))
+    return rc;
+  if (nq == 0) return RNNL_OK;
+  p.agg = RNNL_AGG_SUM;
+  p.feature = feature;
+  p.score = score;
+  p.mask = mask;
+  hipLaunchKernelGGL(score_linear_kernel, dim3((unsigned)std::min<int64_t>(nq, (int64_t)NUM_CU * 8)), dim3(BS), 0,
+                     (hipStream_t)stream, p, static_cast<const int *>(node_w));
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
 int rnnl_predictor_rule_stats(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand, rnnl_rules r,
                               const int64_t *all_r, const int64_t *all_t, int32_t ld, int64_t *pos, int64_t *tot,
                               void *stream) {
@@ -3494,10 +3530,18 @@ int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t poo
   return RNNL_OK;
 }
 
+constexpr int STATUS_WORDS = 18;  // header words 0..17: status, ..., H_NCAND, the pool counter (byte 64)
+
+static int status_from_header(const unsigned int *st, int64_t *totals);
+
 static int forward_status(void *ws, void *stream, int64_t *totals) {
-  unsigned int st[18] = {0};  // header words 0..17: status, ..., H_NCAND, the pool counter (byte 64)
+  unsigned int st[STATUS_WORDS] = {0};
   RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
   RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  return status_from_header(st, totals);
+}
+
+static int status_from_header(const unsigned int *st, int64_t *totals) {
   if (totals) {
     unsigned long long c, e;
     memcpy(&c, st + H_NCAND, 8);
@@ -3528,6 +3572,25 @@ static int forward_status(void *ws, void *stream, int64_t *totals) {
 }
 
 int rnnl_forward_status(void *ws, void *stream) { return forward_status(ws, stream, nullptr); }
+
+int rnnl_forward_header_bytes(size_t *bytes) {
+  if (!bytes) {
+    set_error("rnnl_forward_header_bytes: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = sizeof(unsigned int) * STATUS_WORDS;
+  return RNNL_OK;
+}
+
+int rnnl_forward_status_host(const void *header, int64_t *totals) {
+  if (!header) {
+    set_error("rnnl_forward_status_host: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  unsigned int st[STATUS_WORDS];
+  memcpy(st, header, sizeof(st));
+  return status_from_header(st, totals);
+}
 
 int rnnl_forward_status_totals(void *ws, void *stream, int64_t *totals) {
   if (!ws || !totals) {

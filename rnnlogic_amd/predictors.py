@@ -18,6 +18,7 @@ the exported grounding COO.
 
 There is no CPU fallback: on a CPU tensor forward() raises.
 """
+import collections
 import ctypes
 import os
 import logging
@@ -138,9 +139,14 @@ class _HipGrounding(object):
                              self.capacity_scale)
                 continue
             _native.check(rc)
-            # launch generation: a saved workspace is stale once this moves on
-            self._ws_gen[device] = self._ws_gen.get(device, 0) + 1
+            self._ws_touch(ws)
             return ws, scale
+
+    def _ws_touch(self, ws):
+        """Count a launch onto workspace `ws`: a grounding saved for a backward
+        is stale once its workspace's count moves on."""
+        self._ws_uses[ws.data_ptr()] = self._ws_uses.get(ws.data_ptr(), 0) + 1
+        return self._ws_uses[ws.data_ptr()]
 
     def ground(self, all_h, all_r, edges_to_remove=None, totals=None):
         """Grounding of every rule of every row into the workspace (HIP
@@ -216,7 +222,7 @@ class _PredictorLinear(torch.autograd.Function):
         # get no gradient (None, which Adam skips — a zero gradient would still
         # move them through the moment estimates)
         ctx.no_cand = n_total == 0
-        ctx.gen = model._ws_gen.get(device)
+        ctx.gen = model._ws_uses.get(ws.data_ptr()) if ws is not None else None
         ctx.rows = model._rows(all_h, all_r, edges_to_remove)[1:]
         ctx.has_bias = bias is not None
         ctx.mark_non_differentiable(mask)
@@ -231,7 +237,7 @@ class _PredictorLinear(torch.autograd.Function):
         gw = gb = None
         if nq and ctx.needs_input_grad[0] and not ctx.no_cand:
             ws, scale, n_cand = ctx.ws, ctx.scale, ctx.n_cand
-            if model._ws_gen.get(device) != ctx.gen:  # the workspace was reused: ground again
+            if model._ws_uses.get(ws.data_ptr()) != ctx.gen:  # the workspace was reused: ground again
                 ws, scale, n_cand = model.ground(all_h, all_r, etr)
             nr = model.native_rules(device)
             _, ld = model.head_roots(device)
@@ -267,7 +273,11 @@ class Predictor(_HipGrounding, torch.nn.Module):
         self._ws = {}
         self._lin_cache = {}
         self._roots = {}
-        self._ws_gen = {}  # per device: launches on the workspace so far
+        self._ws_uses = {}  # per workspace pointer: launches onto it so far
+        self._pf = {}  # per device: training lookahead (prefetch): side stream, workspace ring, queue
+        # groundings launched ahead of the training step that needs them
+        # (TrainerPredictor.train; RNNL_PREFETCH=0 turns the lookahead off)
+        self.prefetch_depth = int(os.environ.get("RNNL_PREFETCH", "2"))
         self.capacity_scale = 1
 
     def set_rules(self, input):
@@ -317,6 +327,89 @@ class Predictor(_HipGrounding, torch.nn.Module):
         score, mask, n_cand, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
+    def prefetch(self, all_h, all_r, edges_to_remove=None):
+        """Ground these rows now, on a side stream, for a forward that will be
+        called with the same tensor objects (the training loop's lookahead:
+        the grounding does not depend on the weights, so batch k + 1's runs
+        while batch k scores, steps back and updates).  Up to prefetch_depth
+        groundings are queued, each in its own workspace of a ring; a forward
+        whose rows are not the queue's head drops the queue."""
+        if self.prefetch_depth <= 0:
+            return
+        device, h, r, etr = self._rows(all_h, all_r, edges_to_remove)
+        nq = h.numel()
+        if nq == 0:
+            return
+        key = self._device_index(device)
+        pf = self._pf.get(key)
+        if pf is None:
+            pf = self._pf[key] = {"stream": torch.cuda.Stream(device), "ring": {}, "next": 0,
+                                  "queue": collections.deque()}
+        if len(pf["queue"]) >= self.prefetch_depth:
+            return
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        scale = self.capacity_scale
+        need = ctypes.c_size_t()
+        _native.call("rnnl_forward_workspace_size", g, nr.ptr, nq, scale, ctypes.byref(need))
+        # ring of depth + 1 workspaces: the forward in flight keeps one until its backward
+        slot = pf["next"] % (self.prefetch_depth + 1)
+        pf["next"] += 1
+        ws = pf["ring"].get(slot)
+        if ws is None or ws.numel() < need.value:
+            ws = pf["ring"][slot] = torch.empty(need.value, dtype=torch.uint8, device=device)
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        side, main = pf["stream"], torch.cuda.current_stream(device)
+        # inputs, and the slot's previous user (its backward is on the current stream already)
+        side.wait_stream(main)
+        _native.call("rnnl_predictor_ground", g, nr.ptr, h.data_ptr(), r.data_ptr(),
+                     etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(), ws.numel(),
+                     scale, side.cuda_stream)
+        # the grounding's status / totals and the one-relation check, copied to the
+        # host behind it: the forward reads them without waiting for the current stream
+        hb = self._header_bytes()
+        hdr = torch.empty(hb + 1, dtype=torch.uint8, pin_memory=True)
+        with torch.cuda.stream(side):
+            hdr[:hb].copy_(ws[:hb], non_blocking=True)
+            hdr[hb:].copy_((r != r[0]).any().view(1).to(torch.uint8), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        # the side stream's use of these blocks outlives a dropped queue entry or a
+        # grown ring slot: the caching allocator must not hand them out before it ends
+        for t in (ws, n_cand, h, r) + ((etr,) if etr is not None else ()):
+            t.record_stream(side)
+        self._ws_touch(ws)
+        pf["queue"].append((all_h, all_r, edges_to_remove, ws, scale, n_cand, ev, (h, r, etr), hdr))
+
+    def _header_bytes(self):
+        if getattr(self, "_hdr_bytes", None) is None:
+            n = ctypes.c_size_t()
+            _native.call("rnnl_forward_header_bytes", ctypes.byref(n))
+            self._hdr_bytes = n.value
+        return self._hdr_bytes
+
+    def check_deferred(self):
+        """Raise the scoring pass's own error (an integer range flag) of the
+        last lookahead forward, whose status is read one step late so the
+        host does not wait for the scoring each step."""
+        d = getattr(self, "_deferred_status", None)
+        if d is None:
+            return
+        self._deferred_status = None
+        d[1].synchronize()
+        _native.check(_native.lib().rnnl_forward_status_host(d[0].data_ptr(), None))
+
+    def _prefetched(self, device, all_h, all_r, edges_to_remove):
+        """The queued grounding of exactly these row tensors, or None (a
+        mismatch drops the lookahead queue)."""
+        pf = self._pf.get(self._device_index(device))
+        if not pf or not pf["queue"]:
+            return None
+        e = pf["queue"][0]
+        if e[0] is all_h and e[1] is all_r and e[2] is edges_to_remove and e[4] == self.capacity_scale:
+            return pf["queue"].popleft()
+        pf["queue"].clear()
+        return None
+
     def _forward_launch(self, all_h, all_r, edges_to_remove, single_relation=False):
         """rnnl_predictor_forward over the rows -> (score, mask, n_cand, ws,
         scale, candidate total); the workspace keeps the grounding for a
@@ -324,14 +417,17 @@ class Predictor(_HipGrounding, torch.nn.Module):
         `single_relation` the reference's one-relation-per-batch check
         (predictors.py:54-55) is read back with the launch status (no extra
         host sync)."""
+        raw = (all_h, all_r, edges_to_remove)
         device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
         nq, E = all_h.numel(), self.num_entities
         if nq == 0:  # no rows: empty outputs, no launch
             return (torch.empty((0, E), dtype=torch.float32, device=device),
                     torch.empty((0, E), dtype=torch.bool, device=device),
                     torch.empty(0, dtype=torch.int32, device=device), None, None, 0)
+        self.check_deferred()
+        pre = self._prefetched(device, *raw)
         mixed = None
-        if single_relation:
+        if single_relation and pre is None:
             mixed = torch.empty((), dtype=torch.bool, pin_memory=True)
             mixed.copy_((all_r != all_r[0]).any(), non_blocking=True)
         g, nr = self.graph.device_graph(device), self.native_rules(device)
@@ -344,18 +440,45 @@ class Predictor(_HipGrounding, torch.nn.Module):
         mask8 = None if bias_mode else torch.empty((nq, E), dtype=torch.uint8, device=device)
         bias = self.bias.detach().float().contiguous() if bias_mode else None
 
-        def run(ws, scale):
+        def fill():
             if bias_mode:
                 _native.call("rnnl_fill_rows", bias.data_ptr(), nq, E, score.data_ptr(), stream)
             else:
                 _native.call("rnnl_fill_value", float("-inf"), score.numel(), score.data_ptr(), stream)
                 mask8.zero_()
+
+        def run(ws, scale):
+            fill()
             _native.call("rnnl_predictor_forward", g, nr.ptr, node_w.data_ptr(), feature, all_h.data_ptr(),
                          all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
                          mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(), ws.data_ptr(),
                          ws.numel(), scale, stream)
         totals = np.zeros(2, dtype=np.int64)  # (candidates, bucket entries), read with the status
-        ws, scale = self._launch(device, nq, run, totals)
+        if pre is not None:  # grounded ahead (prefetch): the scoring half only
+            _, _, _, ws, scale, n_cand_pf, ev, _, hdr = pre
+            ev.synchronize()  # that grounding and its header copy, not the later side-stream work
+            hb = self._header_bytes()
+            rc = _native.lib().rnnl_forward_status_host(hdr.data_ptr(), totals.ctypes.data_as(ctypes.c_void_p))
+            if single_relation:
+                assert not bool(hdr[hb]), "a batch must hold one relation (predictors.py:54-55)"
+            if rc == _native.RNNL_OK:
+                fill()
+                main = torch.cuda.current_stream(device)
+                main.wait_event(ev)
+                _native.call("rnnl_predictor_score", g, nr.ptr, node_w.data_ptr(), feature, all_h.data_ptr(),
+                             all_r.data_ptr(), nq, score.data_ptr(), mask8.data_ptr() if mask8 is not None else None,
+                             n_cand_pf.data_ptr(), ws.data_ptr(), ws.numel(), scale, stream)
+                # the scoring pass's range flag: copied behind it, read at the next forward
+                dh = torch.empty(hb, dtype=torch.uint8, pin_memory=True)
+                dh.copy_(ws[:hb], non_blocking=True)
+                dev_ev = torch.cuda.Event()
+                dev_ev.record(main)
+                self._deferred_status = (dh, dev_ev)
+                n_cand = n_cand_pf
+            else:  # overflow (or another failure): the one-call path, with its retry
+                pre = None
+        if pre is None:
+            ws, scale = self._launch(device, nq, run, totals)
         if mixed is not None:
             assert not bool(mixed), "a batch must hold one relation (predictors.py:54-55)"
         mask = torch.ones((nq, E), dtype=torch.bool, device=device) if bias_mode else mask8.bool()
@@ -550,7 +673,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._ws = {}
         self._ws_chunks = {}
         self._side = {}
-        self._ws_gen = {}
+        self._ws_uses = {}
         self.capacity_scale = 1
         # RotatE base score: the grounding runs on a side stream beside the
         # RotatE kernel; rows may be split into chunks so that each chunk's

@@ -12,6 +12,7 @@ the padded count — with two differences in *how*, not *what*:
   * training forwards run PredictorPlus's differentiable path (HIP grounding,
     autograd on the exported path-count COO).
 """
+import collections
 import logging
 import os
 from itertools import islice
@@ -41,6 +42,10 @@ class _SizedIter(object):
     def __iter__(self):
         torch.empty((), dtype=torch.int64).random_()
         return (self.fn(i) for i in self.sampler)
+
+
+class _Prepared(tuple):
+    """A training batch already squeezed and on the device (TrainerPredictor._prepare)."""
 
 
 class TrainerPredictor(object):
@@ -118,7 +123,7 @@ class TrainerPredictor(object):
         total_loss = torch.zeros((), dtype=torch.float64, device=self.device)
         total_size = 0.0
         sampler.set_epoch(0)
-        for batch_id, batch in enumerate(islice(dataloader, batch_per_epoch)):
+        for batch_id, batch in enumerate(self._lookahead(model, islice(dataloader, batch_per_epoch))):
             loss, size = self.train_step(model, batch, smoothing, sync=False)
             if loss is not None:
                 total_loss += loss.detach().double()
@@ -129,8 +134,47 @@ class TrainerPredictor(object):
                                                              total_loss.item() / print_every, total_size / print_every))
                 total_loss.zero_()
                 total_size = 0.0
+        check = getattr(getattr(model, "module", model), "check_deferred", None)
+        if check is not None:  # the last lookahead step's scoring status
+            check()
         if self.scheduler:
             self.scheduler.step()
+
+    def _prepare(self, batch):
+        """A loader batch as the tensors train_step uses (squeezed, on the
+        device)."""
+        out = [x.squeeze(0) for x in batch]
+        if self.device.type == "cuda":
+            out = [x.cuda(device=self.device) for x in out]
+        return _Prepared(out)
+
+    def _lookahead(self, model, batches):
+        """The batches, prepared; where the model grounds ahead (Predictor.
+        prefetch, on a GPU) the grounding of the next prefetch_depth batches
+        is launched before the current batch's step, so it runs on a side
+        stream while the step scores, steps back and updates (the grounding
+        does not depend on the weights: same COO, same results)."""
+        inner = getattr(model, "module", model)
+        depth = getattr(inner, "prefetch_depth", 0) if self.device.type == "cuda" else 0
+        if depth <= 0 or not hasattr(inner, "prefetch"):
+            for b in batches:
+                yield self._prepare(b)
+            return
+        pending = collections.deque()
+
+        def pull():
+            b = next(batches, None)
+            if b is not None:
+                b = self._prepare(b)
+                inner.prefetch(b[0], b[1], b[4])
+                pending.append(b)
+        batches = iter(batches)
+        for _ in range(depth):
+            pull()
+        while pending:
+            b = pending.popleft()
+            yield b
+            pull()  # after the step: its inputs are queued, and the ring slot it frees is the oldest
 
     def train_step(self, model, batch, smoothing, sync=True):
         """One optimizer step on one batch (trainer.py:72-98); returns
@@ -143,14 +187,8 @@ class TrainerPredictor(object):
         flattened rows — the same elements in the same order as the
         reference's boolean gather `logits[mask]`, without the gather's
         host sync."""
-        all_h, all_r, all_t, target, edges_to_remove = [x.squeeze(0) for x in batch]
-        E = self.train_set.graph.entity_size
-        if self.device.type == "cuda":
-            all_h = all_h.cuda(device=self.device)
-            all_r = all_r.cuda(device=self.device)
-            all_t = all_t.cuda(device=self.device)
-            target = target.cuda(device=self.device)
-            edges_to_remove = edges_to_remove.cuda(device=self.device)
+        all_h, all_r, all_t, target, edges_to_remove = batch if isinstance(batch, _Prepared) else \
+            self._prepare(batch)
         # one_hot(all_t, E) as a scatter (the same 0 / 1 values; one_hot checks
         # its index range with a host read)
         target_t = torch.zeros_like(target).scatter_(1, all_t.view(-1, 1), 1.0)

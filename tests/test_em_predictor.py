@@ -274,3 +274,71 @@ def test_predictor_batch_without_candidates_gives_no_rule_gradient():
         (torch.softmax(score, 1)[:, 0].sum()).backward()
         assert (model.rule_weights.grad is not None) == want_grad
         assert model.bias.grad is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overflow", [False, True])
+def test_predictor_train_lookahead_is_bit_identical(overflow):
+    """TrainerPredictor.train grounds the next batches ahead on a side stream
+    (Predictor.prefetch, rnnl_predictor_ground / rnnl_predictor_score): the
+    trained weights and the logged losses equal those of the one-call forward
+    (prefetch_depth 0) bit for bit — also when lowered workspace capacities
+    make prefetched groundings overflow and fall back to the retried path."""
+    import io
+    import logging
+    import random
+
+    from rnnlogic_amd import _native, datasets
+    from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset
+    from rnnlogic_amd.predictors import Predictor
+    from rnnlogic_amd.trainer import TrainerPredictor
+    from rnnlogic_amd.utils import set_seed
+    dev = torch.device("cuda:0")
+    set_seed(1)
+    graph = KnowledgeGraph(datasets.materialize("FB15k-237"))
+    train_set, valid_set, test_set = TrainDataset(graph, 32), ValidDataset(graph, 32), TestDataset(graph, 32)
+    rules = [[int(x) for x in line.split()] for line in open(datasets.rule_file("FB15k-237"))][::4]
+    model = Predictor(graph, entity_feature="bias")
+    model.set_rules(rules)
+    torch.manual_seed(3)
+    with torch.no_grad():
+        model.rule_weights.normal_(std=0.1)
+    init = {k: v.clone() for k, v in model.state_dict().items()}
+    rng = (random.getstate(), np.random.get_state(), torch.get_rng_state())
+    r2i = [list(x) for x in train_set.r2instances]  # make_batches shuffles these lists in place
+    runs = []
+    for depth in (0, 2):
+        model.load_state_dict(init)
+        train_set.r2instances = [list(x) for x in r2i]
+        random.setstate(rng[0])
+        np.random.set_state(rng[1])
+        torch.set_rng_state(rng[2])
+        model.prefetch_depth = depth
+        model.capacity_scale = 1
+        optim = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0)
+        solver = TrainerPredictor(model, train_set, valid_set, test_set, optim, gpus=[dev])
+        stream = io.StringIO()
+        h = logging.StreamHandler(stream)
+        root = logging.getLogger()
+        old = root.level
+        root.addHandler(h)
+        root.setLevel(logging.INFO)
+        if overflow:
+            _native.call("rnnl_debug_capacity", 8192, 8192, 1024)  # 1/8 of the defaults
+        try:
+            solver.train(batch_per_epoch=60, smoothing=0.2, print_every=20)
+            torch.cuda.synchronize()
+        finally:
+            _native.call("rnnl_debug_capacity", 0, 0, 0)
+            root.removeHandler(h)
+            root.setLevel(old)
+        losses = [line for line in stream.getvalue().splitlines() if line[:1].isdigit()]
+        runs.append(({k: v.detach().cpu().clone() for k, v in solver.model.state_dict().items()}, losses,
+                     model.capacity_scale))
+        model = solver.model
+    (w0, l0, s0), (w1, l1, s1) = runs
+    assert len(l0) == 3 and l0 == l1
+    if overflow:
+        assert s0 > 1 and s1 > 1, (s0, s1)
+    for k in w0:
+        assert torch.equal(w0[k], w1[k]), k
