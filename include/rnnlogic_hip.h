@@ -326,6 +326,16 @@ int rnnl_rotate_score(const float *eemb, const void *entity_table, const float *
                       float gamma, const int64_t *all_h, const int64_t *all_r, int32_t n_queries,
                       int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
                       size_t workspace_bytes, void *stream);
+/* The same scores, bitwise, from `pieces` back-to-back launches over
+ * consecutive ranges of the one-pass grid (the first one `first_share` of it,
+ * 0 = equal pieces; DIRECT mode with enough rows, otherwise one launch).  A
+ * launch boundary lets workgroups of another stream that wait for registers
+ * RotatE's waves hold become resident (the PNA scoring pass
+ * beside RotatE).  rnnl_rotate_score == pieces 1. */
+int rnnl_rotate_score_pieces(const float *eemb, const void *entity_table, const float *relation_table, int32_t dim,
+                             float gamma, const int64_t *all_h, const int64_t *all_r, int32_t n_queries,
+                             int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
+                             size_t workspace_bytes, int32_t pieces, float first_share, void *stream);
 
 /* Backward of the RotatE score (training; embedding.py:45-70 under autograd):
  * for grad = dL/dscore (n_queries x E, row-major), hr = h o r per query

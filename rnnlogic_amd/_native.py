@@ -80,6 +80,8 @@ SIGNATURES = [
     ("rnnl_rule_search", ctypes.c_int, [_P, _I32, _P, _I64, _P, _I64, _P, _P]),
     ("rnnl_rotate_score", ctypes.c_int,
      [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _I32, _P, ctypes.c_size_t, _P]),
+    ("rnnl_rotate_score_pieces", ctypes.c_int,
+     [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _I32, _P, ctypes.c_size_t, _I32, _F32, _P]),
     ("rnnl_rotate_backward", ctypes.c_int, [_P, _I32, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
 ]
 

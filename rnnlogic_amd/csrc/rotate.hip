@@ -78,10 +78,11 @@ constexpr int XCDS = 8;
 #define RNNL_TILE_G 16
 #endif
 constexpr int TILE_G = RNNL_TILE_G;
-__device__ __forceinline__ bool xcd_tile(int nE, int nQ, int &et, int &qt) {
+__device__ __forceinline__ bool xcd_tile(int nE, int nQ, int &et, int &qt, int64_t blk0 = 0) {
   const int64_t n = (int64_t)nE * nQ;
   const int64_t per = (n + XCDS - 1) / XCDS;
-  const int64_t v = (int64_t)(blockIdx.x % XCDS) * per + blockIdx.x / XCDS;
+  const int64_t b = blk0 + blockIdx.x;  // blk0: a multiple of XCDS (one piece of a split launch)
+  const int64_t v = (b % XCDS) * per + b / XCDS;
   if (v >= n) return false;
   const int64_t super = v / ((int64_t)TILE_G * nE);
   const int64_t w = v % ((int64_t)TILE_G * nE);
@@ -355,7 +356,7 @@ static_assert(ROT_RE % 64 == 0 && 256 % ROT_RE == 0, "whole waves per query grou
 __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAVES, 8))) void rotate_direct_kernel(const float *__restrict__ ptab,
                                                            const float *__restrict__ hr, int D, float gamma,
                                                            int nq, int E, float *__restrict__ score,
-                                                           int accumulate, unsigned long long *clk) {
+                                                           int accumulate, unsigned long long *clk, int64_t blk0) {
   const int64_t Ep = ent_pad(E);
   int et, qt;
 #ifdef RNNL_ROT_LDS_PAD  // diagnostic: cap the blocks per CU through LDS
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
   if (threadIdx.x == 0) pad[0] = 0;
 #endif
   const int ngroups = (nq + DQ - 1) / DQ;
-  if (!xcd_tile((int)(Ep / ROT_RE), (ngroups + ROT_QW - 1) / ROT_QW, et, qt)) return;
+  if (!xcd_tile((int)(Ep / ROT_RE), (ngroups + ROT_QW - 1) / ROT_QW, et, qt, blk0)) return;
   // ROT_QW query groups per block, one per wave row, over the same ROT_RE
   // entities (their entity-plane loads meet in L1)
   qt = __builtin_amdgcn_readfirstlane(qt * ROT_QW + (int)threadIdx.x / ROT_RE);  // wave-uniform: SGPR h o r operands
@@ -822,6 +823,14 @@ int rnnl_rotate_relation_table(const float *remb, int32_t n_rel_total, int32_t D
   return RNNL_OK;
 }
 
+static int rot_split(int requested) {
+  static const int k = [] {
+    const char *e = getenv("RNNL_ROT_SPLIT");
+    return e ? std::max(1, atoi(e)) : 0;
+  }();
+  return k ? k : requested;
+}
+
 // hr slabs, then (split form only) the chunk sums, 256-byte aligned
 static size_t hr_bytes(int64_t nq, int D) { return (size_t)((nq + DQ - 1) / DQ) * D * 2 * DQ * sizeof(float); }
 
@@ -843,8 +852,16 @@ int rnnl_rotate_workspace_size(int32_t nq, int32_t E, int32_t D, int32_t mode, s
 int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, int32_t D, float gamma,
                       const int64_t *all_h, const int64_t *all_r, int32_t nq, int32_t E, float *score,
                       int32_t accumulate, int32_t mode, void *workspace, size_t ws_bytes, void *stream) {
+  return rnnl_rotate_score_pieces(eemb, etab, rtab, D, gamma, all_h, all_r, nq, E, score, accumulate, mode, workspace,
+                                  ws_bytes, 1, 0.f, stream);
+}
+
+int rnnl_rotate_score_pieces(const float *eemb, const void *etab, const float *rtab, int32_t D, float gamma,
+                             const int64_t *all_h, const int64_t *all_r, int32_t nq, int32_t E, float *score,
+                             int32_t accumulate, int32_t mode, void *workspace, size_t ws_bytes, int32_t pieces_req,
+                             float first_share, void *stream) {
   if (!eemb || !etab || !rtab || !all_h || !all_r || !score || D <= 0 || E <= 0 || nq < 0 || !valid_mode(mode) ||
-      accumulate < 0 || accumulate > 2) {
+      accumulate < 0 || accumulate > 2 || pieces_req < 1 || !(first_share >= 0.f && first_share < 1.f)) {
     set_error("rnnl_rotate_score: bad arguments");
     return RNNL_ERR_INVALID;
   }
@@ -873,10 +890,25 @@ int rnnl_rotate_score(const float *eemb, const void *etab, const float *rtab, in
       RNNL_HIP_CHECK(hipGetLastError());
       return RNNL_OK;
     }
-    hipLaunchKernelGGL(rotate_direct_kernel,
-                       dim3(xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW)), dim3(RB), 0,
-                       (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E, score,
-                       accumulate, g_clk);
+    // pieces > 1: the grid in back-to-back launches over consecutive block
+    // ranges (the first one `first_share` of the blocks, 0 = equal pieces) —
+    // the same blocks and the same per-element arithmetic, so the scores are
+    // bitwise those of one launch.  Each launch boundary drains RotatE's
+    // waves once: side-stream workgroups that wait for registers RotatE's
+    // waves hold (the 168-VGPR PNA scoring pass) become resident there
+    // (DESIGN §3.7).  RNNL_ROT_SPLIT / RNNL_ROT_SPLIT_AT override (A/B).
+    const int64_t total = xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW);
+    const char *at = getenv("RNNL_ROT_SPLIT_AT");
+    const float share = at ? (float)atof(at) : first_share;
+    const int pieces = (int)std::max<int64_t>(1, std::min<int64_t>(rot_split(pieces_req), total / (64 * XCDS)));
+    int64_t step = (total / pieces + XCDS - 1) / XCDS * XCDS;
+    int64_t first = pieces > 1 ? (int64_t)(share * total) / XCDS * XCDS : step;
+    if (first <= 0 || first >= total) first = step;
+    if (pieces > 1 && first != step) step = ((total - first) / (pieces - 1) + XCDS - 1) / XCDS * XCDS;
+    for (int64_t b0 = 0; b0 < total; b0 += (b0 == 0 ? first : step))
+      hipLaunchKernelGGL(rotate_direct_kernel, dim3((unsigned)std::min(b0 == 0 ? first : step, total - b0)), dim3(RB),
+                         0, (hipStream_t)stream, (const float *)etab, (const float *)workspace, D, gamma, nq, E,
+                         score, accumulate, g_clk, b0);
   } else {
     hipLaunchKernelGGL(rotate_mfma_kernel, dim3(xcd_grid(ent_pad(E) / ME, (nq + MQ - 1) / MQ)), dim3(256), 0,
                        (hipStream_t)stream, eemb, (const uint2 *)etab, (const float2 *)rtab, D, gamma, all_h, all_r,

@@ -103,9 +103,10 @@ class RotatE(torch.nn.Module):
             self._ws = torch.empty((need.value + 3) // 4, dtype=torch.float32, device=self.eemb.device)
         return self._ws.data_ptr(), need.value
 
-    def score_into(self, all_h, all_r, out, accumulate=False):
+    def score_into(self, all_h, all_r, out, accumulate=False, pieces=1, first_share=0.0):
         """out (B, |E|) (+)= gamma - dist(h o r, e) for every entity (HIP);
-        accumulate 2: atomic adds (rnnl_rotate_score)."""
+        accumulate 2: atomic adds (rnnl_rotate_score).  pieces > 1: the same
+        scores, bitwise, from that many launches (rnnl_rotate_score_pieces)."""
         if not self.eemb.is_cuda:
             raise RuntimeError("RotatE.forward runs on the HIP path; move the module to a GPU")
         all_h = all_h.to(self.eemb.device, torch.int64).contiguous()
@@ -113,10 +114,10 @@ class RotatE(torch.nn.Module):
         eemb = self.eemb.detach().contiguous()
         etab, rtab = self._device_tables()
         ws, ws_bytes = self._workspace(all_h.numel())
-        _native.call("rnnl_rotate_score", eemb.data_ptr(), etab.data_ptr(), rtab.data_ptr(),
+        _native.call("rnnl_rotate_score_pieces", eemb.data_ptr(), etab.data_ptr(), rtab.data_ptr(),
                      self.emb_dim, float(self.gamma), all_h.data_ptr(), all_r.data_ptr(), all_h.numel(),
                      self.num_entities, out.data_ptr(), int(accumulate), int(self.mode), ws, ws_bytes,
-                     torch.cuda.current_stream(self.eemb.device).cuda_stream)
+                     int(pieces), float(first_share), torch.cuda.current_stream(self.eemb.device).cuda_stream)
         return out
 
     def forward_torch(self, all_h, all_r):

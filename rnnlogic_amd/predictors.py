@@ -709,6 +709,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # ms overlapped vs 1.02 ms on one stream, the grounding's latency then
         # hiding behind RotatE)
         self.overlap_min_rows = int(os.environ.get("RNNL_OVERLAP_MIN_ROWS", "0"))
+        # pna aggregator: RotatE in two launches, the first over half its grid
+        # (rnnl_rotate_score_pieces; bitwise the same scores).  The PNA scoring
+        # pass needs 168 VGPRs per wave and finds no room beside RotatE's waves
+        # (6 x 76 per SIMD) until a launch boundary drains them: WN18RR step
+        # 21.0-21.1 -> 20.0-20.2 ms with the boundary at 0.4-0.6 of the grid
+        # (0.3: before the grounding ends, no gain).  The sum pass (64 VGPRs)
+        # fits beside RotatE; there the boundary only costs its drain
+        # (FB15k-237 81.2 -> 81.5 ms).  RNNL_ROT_YIELD=0 turns it off.
+        self.rotate_yield = os.environ.get("RNNL_ROT_YIELD", "1") != "0"
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -1028,9 +1037,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                     ev_g[k].record(side_g)
             if atomic:
                 main.wait_event(zero_ev)
+            pieces = 2 if self.rotate_yield and agg == _native.AGG_PNA and deferred and K == 1 else 1
             for k in range(K):
                 lo, hi = bounds[k], bounds[k + 1]
-                self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=2 if atomic else 0)
+                self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=2 if atomic else 0,
+                                       pieces=pieces, first_share=0.5 if pieces > 1 else 0.0)
                 ev_r[k].record(main)
             # the all-True mask (RotatE feature) is filled behind RotatE, beside the side streams' work
             mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)

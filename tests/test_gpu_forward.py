@@ -358,3 +358,12 @@ def test_rotate_split_form_is_bitwise(data, dev):
         base = torch.randn(5, E, device=dev)
         acc = rot.score_into(h[:5], r[:5], base.clone(), accumulate=True)
         assert torch.equal(acc, base + big[:5])
+        # the one-pass grid in several launches (rnnl_rotate_score_pieces, the
+        # PNA overlap's yield point): the same blocks, bitwise the same scores
+        for pieces, share in ((2, 0.5), (2, 0.37), (3, 0.0), (5, 0.1)):
+            out = torch.full_like(big, float("nan"))
+            rot.score_into(h, r, out, pieces=pieces, first_share=share)
+            assert torch.equal(out, big), (pieces, share)
+            zero = torch.zeros_like(big)
+            rot.score_into(h, r, zero, accumulate=2, pieces=pieces, first_share=share)
+            assert torch.equal(zero, big), ("atomic", pieces, share)
