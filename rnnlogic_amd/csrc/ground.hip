@@ -1118,9 +1118,12 @@ __device__ __forceinline__ void pin16(float (&x)[16]) {
                : "memory");
 }
 
+// score_one_2walk up to score_model: x1 = ReLU(LayerNorm(Linear(192, 16)(features)))
+// (returns false in the diagnostic RNNL_SCORE_NOMLP build, `diag` then holds the output).
 template <int AGG>
-__device__ __forceinline__ float score_one_2walk(const KParams &p, const float *wl, const float *relb,
-                                                 int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
+__device__ __forceinline__ bool pna_hidden_2walk(const KParams &p, const float *wl, int beg, int cnt,
+                                                 float mean_scale, uint64_t *dig_out, int t, float (&x1)[16],
+                                                 float &diag) {
   static_assert(AGG == RNNL_AGG_PNA, "the SUM aggregator scores in score_sum_kernel / score_sum_memo_kernel");
   using L = WL<AGG>;
   const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
@@ -1179,7 +1182,8 @@ __device__ __forceinline__ float score_one_2walk(const KParams &p, const float *
     }
 #pragma unroll
     for (int d = 0; d < 16; ++d) z += (float)a[d] + m[d];
-    return z * wl[L::S1B];
+    diag = z * wl[L::S1B];
+    return false;
   }
 #endif
   // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123);
@@ -1188,7 +1192,7 @@ __device__ __forceinline__ float score_one_2walk(const KParams &p, const float *
   const float dcl = fmaxf(degf, 1e-6f);
   const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
   const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
-  float x1[16], mean[16];
+  float mean[16];
 #pragma unroll
   for (int o = 0; o < 16; ++o) x1[o] = 0.f;
 #pragma unroll
@@ -1262,6 +1266,15 @@ __device__ __forceinline__ float score_one_2walk(const KParams &p, const float *
   const float rstd = 1.0f / sqrtf(var + 1e-5f);
 #pragma unroll
   for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+  return true;
+}
+
+template <int AGG>
+__device__ __forceinline__ float score_one_2walk(const KParams &p, const float *wl, const float *relb,
+                                                 int beg, int cnt, float mean_scale, uint64_t *dig_out, int t) {
+  using L = WL<AGG>;
+  float x1[16], diag = 0.f;
+  if (!pna_hidden_2walk<AGG>(p, wl, beg, cnt, mean_scale, dig_out, t, x1, diag)) return diag;
   float out = 0.f;
 #pragma unroll 2
   for (int o = 0; o < 128; ++o) {
@@ -1272,6 +1285,104 @@ __device__ __forceinline__ float score_one_2walk(const KParams &p, const float *
     out = fmaf(acc, wl[L::S1W + o], out);
   }
   return out + wl[L::S1B];
+}
+
+// score_model (Linear(32, 128) with the relation half folded into relb, ReLU,
+// Linear(128, 1)) for the wave's 64 candidates at once on the bf16 matrix
+// cores: 64 x 16 hidden inputs times the 16 x 128 layer-0 weights as
+// v_mfma_f32_16x16x16_bf16 tiles, every fp32 operand split exactly into three
+// bf16 parts (v = v0 + v1 + v2) and the six part products with i + j <= 2 kept
+// (the dropped ones are below 2^-24 of |x w|), accumulated in fp32.  On the
+// VALU this layer is 2,048 FMAs per candidate — a third of the PNA pass's
+// VALU instructions, and those take RotatE's issue slots when the pass runs
+// beside it; the matrix pipe runs beside the VALU.  Tile layout
+// (lane = 16 k + i16): A row i16 (candidate rt * 16 + i16), K 4k .. 4k + 3;
+// B K 4k .. 4k + 3, column i16 (output ct * 16 + i16); D rows 4k + j, column
+// i16.  Whole-wave (EXEC full): dead lanes pass x1 = 0 and ignore the result.
+// sb: [8 column tiles][3 parts][64 lanes] B fragments (built once per block);
+// sx: the wave's [3 parts][64 candidates][4 K-groups] staging; so: [64].
+typedef short pna_s16x4 __attribute__((ext_vector_type(4)));
+typedef float pna_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned short pna_bf16(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
+__device__ __forceinline__ void pna_split3(float v, unsigned short (&q)[3]) {
+  q[0] = pna_bf16(v);
+  const float r1 = v - __uint_as_float((unsigned)q[0] << 16);
+  q[1] = pna_bf16(r1);
+  q[2] = pna_bf16(r1 - __uint_as_float((unsigned)q[1] << 16));
+}
+__device__ __forceinline__ uint2 pna_pack4(const unsigned short (&q)[4][3], int part) {
+  return make_uint2(q[0][part] | ((unsigned)q[1][part] << 16), q[2][part] | ((unsigned)q[3][part] << 16));
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// score_mlp_mfma's B fragments from the packed weights: column tile ct, lane
+// (k, i16) holds W[ct * 16 + i16][4k .. 4k + 3] as 3 bf16 parts
+__device__ __forceinline__ void build_mlp_b(const float *__restrict__ W, uint2 *sb, int tid) {
+  for (int i = tid; i < 8 * 64; i += BS) {
+    const int ct = i >> 6, l = i & 63, o = ct * 16 + (l & 15), k0 = (l >> 4) * 4;
+    unsigned short q[4][3];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) pna_split3(W[W_S0X + o * 16 + k0 + kk], q[kk]);
+#pragma unroll
+    for (int part = 0; part < 3; ++part) sb[(ct * 3 + part) * 64 + l] = pna_pack4(q, part);
+  }
+}
+template <int AGG>
+__device__ __forceinline__ float score_mlp_mfma(const float (&x1)[16], const uint2 *__restrict__ sb, uint2 *sx,
+                                                float *so, const float *relb, const float *wl, int lane) {
+  using L = WL<AGG>;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    unsigned short q[4][3];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) pna_split3(x1[4 * g + kk], q[kk]);
+#pragma unroll
+    for (int part = 0; part < 3; ++part) sx[(part * 64 + lane) * 4 + g] = pna_pack4(q, part);
+  }
+  wave_lds_sync();
+  const int k = lane >> 4, i16 = lane & 15;
+#pragma unroll 1
+  for (int rt = 0; rt < 4; ++rt) {
+    pna_s16x4 a[3];
+#pragma unroll
+    for (int part = 0; part < 3; ++part)
+      a[part] = __builtin_bit_cast(pna_s16x4, sx[(part * 64 + rt * 16 + i16) * 4 + k]);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int ct = 0; ct < 8; ++ct) {
+      pna_s16x4 b[3];
+#pragma unroll
+      for (int part = 0; part < 3; ++part) b[part] = __builtin_bit_cast(pna_s16x4, sb[(ct * 3 + part) * 64 + lane]);
+      const float rb = relb[ct * 16 + i16], w1 = wl[L::S1W + ct * 16 + i16];
+      pna_f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], b[0], d, 0, 0, 0);  // smallest parts first
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[2], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[0], d, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(fmaxf(d[j] + rb, 0.f), w1, acc[j]);
+    }
+    // each lane holds 8 of the 128 output terms of rows 4k + j: sum over the
+    // 16 lanes of its K-group (xor 1, 2, 4, 8 stays inside the group)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[j];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 8);
+      if (i16 == 0) so[rt * 16 + 4 * k + j] = v;
+    }
+  }
+  wave_lds_sync();
+  const float out = so[lane] + wl[L::S1B];
+  wave_lds_sync();  // sx / so are rewritten by the next call
+  return out;
 }
 
 // One walk over a candidate's bucket entries for 8 dims (d0 .. d0 + 7) of
@@ -1634,6 +1745,11 @@ __device__ __forceinline__ void next_chunks(unsigned int *ctr, long long nchunks
 #ifndef RNNL_PNA_CK
 #define RNNL_PNA_CK 1
 #endif
+// score_model on the matrix cores in the chunked PNA pass (score_mlp_mfma);
+// -DRNNL_PNA_MFMA=0 builds the VALU form
+#ifndef RNNL_PNA_MFMA
+#define RNNL_PNA_MFMA 1
+#endif
 constexpr int PNA_CK = RNNL_PNA_CK;  // chunks per dequeue
 
 // 4 waves/SIMD for the four-walk scoring (128 VGPRs, no spills; 138 unforced
@@ -1646,6 +1762,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_CHU
   using L = WL<RNNL_AGG_PNA>;
   __shared__ __attribute__((aligned(16))) float s_w[L::N];
   __shared__ float s_relb[BS / 64][128];
+#if RNNL_PNA_MFMA
+  __shared__ uint2 s_b[8 * 3 * 64];           // score_model layer-0 B fragments (score_mlp_mfma)
+  __shared__ uint2 s_x[BS / 64][3 * 64 * 4];  // per wave: hidden inputs, 3 bf16 parts
+  __shared__ float s_o[BS / 64][64];
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
   check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna));
@@ -1660,6 +1781,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_CHU
     else if (i == L::S1B) v = W[W_S1B];
     s_w[i] = v;
   }
+#if RNNL_PNA_MFMA
+  build_mlp_b(W, s_b, tid);
+#endif
   __syncthreads();  // the only workgroup barrier: waves run independently from here
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
   float *relb = s_relb[wv];
@@ -1690,6 +1814,28 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_CHU
     }
     const int nc = p.n_cand[q];
     const int s = s0 + lane;
+#if RNNL_PNA_MFMA && !RNNL_PNA_4WALK && !defined(RNNL_SCORE_NOMLP)
+    // every lane reaches the whole-wave score_model; lanes past the chunk's
+    // candidates carry x1 = 0 and store nothing
+    const bool live = s < nc;
+    int64_t qb = 0;
+    int t = 0;
+    float x1[16], diag;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) x1[d] = 0.f;
+    if (live) {
+      qb = p.q_base[q];
+      const float ms = p.q_scale[q];
+      const int4 cr = p.cand[qb + s];
+      t = cr.x;
+      uint64_t dg = 0;
+      asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop (see score_kernel)
+      pna_hidden_2walk<RNNL_AGG_PNA>(p, s_w, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t, x1, diag);
+      if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
+    }
+    const float out = score_mlp_mfma<RNNL_AGG_PNA>(x1, s_b, s_x[wv], s_o[wv], relb, s_w, lane);
+    if (!live) continue;
+#else
     if (s >= nc) continue;
     const int64_t qb = p.q_base[q];
     const float ms = p.q_scale[q];
@@ -1703,6 +1849,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RNNL_PNA_CHU
     const float out = score_one_2walk<RNNL_AGG_PNA>(p, s_w, relb, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t);
 #endif
     if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
+#endif
     if (p.cand_out) {  // deferred: added once the base score exists (deferred_store)
       deferred_store(p, q, qb + s, t, out);
       continue;
@@ -1877,13 +2024,9 @@ __device__ __forceinline__ void gather_sum_entry(const KParams &p, int n, uint32
   fp = DIGEST ? (uint64_t)c * p.rl.node_fp[n] : 0;
 }
 
-// FuncToNodeSum tail + score_model on the candidate's feature sums
-__device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const float *relb, const float f[16]) {
+// FuncToNodeSum tail: x1 = ReLU(LayerNorm(Linear(16, 16)(f)))
+__device__ __forceinline__ void sum_hidden(const float *__restrict__ wl, const float f[16], float (&x1)[16]) {
   using L = WL<RNNL_AGG_SUM>;
-#ifdef RNNL_DIAG_NOMLP  // diagnostic build: the MLP's cost bounded (every caller)
-  return f[0] + f[15];
-#endif
-  float x1[16];
 #pragma unroll
   for (int o = 0; o < 16; ++o) {
     float acc = 0.f;
@@ -1905,6 +2048,16 @@ __device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const flo
   const float rstd = 1.0f / sqrtf(var + 1e-5f);
 #pragma unroll
   for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+}
+
+// FuncToNodeSum tail + score_model on the candidate's feature sums
+__device__ __forceinline__ float mlp_sum(const float *__restrict__ wl, const float *relb, const float f[16]) {
+  using L = WL<RNNL_AGG_SUM>;
+#ifdef RNNL_DIAG_NOMLP  // diagnostic build: the MLP's cost bounded (every caller)
+  return f[0] + f[15];
+#endif
+  float x1[16];
+  sum_hidden(wl, f, x1);
   float out = 0.f;
 #pragma unroll 2
   for (int o = 0; o < 128; ++o) {
@@ -2324,12 +2477,7 @@ __device__ __forceinline__ void pair_insert(const KParams &p, unsigned long long
 // the full gather + MLP, so the MLP runs on full waves; the queue is flushed
 // early only when the next chunk's relation differs (the folded relation bias
 // is per wave) and at the end.  Same arithmetic per candidate as
-// score_sum_memo_kernel.
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// score_sum_memo_kernel (wave_lds_sync: above, score_mlp_mfma).
 
 // A candidate with more than BIG_ENTRIES bucket entries is gathered by the
 // whole wave (lane i takes entries i, i + 64, ...; a butterfly sums the 16
