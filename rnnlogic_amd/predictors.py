@@ -687,11 +687,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # floor).  The grounding beside RotatE runs one workgroup per CU
         # (measured 88.1 vs 91.1 ms/step at full occupancy): it finishes in
         # ~18 ms, well inside the RotatE launch.
-        # The scoring pass beside RotatE runs 512 workgroups (2 per CU): FB15k-237
-        # 83.4-84.0 ms/step for 256-1024 vs 84.4-84.6 at full occupancy
+        # The scoring pass beside RotatE runs 256 workgroups (1 per CU): FB15k-237
+        # 83.4-84.0 ms/step for 256-1024 vs 84.4-84.6 at full occupancy in round 2;
+        # round 3 (pair memo, atomic adds): 256 / 512 / 768 -> 80.6-80.8 /
+        # 81.25-81.27 / 81.1-81.7 ms, WN18RR 256 / 512 -> 20.05 / 20.17 ms; on
+        # another box 128 / 192 / 256 -> 80.9 / 80.9-81.3 / 81.1-81.7 ms (the
+        # box-to-box spread is ~0.5 ms; 128-256 are within it)
         # (tools/env_ab.sh, RNNL_OVERLAP_SCORE_WG).
         self.overlap_ground_wg = int(os.environ.get("RNNL_OVERLAP_GROUND_WG", "256"))
-        self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "512"))
+        self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "256"))
         # sum aggregator: the scoring pass also runs beside RotatE, writing its
         # per-candidate outputs to the workspace; a short apply pass adds them
         # into the finished RotatE rows (rnnl_predictorplus_apply)
