@@ -74,6 +74,8 @@ TRAIN_SPECS = {  # dataset, PredictorPlus kwargs, RotatE dir — mirrors tools/m
     "train_umls_emb_pna_rotate": ("umls", dict(type="emb", entity_feature="RotatE", aggregator="pna"), 200),
     "train_kinship_lstm_sum_none": ("kinship", dict(type="lstm", entity_feature="none", aggregator="sum"), None),
     "train_kinship_emb_pna_bias": ("kinship", dict(type="emb", entity_feature="bias", aggregator="pna"), None),
+    # the headline model (config 4): FB15k-237 lstm/sum + RotatE(D = 1000) trainable, edge removal
+    "train_fb_lstm_sum_rotate": ("FB15k-237", dict(type="lstm", entity_feature="RotatE", aggregator="sum"), 1000),
 }
 # EM rule-weight Predictor fixtures (tools/make_golden_predictor.py)
 PRED_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("pred_") and f.endswith(".npz"))

@@ -20,7 +20,9 @@
       difference is accounted exactly: dL (dH) = the number of probe
       competitors that moved above (to at-or-above) the target minus those
       that moved below;
-  MRR / Hits deltas are logged and |dMRR| is bounded.
+  MRR / Hits deltas are logged, and |dMRR| is held to the sum over moved
+  rows of each row's exact (accounted) or largest (bounded) reciprocal-rank
+  change (tests/rank_parity.py).
 """
 import os
 
@@ -28,6 +30,7 @@ import numpy as np
 import pytest
 import torch
 
+import rank_parity
 from conftest import GOLDEN, Fixture
 
 pytestmark = pytest.mark.gpu
@@ -127,48 +130,16 @@ def test_per_query_ranks_vs_reference(case, dev):
     hip_t = logits[rows_i, t].cpu().numpy().astype(np.float64)
     hip_p = logits.gather(1, torch.from_numpy(np.maximum(pe, 0)).to(dev)).cpu().numpy().astype(np.float64)
     hit = mask[rows_i, t].cpu().numpy()
-    ref_t = z["s_t"].astype(np.float64)
-    ref_p = z["probe_score"].astype(np.float64)
-    valid_p = pe >= 0
-    # the target is a candidate in both or in neither (exact mask parity)
-    assert np.array_equal(hit, ~np.isnan(ref_t))
-    err = np.where(valid_p, np.abs(hip_p - ref_p), 0.0).max(1)
-    err = np.maximum(err, np.where(hit, np.abs(hip_t - np.nan_to_num(ref_t)), 0.0))
-    bp = z["batch_ptr"]
-    eps = np.zeros(n)
-    for b in range(nb):
-        eps[bp[b]:bp[b + 1]] = err[bp[b]:bp[b + 1]].max()
     # the forward's score tolerance (1e-4) must leave 2 eps inside the widest stored window
-    assert eps.max() <= 5e-5, "score error %g above 5e-5" % eps.max()
-    windows = z["windows"]
-    wi = np.searchsorted(windows, 2 * eps)  # smallest stored window >= 2 eps
-    assert (wi < len(windows)).all()
-    allowed = z["near_w"][np.arange(n), wi]
-    dL, dH = L - want[:, 3], H - want[:, 4]
-    diff = (dL != 0) | (dH != 0)
-    bad = np.nonzero((np.abs(dL) > allowed) | (np.abs(dH) > allowed))[0]
-    assert len(bad) == 0, (bad[:10], L[bad[:10]], H[bad[:10]], want[bad[:10]], allowed[bad[:10]])
-    # exact accounting where the window's competitors are all probes
-    nclose = pe.shape[1] - 4
-    close = valid_p[:, :nclose]
-    exact_rows = np.nonzero(hit & (allowed <= nclose))[0]
-    above_h = (hip_p[:, :nclose] > hip_t[:, None]) & close
-    above_r = (ref_p[:, :nclose] > ref_t[:, None]) & close
-    atleast_h = (hip_p[:, :nclose] >= hip_t[:, None]) & close
-    atleast_r = (ref_p[:, :nclose] >= ref_t[:, None]) & close
-    exp_dL = above_h.sum(1) - above_r.sum(1)
-    exp_dH = atleast_h.sum(1) - atleast_r.sum(1)
-    mism = exact_rows[(dL[exact_rows] != exp_dL[exact_rows]) | (dH[exact_rows] != exp_dH[exact_rows])]
-    assert len(mism) == 0, (mism[:10], dL[mism[:10]], exp_dL[mism[:10]], dH[mism[:10]], exp_dH[mism[:10]])
+    rep = rank_parity.check(want, L, H, hip_t, hip_p, hit, z["s_t"].astype(np.float64),
+                            z["probe_score"].astype(np.float64), pe, z["near_w"], z["windows"], z["batch_ptr"],
+                            eps_max=5e-5, nclose=pe.shape[1] - 4)
     got_m = TrainerPredictor.rank_metrics(np.stack([want[:, 0], want[:, 1], want[:, 2], L, H], 1).tolist(), True)
-    msg = "%s: %d rows / %d batches, score error max %.3g (median batch %.3g); %d rows with differing (L, H), " \
-          "all within their window (%d accounted exactly, %d bounded); " % (
-              case, n, nb, eps.max(), float(np.median(eps[bp[:-1]])), int(diff.sum()),
-              int(diff[exact_rows].sum()), int(diff.sum() - diff[exact_rows].sum()))
-    msg += ", ".join("%s delta %.3g" % (k, got_m[k] - float(z["metric/" + k]))
-                     for k in ("MRR", "Hit1", "Hit3", "Hit10", "MR"))
-    print(msg)
-    if not diff.any():
+    # the closed-form metric and the per-row accounting agree on the MRR change
+    assert abs((got_m["MRR"] - float(z["metric/MRR"])) - rep["d_mrr"]) <= 1e-10
+    print("%s (%d batches, %s): %s; %s" % (case, nb, str(z["source"]) if "source" in z.files else "reference run",
+                                           rank_parity.describe(rep), ", ".join(
+                                               "%s delta %.3g" % (k, got_m[k] - float(z["metric/" + k]))
+                                               for k in ("Hit1", "Hit3", "Hit10", "MR"))))
+    if not rep["moved"]:
         assert abs(got_m["MRR"] - float(z["metric/MRR"])) <= 1e-12
-    # each differing row moves its reciprocal-rank expectation by < 1 / L
-    assert abs(got_m["MRR"] - float(z["metric/MRR"])) <= max(1e-6, float(diff.sum()) / n)

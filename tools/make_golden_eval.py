@@ -96,19 +96,15 @@ def _rotate_rows(rot):
     return forward
 
 
-def _ranks_of_batch(i):
-    graph, test_set, model = _STATE["g"], _STATE["t"], _STATE["m"]
-    all_h, all_r, all_t, flag = test_set[i]
-    with torch.no_grad():
-        score, mask = model(all_h, all_r, None)
+def batch_records(score, mask, all_h, all_r, all_t, flag, E, rng, windows=WINDOWS):
+    """Per row of one batch: (h, r, t, L, H, near, s_t, near_w, probe_ent,
+    probe_score) from the reference's scores and mask (see the module doc)."""
     out = []
-    E = graph.entity_size
-    rng = np.random.RandomState(1000 + i)
     for k in range(all_t.numel()):
         t = int(all_t[k])
         pe = np.full(NPROBE, -1, np.int64)
         ps = np.full(NPROBE, np.nan, np.float32)
-        nw = np.zeros(len(WINDOWS), np.int64)
+        nw = np.zeros(len(windows), np.int64)
         if bool(mask[k, t]):
             val = score[k, t]
             fl = flag[k]
@@ -118,17 +114,25 @@ def _ranks_of_batch(i):
             near = int(((s - val).abs() <= TOL).sum())
             st = float(val)
             d = (s - val).abs().double().numpy()
-            nw[:] = [int((d <= w).sum()) for w in WINDOWS]
+            nw[:] = [int((d <= w).sum()) for w in windows]
             ids = torch.nonzero(fl).squeeze(1).numpy()
             close = ids[np.argsort(d, kind="stable")[:NCLOSE]]
             pe[:len(close)] = close
         else:
-            L, H, near, st = 1, graph.entity_size + 1, 0, float("nan")
+            L, H, near, st = 1, E + 1, 0, float("nan")
         pe[NCLOSE:] = rng.randint(0, E, NRAND)
         ok = pe >= 0
         ps[ok] = score[k][torch.from_numpy(pe[ok])].numpy()
         out.append((int(all_h[k]), int(all_r[k]), t, L, H, near, st, nw, pe, ps))
-    return i, out
+    return out
+
+
+def _ranks_of_batch(i):
+    graph, test_set, model = _STATE["g"], _STATE["t"], _STATE["m"]
+    all_h, all_r, all_t, flag = test_set[i]
+    with torch.no_grad():
+        score, mask = model(all_h, all_r, None)
+    return i, batch_records(score, mask, all_h, all_r, all_t, flag, graph.entity_size, np.random.RandomState(1000 + i))
 
 
 def _init_worker(case, rotate_rows):
@@ -138,13 +142,39 @@ def _init_worker(case, rotate_rows):
     _STATE.update(g=graph, t=test_set, m=model)
 
 
+def _cached(cache, i):
+    """Rows of batch i from a resumable per-batch cache (None if absent)."""
+    if not cache:
+        return None
+    f = os.path.join(cache, "b%05d.npz" % i)
+    if not os.path.exists(f):
+        return None
+    z = np.load(f)
+    return i, [(int(a[0]), int(a[1]), int(a[2]), int(a[3]), int(a[4]), int(a[5]), np.float32(s), nw, pe, ps)
+               for a, s, nw, pe, ps in zip(z["a"], z["s"], z["nw"], z["pe"], z["ps"])]
+
+
+def _store(cache, i, out):
+    if not cache:
+        return
+    rows = out[1]
+    tmp = os.path.join(cache, "b%05d.tmp.npz" % i)
+    np.savez(tmp, a=np.asarray([r[:6] for r in rows], np.int64), s=np.asarray([r[6] for r in rows], np.float32),
+             nw=np.stack([r[7] for r in rows]), pe=np.stack([r[8] for r in rows]), ps=np.stack([r[9] for r in rows]))
+    os.replace(tmp, os.path.join(cache, "b%05d.npz" % i))
+
+
 def _worker(args):
-    idx, threads = args
+    idx, threads, cache = args
     torch.set_num_threads(threads)
     res = []
     t0 = time.time()
     for j, i in enumerate(idx):
-        res.append(_ranks_of_batch(i))
+        got = _cached(cache, i)
+        if got is None:
+            got = _ranks_of_batch(i)
+            _store(cache, i, got)
+        res.append(got)
         if j % 50 == 0:
             print("  worker %d: %d/%d batches, %.0f s" % (os.getpid(), j, len(idx), time.time() - t0), flush=True)
     return res
@@ -175,7 +205,11 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--threads", type=int, default=2)
     ap.add_argument("--rotate-rows", action="store_true", help="row-wise RotatE from the reference's methods")
+    ap.add_argument("--cache", default="", help="directory of per-batch results (resumable long runs)")
+    ap.add_argument("--out", default="", help="output path (default tests/golden/eval_<case>.npz)")
     a = ap.parse_args()
+    if a.cache:
+        os.makedirs(a.cache, exist_ok=True)
     graph, test_set, model = _build(a.case)
     if a.rotate_rows:
         rot = model.RotatE
@@ -199,11 +233,11 @@ def main():
     t0 = time.time()
     import multiprocessing as mp
     if a.workers == 1:
-        parts = [_worker((order, a.threads))]
+        parts = [_worker((order, a.threads, a.cache))]
     else:
         # spawn: the parent has run torch ops (an OpenMP pool does not survive fork)
         with mp.get_context("spawn").Pool(a.workers, _init_worker, (a.case, a.rotate_rows)) as pool:
-            parts = pool.map(_worker, [(c, a.threads) for c in chunks])
+            parts = pool.map(_worker, [(c, a.threads, a.cache) for c in chunks])
     res = dict(x for p in parts for x in p)
     rows = [row for i in range(nb) for row in res[i]]
     arr = np.asarray([r[:6] for r in rows], dtype=np.int64)
@@ -216,7 +250,7 @@ def main():
                probe_score=np.stack([r[9] for r in rows]))
     for k, v in m.items():
         out["metric/" + k] = np.float64(v)
-    path = os.path.join(MG.OUT, "eval_%s.npz" % a.case)
+    path = a.out or os.path.join(MG.OUT, "eval_%s.npz" % a.case)
     np.savez_compressed(path, **out)
     print("%s: %d batches, %d rows in %.0f s -> %s (%d B); MRR %.6f, rows with near-ties %d" % (
         a.case, nb, len(rows), time.time() - t0, path, os.path.getsize(path), m["MRR"], int((arr[:, 5] > 0).sum())))

@@ -18,6 +18,12 @@ Stored in tests/golden/flow_umls.npz:
                          of flagged competitors within 1e-4 of the target's
                          score), TestDataset / ValidDataset batch order
   final/<split>/metric/<k>   the reference formula over those rows
+  it<k>/<split>/...      per iteration k, every valid / test query's record
+                         of tools/make_golden_eval.py (`batch_records`: L, H,
+                         near_w over FLOW_WINDOWS, probe entities and their
+                         reference scores), so that tests/test_gpu_flow.py
+                         holds each iteration's ranks and MRR to the score
+                         error it measures (tests/rank_parity.py)
 
 Usage: python tools/make_golden_flow.py
 """
@@ -41,13 +47,16 @@ import predictors as R_pred  # noqa: E402
 import trainer as R_trainer  # noqa: E402
 import utils as R_utils  # noqa: E402
 
-from make_golden_eval import metrics  # noqa: E402
+from make_golden_eval import WINDOWS, batch_records, metrics  # noqa: E402
 from rnnlogic_amd import datasets  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden", "flow_umls.npz")
 ITERS = 2
 BATCHES = 20
 TOL = 1e-4
+# trained weights differ from the reference's by ~1e-5 after 20 Adam steps, so the
+# score error is wider than a fixed-weight forward's: windows up to 5e-3
+FLOW_WINDOWS = WINDOWS + (2e-4, 5e-4, 1e-3, 2e-3, 5e-3)
 
 
 class _Losses(logging.Handler):
@@ -84,6 +93,26 @@ def ranks(model, ds, graph):
     return np.asarray(rows, dtype=np.int64)
 
 
+def records(model, ds, graph, out, prefix):
+    """Per-row parity records of one split (make_golden_eval.batch_records)."""
+    rows, ptr = [], [0]
+    model.eval()
+    with torch.no_grad():
+        for i in range(len(ds)):
+            all_h, all_r, all_t, flag = ds[i]
+            score, mask = model(all_h, all_r, None)
+            rows += batch_records(score, mask, all_h, all_r, all_t, flag, graph.entity_size,
+                                  np.random.RandomState(1000 + i), FLOW_WINDOWS)
+            ptr.append(len(rows))
+    out[prefix + "rows"] = np.asarray([r[:6] for r in rows], dtype=np.int64)
+    out[prefix + "s_t"] = np.asarray([r[6] for r in rows], dtype=np.float32)
+    out[prefix + "near_w"] = np.stack([r[7] for r in rows])
+    out[prefix + "probe_ent"] = np.stack([r[8] for r in rows]).astype(np.int32)
+    out[prefix + "probe_score"] = np.stack([r[9] for r in rows])
+    out[prefix + "batch_ptr"] = np.asarray(ptr, dtype=np.int64)
+    out[prefix + "windows"] = np.asarray(FLOW_WINDOWS, np.float64)
+
+
 def main():
     torch.set_num_threads(8)
     R_utils.set_seed(1)
@@ -106,6 +135,8 @@ def main():
         out["it%d/loss" % k] = np.asarray(handler.vals, dtype=np.float64)
         out["it%d/valid_mrr" % k] = np.float64(solver.evaluate("valid", expectation=True))
         out["it%d/test_mrr" % k] = np.float64(solver.evaluate("test", expectation=True))
+        for name, ds in (("valid", valid_set), ("test", test_set)):
+            records(model, ds, graph, out, "it%d/%s/" % (k, name))
         print("iteration %d: %d steps, valid MRR %.6f, test MRR %.6f" % (
             k, len(handler.vals), out["it%d/valid_mrr" % k], out["it%d/test_mrr" % k]), flush=True)
     for k, v in model.state_dict().items():

@@ -11,6 +11,19 @@ lr 0.005) are replayed on the seeded model.  Stored:
   s<k>/h,r,t,etr   the batch of step k
   s<k>/loss        loss of step k
   g/<name>         gradients of step 0 (before the optimizer step)
+  gs/<name>/...    for gradients too large to store (the RotatE tables at
+                   D = 1000): `rows` (every nonzero row when there are <= 64,
+                   else the step's h / t entities + 64 seeded random rows),
+                   `vals` (those rows) and `rowabs` (float64 sum of |g| of
+                   every row)
+
+The headline case (FB15k-237 lstm/sum + RotatE D = 1000, trainable) uses the
+row-wise RotatE.forward of tools/make_golden_eval.py (the reference's own
+project() / product() once per row, checked bitwise against the unpatched
+forward on the first rows): the unpatched forward holds (B * |E|, 2D) tensors
+per step (~40 GB with autograd at B = 32).  The forward values are identical;
+the gradients of the h / r rows sum the same per-entity terms in another fp32
+order (one row's product per row instead of one per (row, entity) pair).
 
 Usage:  python tools/make_golden_train.py [case ...]
 """
@@ -35,6 +48,7 @@ import utils as R_utils  # noqa: E402
 
 from rnnlogic_amd import datasets  # noqa: E402
 from make_golden import _rotate_dir  # noqa: E402
+from make_golden_eval import _rotate_rows  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden")
 K = 3
@@ -48,7 +62,28 @@ CASES = {
                                                                    aggregator="sum")),
     "train_kinship_emb_pna_bias": dict(data="kinship", model=dict(type="emb", entity_feature="bias",
                                                                   aggregator="pna")),
+    # the headline model (config 4) with edge removal, RotatE trainable
+    "train_fb_lstm_sum_rotate": dict(data="FB15k-237", model=dict(type="lstm", entity_feature="RotatE",
+                                                                  aggregator="sum", embedding_path="rotate"),
+                                     rotate_rows=True),
 }
+BIG = 1 << 20  # gradients with more elements are stored as sampled rows
+
+
+def _store_grad(out, n, g, h, t):
+    if g.size < BIG:
+        out["g/" + n] = g.copy()
+        return
+    g2 = g.reshape(g.shape[0], -1)
+    nz = np.nonzero(np.abs(g2).sum(1))[0]
+    if len(nz) <= 64:
+        rows = nz
+    else:
+        rng = np.random.RandomState(7)
+        rows = np.unique(np.concatenate([h, t, rng.randint(0, g2.shape[0], 64)]))
+    out["gs/%s/rows" % n] = rows.astype(np.int64)
+    out["gs/%s/vals" % n] = g2[rows].copy()
+    out["gs/%s/rowabs" % n] = np.abs(g2.astype(np.float64)).sum(1)
 
 
 def run_case(name, spec):
@@ -64,6 +99,14 @@ def run_case(name, spec):
     R_data.TestDataset(graph, 32)
     model = R_pred.PredictorPlus(graph, **kw)
     model.set_rules(datasets.rule_file(spec["data"]))
+    if spec.get("rotate_rows"):
+        rot = model.RotatE
+        # any two rows: a bitwise check of the row-wise form
+        h, r = torch.as_tensor([x[0] for x in train_set.batches[0][:2]]), torch.as_tensor(
+            [x[1] for x in train_set.batches[0][:2]])
+        with torch.no_grad():
+            assert torch.equal(rot(h, r), _rotate_rows(rot)(h, r))
+        rot.forward = _rotate_rows(rot)
     out = {}
     for k, v in model.state_dict().items():
         if k.startswith("RotatE."):
@@ -94,7 +137,7 @@ def run_case(name, spec):
             if k == 0:
                 for n, prm in model.named_parameters():
                     if prm.grad is not None:
-                        out["g/" + n] = prm.grad.detach().numpy().copy()
+                        _store_grad(out, n, prm.grad.detach().numpy(), all_h.numpy(), all_t.numpy())
             optim.step()
             optim.zero_grad()
         else:
@@ -106,6 +149,6 @@ def run_case(name, spec):
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    torch.set_num_threads(8)
+    torch.set_num_threads(int(os.environ.get("THREADS", "8")))
     for n in sys.argv[1:] or list(CASES):
         run_case(n, CASES[n])
