@@ -188,6 +188,21 @@ def reference_pytorch_baseline(model, graph, test_set, dev, feature, budget_s=15
             "note": "reference PyTorch predictor, dense torch-eager (oracle/reference_torch.py)"}
 
 
+def csrc_fingerprint():
+    """sha256 over the HIP/C++ sources of the library (rnnlogic_amd/csrc),
+    name-ordered: the stamp tools/pmc_traffic.py writes into the committed
+    traffic summaries (no git on the GPU box)."""
+    import hashlib
+    d = os.path.join(REPO, "rnnlogic_amd", "csrc")
+    h = hashlib.sha256()
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".cpp", ".h")) or name == "Makefile":
+            h.update(name.encode())
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
+
+
 def isolated_ground_ms(model, graph, h, r, dev):
     """Device time of the grounding + scoring kernels alone: one untimed
     one-stream rnnl_predictorplus_forward over all rows into a scratch score."""
@@ -583,7 +598,7 @@ def main():
     base_ms = float(np.mean([e["base"].elapsed_time(e["ground"]) for e in evs]))
     tail_ms = float(np.mean([e["ground"].elapsed_time(e["end"]) for e in evs]))
     overlapped = args.feature == "RotatE" and model.overlap
-    n_rot = model.overlap_chunks if overlapped else 1  # RotatE launches per step
+    n_rot = 1  # RotatE launches per step
     # the grounding + scoring kernels alone (one untimed one-stream launch), for their roofline
     if world > 1:  # the work-count fixture describes the whole split, not a shard
         ground_ms, ground_how = None, None
@@ -614,17 +629,25 @@ def main():
         del tmp
 
     # HBM traffic per launch from the committed PMC summary of this workload
-    # (tools/pmc_traffic.py; bench.py cannot read counters itself)
     # (tools/pmc_traffic.py; bench.py cannot read counters itself).  RotatE
-    # kernels: traffic_rotate.json (the overlapped chunk launches, as timed);
+    # kernels: traffic_rotate.json (the overlapped launches, as timed);
     # grounding kernels: traffic_bias.json (one launch over all rows, as the
-    # isolated grounding time)
+    # isolated grounding time).  A summary is used only when its stamp
+    # matches the kernel sources this run executes (csrc_fingerprint):
+    # counters of an older tree are not reported as this tree's traffic.
+    traffic_note = {}
+
     def load_traffic(name):
         tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % name)
         if not os.path.exists(tpath):
+            traffic_note[name] = "missing"
             return {}
         with open(tpath) as f:
             tj = json.load(f)
+        if tj.get("csrc_sha256") != csrc_fingerprint():
+            traffic_note[name] = "stale (captured at %s; kernel sources changed since)" % tj.get("commit", "?")
+            return {}
+        traffic_note[name] = "captured at %s" % tj.get("commit", "?")
         return {k.split("::")[-1].split("<")[0]: v["bytes"] for k, v in tj.get("kernels", {}).items()}
     # (the committed PMC summaries describe the one-rank workload: no traffic figure for a shard)
     traffic = load_traffic(args.feature.lower()) if world == 1 else {}
@@ -713,13 +736,14 @@ def main():
     rotate_bytes = 8.0 * D * E * ((nq + 15) // 16) + 8.0 * D * nq + 4.0 * nq * E
     if ground_ms is None:  # --profile-only with the RotatE overlap: no isolated grounding time
         ground_ms = float("nan")
-    gt = [gtraffic.get(k) for k in ("ground_kernel", "score_sum_kernel", "score_sum_memo_kernel", "memo_sum_kernel",
-                                    "score_kernel", "score_sum_chunk_kernel", "score_pna_chunk_kernel",
-                                    "chunk_sum_kernel", "chunk_fill_kernel")]
+    gt = [gtraffic.get(k) for k in ("ground_kernel", "memo_sum_kernel", "score_sum_chunk_kernel",
+                                    "score_pna_chunk_kernel", "pack_weights_kernel", "chunk_sum_kernel",
+                                    "chunk_fill_kernel")]
     gt = sum(x for x in gt if x) or None
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-              "traffic": gt, "kernel": "ground_kernel + scoring (chunk list + memo_sum_kernel + score_sum_chunk_kernel)",
+              "traffic": gt, "traffic_source": "profiles/traffic_bias.json: " + traffic_note.get("bias", "n/a"),
+              "kernel": "ground_kernel + scoring (chunk list + memo_sum_kernel + score_sum_chunk_kernel)",
               "ms": round(ground_ms, 3),
               "measured": ground_how,
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
@@ -739,6 +763,7 @@ def main():
         floor = 19.1 if mode == "direct" else 13.1
         roof = {"bound": "valu", "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": traffic.get("rotate_%s_kernel" % mode),
+                "traffic_source": "profiles/traffic_rotate.json: " + traffic_note.get("rotate", "n/a"),
                 "kernel": "rotate_%s_kernel" % mode,
                 "ms": round(base_ms / n_rot, 3), "alg_flops": rotate_flops / n_rot, "launches_per_step": n_rot,
                 "valu_issue": {"cycles_per_64_terms": round(cyc, 2), "floor": floor, "frac": round(floor / cyc, 3),

@@ -165,18 +165,13 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
 /* workgroups: cap on the persistent workgroups of the launch (0 = the full
  * default occupancy); a smaller grid leaves room on the CUs for a kernel on
  * another stream (the RotatE overlap).
- * deferred (either aggregator): the score pass writes each candidate's
- * score_model output into the workspace instead of adding it into `score`
- * (it then neither reads nor writes `score`, so it can run beside
- * rnnl_rotate_score); rnnl_predictorplus_apply adds the outputs into the
- * finished base score and sets mask (same fp32 sums as the direct pass).
- * deferred == 2 (feature add, mask NULL): the outputs are added atomically
- * into `score`, which the caller zeroed and whose base score arrives by
- * atomic adds too (rnnl_rotate_score accumulate == 2) — two addends on an
- * exact zero round to fl(base + out) in either order, so no apply pass is
- * needed and the result is the direct pass's bit for bit. */
-int rnnl_predictorplus_apply(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
-                             int32_t feature, float *score, uint8_t *mask, int32_t n_entities, void *stream);
+ * deferred: 0 = add each candidate's output into the finished base score in
+ * `score` and set mask; 2 = (feature add, mask NULL) add the outputs
+ * atomically into `score`, which the caller zeroed and whose base score
+ * arrives by atomic adds too (rnnl_rotate_score accumulate == 2): the pass
+ * then does not wait for the base score and runs beside rnnl_rotate_score;
+ * two addends on an exact zero round to fl(base + out) in either order, so
+ * the result is deferred == 0's bit for bit. */
 /* After a forward: RNNL_OK, or RNNL_ERR_OVERFLOW if any query exceeded the
  * workspace (those rows are incomplete; rerun with a larger capacity_scale).
  * Synchronises `stream`. */
@@ -227,6 +222,10 @@ int rnnl_debug_clock(void *dev_counters);
  * Affects the sizes computed by later rnnl_forward_workspace_size / launches
  * in this process. */
 int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t pool_per_query);
+/* Test hook: turn the SUM scoring pass's pair memo (score_model outputs
+ * reused between candidates with equal bucket entries) off (0) or on (1,
+ * the default), so that a test can compare the outputs both ways. */
+int rnnl_debug_pair_memo(int32_t on);
 
 /* ------------------------------------------------------- EM Predictor --
  * The EM loop's rule-weight predictor (reference src/predictors.py:17-119,

@@ -46,7 +46,6 @@ SIGNATURES = [
      [_P, _P, _I32, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _I32, _P]),
     ("rnnl_predictorplus_score", ctypes.c_int,
      [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _I32, _I32, _P]),
-    ("rnnl_predictorplus_apply", ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _I32, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_forward_header_bytes", ctypes.c_int, [_P]),
@@ -66,6 +65,7 @@ SIGNATURES = [
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_debug_clock", ctypes.c_int, [_P]),
     ("rnnl_debug_capacity", ctypes.c_int, [_I64, _I64, _I64]),
+    ("rnnl_debug_pair_memo", ctypes.c_int, [_I32]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
     ("rnnl_rotate_table_sizes", ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P]),

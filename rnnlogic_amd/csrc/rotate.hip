@@ -74,10 +74,7 @@ __device__ __forceinline__ void rotate_head(const float *hrow, const float2 *rro
 // and both the entity table slices and the query rows are re-read from that
 // XCD's L2 instead of MALL/HBM.  Only the speed depends on the placement.
 constexpr int XCDS = 8;
-#ifndef RNNL_TILE_G
-#define RNNL_TILE_G 16
-#endif
-constexpr int TILE_G = RNNL_TILE_G;
+constexpr int TILE_G = 16;
 __device__ __forceinline__ bool xcd_tile(int nE, int nQ, int &et, int &qt, int64_t blk0 = 0) {
   const int64_t n = (int64_t)nE * nQ;
   const int64_t per = (n + XCDS - 1) / XCDS;
@@ -121,20 +118,11 @@ static unsigned xcd_grid(int64_t nE, int64_t nQ) { return (unsigned)((nE * nQ + 
 // ahead.
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-#ifndef RNNL_WQ
-#define RNNL_WQ 4
-#endif
-#ifndef RNNL_WE
-#define RNNL_WE 4
-#endif
-#ifndef RNNL_MDC
-#define RNNL_MDC 8
-#endif
-constexpr int WQ = RNNL_WQ;    // 16-query tile rows per wave
-constexpr int WE = RNNL_WE;    // 16-entity tile columns per wave
+constexpr int WQ = 4;    // 16-query tile rows per wave
+constexpr int WE = 4;    // 16-entity tile columns per wave
 constexpr int MQ = 16 * WQ;    // queries per block
 constexpr int ME = 64 * WE;    // entities per block (4 waves side by side; divides 256)
-constexpr int MDC = RNNL_MDC;  // dims per LDS chunk (unrolled; even)
+constexpr int MDC = 8;  // dims per LDS chunk (unrolled; even)
 constexpr int AST = 256 / MQ;  // A side: dims built per pass of the block
 static_assert(MDC % 2 == 0 && MDC % AST == 0, "chunk shape");
 
@@ -153,10 +141,7 @@ __device__ __forceinline__ uint2 pack4(unsigned short a, unsigned short b, unsig
   return make_uint2(a | ((unsigned)b << 16), c | ((unsigned)d << 16));
 }
 
-#ifndef RNNL_ROT_MINB
-#define RNNL_ROT_MINB 1
-#endif
-__global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const float *__restrict__ eemb,
+__global__ __launch_bounds__(256, 1) void rotate_mfma_kernel(const float *__restrict__ eemb,
                                                           const uint2 *__restrict__ etab,
                                                           const float2 *__restrict__ rtab, int D, float gamma,
                                                           const int64_t *__restrict__ all_h,
@@ -301,15 +286,9 @@ __global__ __launch_bounds__(256, RNNL_ROT_MINB) void rotate_mfma_kernel(const f
 // FB15k-237 bench shape): more terms per dim amortise the per-dim loads and
 // address work, at 5 waves per SIMD.
 constexpr int RB = 256;   // entities per block (one per lane)
-#ifndef RNNL_DQ
-#define RNNL_DQ 20
-#endif
-constexpr int DQ = RNNL_DQ;  // queries per block (SGPR-resident)
+constexpr int DQ = 20;  // queries per block (SGPR-resident)
 constexpr int DCH = 32;   // dims per partial sum
-#ifndef RNNL_LCH
-#define RNNL_LCH 2
-#endif
-constexpr int LCH = RNNL_LCH;  // dims per entity-value prefetch block (divides DCH)
+constexpr int LCH = 2;  // dims per entity-value prefetch block (divides DCH)
 
 // hr[g][d][0..DQ-1 | DQ..2DQ-1] = (re | im) of (h o r)_d for queries DQ g + k.
 // One block per (query group, 64 dims): entity rows read coalesced along d,
@@ -338,43 +317,21 @@ __global__ __launch_bounds__(256) void rotate_hr_kernel(const float *__restrict_
   }
 }
 
-#ifndef RNNL_ROT_WAVES
-#define RNNL_ROT_WAVES 1
-#endif
-#ifndef RNNL_ROT_ACC_LDS
-#define RNNL_ROT_ACC_LDS 0
-#endif
-#ifndef RNNL_ROT_PRIO
-#define RNNL_ROT_PRIO 0
-#endif
-#ifndef RNNL_ROT_QW
-#define RNNL_ROT_QW 1
-#endif
-constexpr int ROT_QW = RNNL_ROT_QW;    // query groups per block (divides RB / 64)
+constexpr int ROT_QW = 1;              // query groups per block (divides RB / 64)
 constexpr int ROT_RE = RB / ROT_QW;    // entities per block
 static_assert(ROT_RE % 64 == 0 && 256 % ROT_RE == 0, "whole waves per query group; ent_pad divisible");
-__global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAVES, 8))) void rotate_direct_kernel(const float *__restrict__ ptab,
+__global__ __launch_bounds__(RB) void rotate_direct_kernel(const float *__restrict__ ptab,
                                                            const float *__restrict__ hr, int D, float gamma,
                                                            int nq, int E, float *__restrict__ score,
                                                            int accumulate, unsigned long long *clk, int64_t blk0) {
   const int64_t Ep = ent_pad(E);
   int et, qt;
-#ifdef RNNL_ROT_LDS_PAD  // diagnostic: cap the blocks per CU through LDS
-  __shared__ volatile char pad[RNNL_ROT_LDS_PAD];
-  if (threadIdx.x == 0) pad[0] = 0;
-#endif
   const int ngroups = (nq + DQ - 1) / DQ;
   if (!xcd_tile((int)(Ep / ROT_RE), (ngroups + ROT_QW - 1) / ROT_QW, et, qt, blk0)) return;
   // ROT_QW query groups per block, one per wave row, over the same ROT_RE
   // entities (their entity-plane loads meet in L1)
   qt = __builtin_amdgcn_readfirstlane(qt * ROT_QW + (int)threadIdx.x / ROT_RE);  // wave-uniform: SGPR h o r operands
   if (qt >= ngroups) return;  // wave-uniform; the kernel has no barrier
-#if RNNL_ROT_PRIO
-  // diagnostic: wave priority above the side-stream grounding / scoring waves
-  // sharing the SIMDs (RotatE then runs near its alone time but
-  // starves the side streams)
-  __builtin_amdgcn_s_setprio(RNNL_ROT_PRIO);
-#endif
   ClockStamp cs;
   cs.begin(clk);
   const int e = et * ROT_RE + (int)threadIdx.x % ROT_RE;  // < Ep: the table is padded
@@ -384,22 +341,9 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
   // software pipeline: the sqrt of dim d runs one dim later than its
   // squared distance (a VALU result feeding v_sqrt directly costs ~6 more
   // cycles per term; tools/micro/valu_rates.hip "direct pipelined")
-#if RNNL_ROT_ACC_LDS
-  // row totals live in LDS (each lane its own column: no barrier), which
-  // frees DQ VGPRs so RotatE keeps its occupancy beside the side-stream
-  // grounding waves
-  __shared__ float s_acc[DQ][RB];
-  float sq[DQ];
-#pragma unroll
-  for (int k = 0; k < DQ; ++k) {
-    s_acc[k][threadIdx.x] = 0.f;
-    sq[k] = 0.f;
-  }
-#else
   float acc[DQ], sq[DQ];
 #pragma unroll
   for (int k = 0; k < DQ; ++k) acc[k] = sq[k] = 0.f;
-#endif
   // entity values: LCH dims at a time, loaded one LCH-block ahead (fixed
   // register slots per dim, so the prefetch never waits on a rotation)
   float va[LCH], vb[LCH], na[LCH], nb[LCH];
@@ -442,22 +386,8 @@ __global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RNNL_ROT_WAV
       }
     }
 #pragma unroll
-    for (int k = 0; k < DQ; ++k) {
-#if RNNL_ROT_ACC_LDS
-      s_acc[k][threadIdx.x] += part[k];
-#else
-      acc[k] += part[k];
-#endif
-    }
-#if RNNL_ROT_ACC_LDS
-    asm volatile("" ::: "memory");  // keeps LICM from promoting the columns back into VGPRs
-#endif
+    for (int k = 0; k < DQ; ++k) acc[k] += part[k];
   }
-#if RNNL_ROT_ACC_LDS
-  float acc[DQ];
-#pragma unroll
-  for (int k = 0; k < DQ; ++k) acc[k] = s_acc[k][threadIdx.x];
-#endif
 #pragma unroll
   for (int k = 0; k < DQ; ++k) acc[k] += __builtin_amdgcn_sqrtf(sq[k]);  // v_sqrt_f32 (1 ulp)
   cs.end(clk);
@@ -823,14 +753,6 @@ int rnnl_rotate_relation_table(const float *remb, int32_t n_rel_total, int32_t D
   return RNNL_OK;
 }
 
-static int rot_split(int requested) {
-  static const int k = [] {
-    const char *e = getenv("RNNL_ROT_SPLIT");
-    return e ? std::max(1, atoi(e)) : 0;
-  }();
-  return k ? k : requested;
-}
-
 // hr slabs, then (split form only) the chunk sums, 256-byte aligned
 static size_t hr_bytes(int64_t nq, int D) { return (size_t)((nq + DQ - 1) / DQ) * D * 2 * DQ * sizeof(float); }
 
@@ -896,11 +818,10 @@ int rnnl_rotate_score_pieces(const float *eemb, const void *etab, const float *r
     // bitwise those of one launch.  Each launch boundary drains RotatE's
     // waves once: side-stream workgroups that wait for registers RotatE's
     // waves hold (the 168-VGPR PNA scoring pass) become resident there
-    // (DESIGN §3.7).  RNNL_ROT_SPLIT / RNNL_ROT_SPLIT_AT override (A/B).
+    // (DESIGN §3.7).
     const int64_t total = xcd_grid(ent_pad(E) / ROT_RE, ((nq + DQ - 1) / DQ + ROT_QW - 1) / ROT_QW);
-    const char *at = getenv("RNNL_ROT_SPLIT_AT");
-    const float share = at ? (float)atof(at) : first_share;
-    const int pieces = (int)std::max<int64_t>(1, std::min<int64_t>(rot_split(pieces_req), total / (64 * XCDS)));
+    const float share = first_share;
+    const int pieces = (int)std::max<int64_t>(1, std::min<int64_t>(pieces_req, total / (64 * XCDS)));
     int64_t step = (total / pieces + XCDS - 1) / XCDS * XCDS;
     int64_t first = pieces > 1 ? (int64_t)(share * total) / XCDS * XCDS : step;
     if (first <= 0 || first >= total) first = step;

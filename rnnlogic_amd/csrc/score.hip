@@ -1,0 +1,1048 @@
+// PredictorPlus forward for gfx950 (MI355X), K2: rule_to_entity + score_model.
+//
+// After the grounding (ground.hip) every candidate of a query has a bucket of
+// (trie node, path count) entries.  Its score (ref src/predictors.py:238-271):
+//   rule_to_entity (layers.py:53-126): FuncToNodeSum — the exact sum of
+//       count x node record (int32 fixed point, one shift per table; summed in
+//       fp64, which is exact below 2^23 total count, else int64), then
+//       Linear(16, 16), LayerNorm, ReLU; FuncToNode (pna) — sums of x and x^2,
+//       min and max per node, degree scalers, Linear(192, 16), LayerNorm, ReLU
+//   score_model (layers.py:9-51): Linear(32, 128) (the relation half folded
+//       into a per-relation bias), ReLU, Linear(128, 1)
+// added into the base score (bias / RotatE) or written (entity_feature none).
+// The unit of work is one wave x one chunk of <= 64 candidates of a query
+// (the chunk list in row order, see ground.hip).
+#include <hip/hip_runtime.h>
+
+#include "fwd.h"
+
+namespace rnnl {
+
+// Exact int64 sums of count x record word (off + d) over a candidate's bucket
+// entries, one dim at a time (few registers), as a double: the fallback of
+// pna_hidden_2walk's fp64 sums past a total count of 2^23.
+__device__ __forceinline__ void exact_sums(const KParams &p, int beg, int cnt, int off, double (&a)[16]) {
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    long long acc = 0;
+#pragma unroll 1
+    for (int e = beg; e < beg + cnt; ++e) {
+      const int2 be = p.bent[e];
+      acc += (long long)(uint32_t)be.y * reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna)[off + d];
+    }
+    a[d] = (double)acc;
+  }
+}
+
+// Two walks over the candidate's bucket entries, one per half of the node
+// record, each folding its features into the Linear(192, 16) sums as soon
+// as it ends: walk 1 the mean and min features (sum c x, min), walk 2 the max
+// and std ones (sum c x^2, max; std from walk 1's means).  Only one half's
+// accumulators (16 fp64 + 16 float) and the 16 sums and 16 means are live
+// in either walk instead of both halves' (one walk held ~250 VGPRs, 2
+// waves/SIMD); the entries are read twice (the second walk's loads hit L2).
+// Materialise the 16 sums here, and keep later loads below: the FMAs of one
+// Linear input complete before the next input's weights are read (a plain
+// memory clobber orders the loads but lets the scheduler hoist all of them
+// ahead of the FMAs, which spills).
+__device__ __forceinline__ void pin16(float (&x)[16]) {
+  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+               "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
+               :
+               : "memory");
+}
+
+// FuncToNode (pna) up to score_model: x1 = ReLU(LayerNorm(Linear(192, 16)(features)))
+__device__ __forceinline__ void pna_hidden_2walk(const KParams &p, const float *wl, int beg, int cnt,
+                                                 float mean_scale, uint64_t *dig_out, int t, float (&x1)[16]) {
+  using L = WL<RNNL_AGG_PNA>;
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  double a[16];  // exact: see the walk
+  float m[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    a[d] = 0;
+    m[d] = __builtin_huge_valf();
+  }
+  long long deg = 0;
+  uint64_t fp = 0, csum = 0;
+#pragma unroll 1
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const long long c = (uint32_t)be.y;
+    const double cd = (double)(uint32_t)be.y;
+    csum += (uint64_t)c;
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStridePna);
+    const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] = fma(cd, (double)rec[d], a[d]);
+      m[d] = fminf(m[d], fr[d]);
+    }
+    deg += c * p.rl.node_nrules[n];
+    if (dig_out) fp += (uint64_t)c * p.rl.node_fp[n];
+  }
+  if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
+  if (csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33 total count
+  // |record| < 2^30, so below a total count of 2^23 every product and partial
+  // sum is an integer under 2^53 and the fp64 FMAs are exact: a[d] is the
+  // int64 sum itself.  Past it (rare), exact int64 sums one dim at a time.
+  if (csum >> 23) exact_sums(p, beg, cnt, 0, a);
+  const double inv1 = ldexp(1.0, -(int)trailer[1]);
+  // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123);
+  // input j = (block * 16 + d) * 3 + s3, weights in LDS as [j][o]
+  const float degf = (float)(deg + 1);
+  const float dcl = fmaxf(degf, 1e-6f);
+  const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
+  const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
+  float mean[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float s = (float)(a[d] * inv1);
+    mean[d] = s / dcl;
+    const float fv[2] = {mean[d], m[d]};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) {
+        pin16(x1);  // one input's 16 weights live at a time: its FMAs end before the next loads
+        const float v = fv[b] * sc[s3];
+        const float *w = wl + L::ADDW + ((b * 16 + d) * 3 + s3) * 16;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
+      }
+    }
+  }
+  // walk 2: the squared half of the records and the max
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    a[d] = 0;
+    m[d] = -__builtin_huge_valf();
+  }
+  asm volatile("" ::: "memory");
+#pragma unroll 1
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const double cd = (double)(uint32_t)be.y;
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna);
+    const float *fr = reinterpret_cast<const float *>(rec + 48);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] = fma(cd, (double)rec[16 + d], a[d]);
+      m[d] = fmaxf(m[d], fr[d]);
+    }
+  }
+  if (csum >> 23) exact_sums(p, beg, cnt, 16, a);
+  const double inv2 = ldexp(1.0, -(int)trailer[4]);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float sq = (float)(a[d] * inv2);
+    const float sqm = sq / dcl;
+    const float fv[2] = {m[d], sqrtf(fmaxf(sqm - mean[d] * mean[d], 1e-6f))};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) {
+        pin16(x1);  // one input's 16 weights live at a time: its FMAs end before the next loads
+        const float v = fv[b] * sc[s3];
+        const float *w = wl + L::ADDW + (((b + 2) * 16 + d) * 3 + s3) * 16;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 16; ++o) x1[o] += wl[L::ADDB + o];
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+}
+
+// score_model (Linear(32, 128) with the relation half folded into relb, ReLU,
+// Linear(128, 1)) for the wave's 64 candidates at once on the bf16 matrix
+// cores: 64 x 16 hidden inputs times the 16 x 128 layer-0 weights as
+// v_mfma_f32_16x16x16_bf16 tiles, every fp32 operand split exactly into three
+// bf16 parts (v = v0 + v1 + v2) and the six part products with i + j <= 2 kept
+// (the dropped ones are below 2^-24 of |x w|), accumulated in fp32.  On the
+// VALU this layer is 2,048 FMAs per candidate — a third of the PNA pass's
+// VALU instructions, and those take RotatE's issue slots when the pass runs
+// beside it; the matrix pipe runs beside the VALU.  Tile layout
+// (lane = 16 k + i16): A row i16 (candidate rt * 16 + i16), K 4k .. 4k + 3;
+// B K 4k .. 4k + 3, column i16 (output ct * 16 + i16); D rows 4k + j, column
+// i16.  Whole-wave (EXEC full): dead lanes pass x1 = 0 and ignore the result.
+// sb: [8 column tiles][3 parts][64 lanes] B fragments (built once per block);
+// sx: the wave's [3 parts][64 candidates][4 K-groups] staging; so: [64].
+typedef short pna_s16x4 __attribute__((ext_vector_type(4)));
+typedef float pna_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned short pna_bf16(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
+__device__ __forceinline__ void pna_split3(float v, unsigned short (&q)[3]) {
+  q[0] = pna_bf16(v);
+  const float r1 = v - __uint_as_float((unsigned)q[0] << 16);
+  q[1] = pna_bf16(r1);
+  q[2] = pna_bf16(r1 - __uint_as_float((unsigned)q[1] << 16));
+}
+__device__ __forceinline__ uint2 pna_pack4(const unsigned short (&q)[4][3], int part) {
+  return make_uint2(q[0][part] | ((unsigned)q[1][part] << 16), q[2][part] | ((unsigned)q[3][part] << 16));
+}
+// score_mlp_mfma's B fragments from the packed weights: column tile ct, lane
+// (k, i16) holds W[ct * 16 + i16][4k .. 4k + 3] as 3 bf16 parts
+__device__ __forceinline__ void build_mlp_b(const float *__restrict__ W, uint2 *sb, int tid) {
+  for (int i = tid; i < 8 * 64; i += BS) {
+    const int ct = i >> 6, l = i & 63, o = ct * 16 + (l & 15), k0 = (l >> 4) * 4;
+    unsigned short q[4][3];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) pna_split3(W[W_S0X + o * 16 + k0 + kk], q[kk]);
+#pragma unroll
+    for (int part = 0; part < 3; ++part) sb[(ct * 3 + part) * 64 + l] = pna_pack4(q, part);
+  }
+}
+template <int AGG>
+__device__ __forceinline__ float score_mlp_mfma(const float (&x1)[16], const uint2 *__restrict__ sb, uint2 *sx,
+                                                float *so, const float *relb, const float *wl, int lane) {
+  using L = WL<AGG>;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    unsigned short q[4][3];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) pna_split3(x1[4 * g + kk], q[kk]);
+#pragma unroll
+    for (int part = 0; part < 3; ++part) sx[(part * 64 + lane) * 4 + g] = pna_pack4(q, part);
+  }
+  wave_lds_sync();
+  const int k = lane >> 4, i16 = lane & 15;
+#pragma unroll 1
+  for (int rt = 0; rt < 4; ++rt) {
+    pna_s16x4 a[3];
+#pragma unroll
+    for (int part = 0; part < 3; ++part)
+      a[part] = __builtin_bit_cast(pna_s16x4, sx[(part * 64 + rt * 16 + i16) * 4 + k]);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int ct = 0; ct < 8; ++ct) {
+      pna_s16x4 b[3];
+#pragma unroll
+      for (int part = 0; part < 3; ++part) b[part] = __builtin_bit_cast(pna_s16x4, sb[(ct * 3 + part) * 64 + lane]);
+      const float rb = relb[ct * 16 + i16], w1 = wl[L::S1W + ct * 16 + i16];
+      pna_f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], b[0], d, 0, 0, 0);  // smallest parts first
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[2], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[0], d, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(fmaxf(d[j] + rb, 0.f), w1, acc[j]);
+    }
+    // each lane holds 8 of the 128 output terms of rows 4k + j: sum over the
+    // 16 lanes of its K-group (xor 1, 2, 4, 8 stays inside the group)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[j];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 8);
+      if (i16 == 0) so[rt * 16 + 4 * k + j] = v;
+    }
+  }
+  wave_lds_sync();
+  const float out = so[lane] + wl[L::S1B];
+  wave_lds_sync();  // sx / so are rewritten by the next call
+  return out;
+}
+
+// ---------------------------------------------------------------- PNA scoring over chunks
+// The unit of work is one wave x one chunk of <= 64 consecutive candidates of
+// one query (lane = candidate), p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue
+// chunks independently, so a query with 17k candidates (WN18RR) is spread
+// over ~280 waves instead of holding one workgroup while the rest of the grid
+// drains; no workgroup barrier per query.  Each wave folds its relation's
+// half of score_model.layers.0 into its own LDS slice when the relation
+// changes.  Per candidate: pna_hidden_2walk (VALU), then score_model on the
+// matrix cores for the wave's 64 candidates at once (score_mlp_mfma).
+__global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const float *__restrict__ W) {
+  using L = WL<RNNL_AGG_PNA>;
+  __shared__ __attribute__((aligned(16))) float s_w[L::N];
+  __shared__ float s_relb[BS / 64][128];
+  __shared__ uint2 s_b[8 * 3 * 64];           // score_model layer-0 B fragments (score_mlp_mfma)
+  __shared__ uint2 s_x[BS / 64][3 * 64 * 4];  // per wave: hidden inputs, 3 bf16 parts
+  __shared__ float s_o[BS / 64][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna));
+  for (int i = tid; i < L::N; i += BS) {
+    float v = 0.f;
+    if (i < L::ADDB) v = W[W_ADDW + (i % 16) * L::KIN + i / 16];  // add_w transposed: [input j][output o]
+    else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
+    else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
+    else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
+    else if (i < L::S1W) v = W[W_S0X + i - L::S0X];
+    else if (i < L::S1B) v = W[W_S1W + i - L::S1W];
+    else if (i == L::S1B) v = W[W_S1B];
+    s_w[i] = v;
+  }
+  build_mlp_b(W, s_b, tid);
+  __syncthreads();  // the only workgroup barrier: waves run independently from here
+  const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
+  float *relb = s_relb[wv];
+  int cur_r = -1;
+  unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
+#pragma unroll 1
+  for (;; ++c) {
+    if (c == cend) next_chunks(&hdr[H_DEQUEUE2], nchunks, 1, c, cend);
+    if ((long long)c >= nchunks) break;
+    const int2 ck = p.chunks[c];
+    const int q = __builtin_amdgcn_readfirstlane(ck.x);
+    const int s0 = __builtin_amdgcn_readfirstlane(ck.y);
+    const int r = __builtin_amdgcn_readfirstlane((int)p.all_r[q]);
+    if (r != cur_r) {
+      // relation half of score_model.layers.0 folded into a per-wave bias
+      __builtin_amdgcn_wave_barrier();  // the previous chunk's reads of the slice are done
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = lane + 64 * j;
+        float acc = p.s0_b[o];
+        for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+        relb[o] = acc;
+      }
+      wave_lds_sync();
+      cur_r = r;
+    }
+    const int nc = p.n_cand[q];
+    const int s = s0 + lane;
+    // every lane reaches the whole-wave score_model; lanes past the chunk's
+    // candidates carry x1 = 0 and store nothing
+    const bool live = s < nc;
+    int64_t qb = 0;
+    int t = 0;
+    float x1[16];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) x1[d] = 0.f;
+    if (live) {
+      qb = p.q_base[q];
+      const float ms = p.q_scale[q];
+      const int4 cr = p.cand[qb + s];
+      t = cr.x;
+      uint64_t dg = 0;
+      asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop
+      pna_hidden_2walk(p, s_w, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t, x1);
+      if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
+    }
+    const float out = score_mlp_mfma<RNNL_AGG_PNA>(x1, s_b, s_x[wv], s_o[wv], relb, s_w, lane);
+    if (!live) continue;
+    const int64_t idx = (int64_t)q * p.g.E + t;
+    if (p.atomic_out) {  // deferred beside RotatE: added into the zeroed row (see deferred_add)
+      unsafeAtomicAdd(p.score + idx, out);
+      continue;
+    }
+    if (p.feature == RNNL_FEATURE_NONE)
+      p.score[idx] = out;
+    else
+      p.score[idx] = out + (p.base_row ? p.base_row[t] : p.score[idx]);
+    if (p.mask) p.mask[idx] = 1;
+  }
+}
+
+// ---------------------------------------------------------------- SUM aggregator (FuncToNodeSum)
+// A candidate's feature is the exact sum over its bucket entries (trie node
+// n, path count c) of c x record[n], the record being the int32 fixed-point
+// sum of the rule embeddings ending at n (one shift for the table, every
+// value < 2^30).  The sums are accumulated in fp64: below a total count of
+// 2^23 every product and partial sum is an integer under 2^53, so the fp64
+// sum IS the int64 sum (one v_cvt_f64_i32 + one v_fma_f64 per element instead
+// of two 64-bit integer multiply-adds and their fix-ups) and does not depend
+// on the entry order; past it the int64 walk below.
+
+// The exact int64 walk (counts past the fp64 range; also the digest's
+// degree / fingerprint terms).
+template <bool DIGEST>
+__device__ __forceinline__ void gather_sum_int64(const KParams &p, int beg, int cnt, float inv_scale, float f[16],
+                                              long long &deg, uint64_t &fp) {
+  long long acc[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) acc[d] = 0;
+  deg = 0;
+  fp = 0;
+  uint64_t csum = 0;
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const uint32_t cu = (uint32_t)be.y;
+    const long long c = cu;
+    csum += cu;
+    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) acc[d] += c * x[d];
+    if constexpr (DIGEST) {
+      deg += c * p.rl.node_nrules[n];
+      fp += (uint64_t)c * p.rl.node_fp[n];
+    }
+  }
+  if (csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33 total count
+#pragma unroll
+  for (int d = 0; d < 16; ++d) f[d] = (float)((double)acc[d] * (double)inv_scale);
+}
+
+template <bool DIGEST>
+__device__ __forceinline__ void gather_sum(const KParams &p, int beg, int cnt, float inv_scale, float f[16],
+                                           long long &deg, uint64_t &fp) {
+  double accd[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) accd[d] = 0.0;
+  deg = 0;
+  fp = 0;
+  uint64_t csum = 0;
+  for (int e = beg; e < beg + cnt; ++e) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const uint32_t cu = (uint32_t)be.y;
+    csum += cu;
+    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const double cd = (double)cu;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) accd[d] = fma(cd, (double)x[d], accd[d]);
+    if constexpr (DIGEST) {
+      deg += (long long)cu * p.rl.node_nrules[n];
+      fp += (uint64_t)cu * p.rl.node_fp[n];
+    }
+  }
+  if (csum >= (1ull << 23)) {  // rare: the exact int64 walk
+    gather_sum_int64<DIGEST>(p, beg, cnt, inv_scale, f, deg, fp);
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 16; ++d) f[d] = (float)(accd[d] * (double)inv_scale);
+}
+
+// LDS image of the SUM scoring weights: FuncToNodeSum's Linear(16, 16) and
+// LayerNorm and score_model's last layer as floats (VALU), and
+// score_model.layers.0's candidate half (128 x 16) as the A fragments of
+// v_mfma_f32_16x16x16_f16, each weight split into two fp16 parts.
+struct SumLds {
+  float addw[256], addb[16], lnw[16], lnb[16], s1w[128], s1b[4];
+  uint2 a0[8][2][64];  // [output tile][part][lane]: lane (k, i16) holds W0[16 ot + i16][4k .. 4k + 3]
+};
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// v = hi + lo + r with hi, lo fp16 (RNE) and |r| <= 2^-22 |v| for normal
+// parts (a subnormal lo part keeps an absolute error below 2^-25)
+__device__ __forceinline__ void split_f16(float v, _Float16 &hi, _Float16 &lo) {
+  hi = (_Float16)v;
+  lo = (_Float16)(v - (float)hi);
+}
+
+__device__ __forceinline__ void load_sum_weights(SumLds &w, const float *__restrict__ W) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) w.addw[i] = W[W_ADDW + i];
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) w.s1w[i] = W[W_S1W + i];
+  if (threadIdx.x < 16) {
+    w.addb[threadIdx.x] = W[W_ADDB + threadIdx.x];
+    w.lnw[threadIdx.x] = W[W_LNW + threadIdx.x];
+    w.lnb[threadIdx.x] = W[W_LNB + threadIdx.x];
+  }
+  if (threadIdx.x < 4) w.s1b[threadIdx.x] = threadIdx.x == 0 ? W[W_S1B] : 0.f;
+  for (int i = threadIdx.x; i < 8 * 64; i += blockDim.x) {
+    const int ot = i >> 6, l = i & 63, o = ot * 16 + (l & 15), k0 = (l >> 4) * 4;
+    f16x4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      _Float16 h, q;
+      split_f16(W[W_S0X + o * 16 + k0 + j], h, q);
+      hi[j] = h;
+      lo[j] = q;
+    }
+    w.a0[ot][0][l] = __builtin_bit_cast(uint2, hi);
+    w.a0[ot][1][l] = __builtin_bit_cast(uint2, lo);
+  }
+}
+
+// FuncToNodeSum tail: x1 = ReLU(LayerNorm(Linear(16, 16)(f)))   (layers.py:53-77)
+__device__ __forceinline__ void sum_hidden(const SumLds &w, const float f[16], float (&x1)[16]) {
+#pragma unroll
+  for (int o = 0; o < 16; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = fmaf(f[i], w.addw[o * 16 + i], acc);
+    x1[o] = acc + w.addb[o];
+  }
+  float mu = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) mu += x1[d];
+  mu = mu / 16.0f;
+  float var = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const float z = x1[d] - mu;
+    var = fmaf(z, z, var);
+  }
+  var = var / 16.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * w.lnw[d] + w.lnb[d], 0.f);
+}
+
+// score_model (layers.py:9-51) for the wave's 64 candidates (lane = candidate,
+// x1 its FuncToNodeSum output; whole wave, dead lanes pass anything finite):
+// Linear(32, 128) with the relation half folded into relb, ReLU,
+// Linear(128, 1).  Layer 0 runs on the matrix cores as D = W0 . X1^T, 16
+// candidates x 128 outputs per round (8 output tiles of
+// v_mfma_f32_16x16x16_f16; x1 and W0 split into two fp16 parts, the three
+// part products hi.hi, hi.lo, lo.hi accumulated in fp32 onto C = relb, the
+// dropped lo.lo below 2^-22 of |w x|; x1 >= 0 is post-LayerNorm, so fp16's
+// range holds it).  D lane (k, i16) holds outputs 4k .. 4k + 3 of candidate
+// i16: ReLU and the 128 -> 1 dot stay on the VALU per lane, summed over the
+// four k-lanes of a candidate by two xor shuffles.  A candidate's output
+// depends on its own x1 only (its own D column), in a fixed order, so equal
+// inputs give bit-identical outputs whatever the other lanes hold.  On the
+// VALU this layer was 2,048 FMAs + 256 max/fma per candidate, the bulk of the
+// SUM pass's VALU instructions, which take RotatE's issue slots beside it.
+// stage: the wave's 16 x 16 floats; relb: the wave's 128 folded biases.
+__device__ __forceinline__ float sum_mlp_mfma(const float (&x1)[16], const SumLds &w, float *stage,
+                                              const float *relb) {
+  const int lane = threadIdx.x & 63, k = lane >> 4, i16 = lane & 15;
+  float out = 0.f;
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    if (k == t) {
+      float4 *dst = reinterpret_cast<float4 *>(stage + i16 * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = make_float4(x1[4 * j], x1[4 * j + 1], x1[4 * j + 2], x1[4 * j + 3]);
+    }
+    wave_lds_sync();
+    const float4 xv = reinterpret_cast<const float4 *>(stage)[i16 * 4 + k];  // candidate 16 t + i16, K 4k..4k+3
+    wave_lds_sync();  // the next round rewrites the stage
+    f16x4 bh, bl;
+    {
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        _Float16 h, q;
+        split_f16(xs[j], h, q);
+        bh[j] = h;
+        bl[j] = q;
+      }
+    }
+    float acc = 0.f;
+#pragma unroll 1
+    for (int ot = 0; ot < 8; ++ot) {
+      const f16x4 ah = __builtin_bit_cast(f16x4, w.a0[ot][0][lane]);
+      const f16x4 al = __builtin_bit_cast(f16x4, w.a0[ot][1][lane]);
+      const float4 rb = reinterpret_cast<const float4 *>(relb)[ot * 4 + k];
+      f32x4 d = {rb.x, rb.y, rb.z, rb.w};
+      d = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, d, 0, 0, 0);  // smallest products first
+      d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, d, 0, 0, 0);
+      const float4 w1 = reinterpret_cast<const float4 *>(w.s1w)[ot * 4 + k];
+      acc = fmaf(fmaxf(d[0], 0.f), w1.x, acc);
+      acc = fmaf(fmaxf(d[1], 0.f), w1.y, acc);
+      acc = fmaf(fmaxf(d[2], 0.f), w1.z, acc);
+      acc = fmaf(fmaxf(d[3], 0.f), w1.w, acc);
+    }
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    if (k == t) out = acc + w.s1b[0];  // lane 16 t + i16 is candidate i16 of this round
+  }
+  return out;
+}
+
+// relation half of score_model.layers.0 folded into a per-relation bias (128 lanes)
+__device__ __forceinline__ float relation_bias(const KParams &p, int r, int o) {
+  float acc = p.s0_b[o];
+  for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+  return acc;
+}
+
+// ---------------------------------------------------------------- single-path memo
+// 38 % of the FB15k-237 test candidates are reached by exactly one path of
+// one rule-end node n (one bucket entry of count 1).  Their feature is n's
+// record itself, so their score_model output depends on (head relation, n)
+// only: memo_sum_kernel computes it once per launch for every leaf node of
+// every head (131,883 MLPs instead of ~22 M), with the full path's own
+// arithmetic (the single entry's gather, then sum_hidden and sum_mlp_mfma).
+// Launches with at most this many rows skip it (pair-memo keys instead).
+constexpr int MEMO_SCAN_ROWS = 2048;
+
+// One workgroup per head relation with rules: memo[n] for its leaf nodes
+// (whole waves: score_model runs on the matrix cores, sum_mlp_mfma).
+__global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__restrict__ W) {
+  __shared__ SumLds s_w;
+  __shared__ __attribute__((aligned(16))) float s_relb[128];
+  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][256];
+  const int r = blockIdx.x;
+  const int lp = p.rl.head_leaf_ptr[r], nl = p.rl.head_leaf_ptr[r + 1] - lp;
+  if (nl <= 0) return;  // uniform
+  load_sum_weights(s_w, W);
+  if (threadIdx.x < 128) s_relb[threadIdx.x] = relation_bias(p, r, threadIdx.x);
+  __syncthreads();
+  const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
+  const float inv_scale = ldexpf(1.f, -shift);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int b0 = wv * 64; b0 < nl; b0 += BS) {  // wave-uniform
+    const int i = b0 + lane;
+    const int n = i < nl ? p.rl.head_leaf_node[lp + i] : -1;
+    float f[16];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) f[d] = 0.f;
+    if (n >= 0) {
+      const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) f[d] = (float)((double)x[d] * (double)inv_scale);  // gather_sum of (n, 1)
+    }
+    float x1[16];
+    sum_hidden(s_w, f, x1);
+    const float out = sum_mlp_mfma(x1, s_w, s_stage[wv], s_relb);
+    if (n >= 0) p.memo[n] = out;
+  }
+}
+
+__device__ __forceinline__ void sum_write_out(const KParams &p, int q, int t, float out, float base) {
+  const int64_t idx = (int64_t)q * p.g.E + t;
+  if (p.atomic_out) {
+    // deferred beside RotatE: the row starts at zero and RotatE adds its score
+    // atomically too — two addends on an exact zero give fl(base + out) in
+    // either order, the one-stream path's bit for bit
+    unsafeAtomicAdd(p.score + idx, out);
+    return;
+  }
+  p.score[idx] = p.feature == RNNL_FEATURE_NONE ? out : out + base;
+  if (p.mask) p.mask[idx] = 1;
+}
+
+__device__ __forceinline__ float sum_base(const KParams &p, int q, int t) {
+  if (p.feature == RNNL_FEATURE_NONE || p.atomic_out) return 0.f;
+  return p.base_row ? p.base_row[t] : p.score[(int64_t)q * p.g.E + t];
+}
+
+// ---------------------------------------------------------------- pair memo
+// A candidate's feature is the exact sum of count x record over its bucket
+// entries, so candidates whose entries are equal get bit-identical
+// score_model outputs.  On an FB15k-237 test sample 57 % of the candidates
+// past the single-path memo hold one or two entries and 19 % three, and
+// within a 32-row relation batch only 7 % / 27 % of those entry lists are
+// distinct.  The key packs (relation, each entry's node offset and count, in
+// canonical order) exactly into K = 31 + psbits bits and is mixed by a
+// bijection of [0, 2^K): the low psbits bits pick the slot, the high 31 bits
+// are the tag, so (slot, tag) identifies the entries exactly.  A slot is one
+// 8-B word (tag + 1) << 32 | output bits, written and read whole: any word a
+// lane reads is some key's true output, and a lost or overwritten insert
+// only costs a recomputation.
+constexpr unsigned long long PAIR_NOKEY = ~0ull;
+
+__device__ __forceinline__ void entry_cswap(unsigned &oa, unsigned &ca, unsigned &ob, unsigned &cb) {
+  if (ob < oa || (ob == oa && cb < ca)) {
+    const unsigned to = oa, tc = ca;
+    oa = ob;
+    ca = cb;
+    ob = to;
+    cb = tc;
+  }
+}
+
+// z = 1..3 bucket entries (absent ones (0, 0): a node offset is never 0, the
+// root ends no rule).  Format bit 0: one or two entries, pbc-bit counts; 1:
+// three entries, pbc3-bit counts.
+__device__ __forceinline__ unsigned long long pair_key(const KParams &p, int r, int root, int z, int2 b0, int2 b1,
+                                                       int2 b2) {
+  unsigned o0 = (unsigned)(b0.x - root), c0 = (unsigned)b0.y;
+  unsigned o1 = z >= 2 ? (unsigned)(b1.x - root) : 0u, c1 = z >= 2 ? (unsigned)b1.y : 0u;
+  unsigned o2 = z >= 3 ? (unsigned)(b2.x - root) : 0u, c2 = z >= 3 ? (unsigned)b2.y : 0u;
+  if (z >= 2) entry_cswap(o0, c0, o1, c1);  // canonical order
+  if (z == 3) {
+    entry_cswap(o1, c1, o2, c2);
+    entry_cswap(o0, c0, o1, c1);
+  }
+  const int bc = z == 3 ? p.pbc3 : p.pbc;
+  if (bc <= 0 || ((c0 | c1 | c2) >> bc)) return PAIR_NOKEY;  // a count past the key's field
+  unsigned long long k = z == 3 ? 1ull : 0ull;
+  int sh = 1;
+  k |= (unsigned long long)r << sh;
+  sh += p.pbr;
+  k |= (unsigned long long)o0 << sh;
+  sh += p.pbo;
+  k |= (unsigned long long)o1 << sh;
+  sh += p.pbo;
+  if (z == 3) {
+    k |= (unsigned long long)o2 << sh;
+    sh += p.pbo;
+  }
+  k |= (unsigned long long)c0 << sh;
+  sh += bc;
+  k |= (unsigned long long)c1 << sh;
+  sh += bc;
+  if (z == 3) k |= (unsigned long long)c2 << sh;
+  const int K = 31 + p.psbits;
+  const unsigned long long mk = (1ull << K) - 1ull;
+  k = (k * 0x9E3779B97F4A7C15ull) & mk;  // odd multiplier mod 2^K, xor-shifts: a bijection of [0, 2^K)
+  k ^= k >> (K / 2);
+  k = (k * 0xBF58476D1CE4E5B9ull) & mk;
+  k ^= k >> (K / 2 + 1);
+  return k;
+}
+
+__device__ __forceinline__ bool pair_lookup(const KParams &p, unsigned long long m, float &out) {
+  const unsigned long long w = p.ptab[m & ((1ull << p.psbits) - 1ull)];
+  out = __uint_as_float((unsigned)w);
+  return (unsigned)(w >> 32) == (unsigned)(m >> p.psbits) + 1u;
+}
+
+__device__ __forceinline__ void pair_insert(const KParams &p, unsigned long long m, float out) {
+  p.ptab[m & ((1ull << p.psbits) - 1ull)] =
+      ((unsigned long long)((unsigned)(m >> p.psbits) + 1u) << 32) | (unsigned long long)__float_as_uint(out);
+}
+
+// ---------------------------------------------------------------- SUM scoring over chunks
+// One wave x one 64-candidate chunk of one query at a time (p.chunks, in row
+// order), no workgroup barrier after the weight load.  Single-path
+// candidates take the memo and candidates whose entries are in the pair memo
+// take it (three loads and the store); the others are compacted (ballot +
+// prefix) into the wave's LDS queue of (query, pool index) and scored 64 at a
+// time by the full gather + MLP, so the MLP runs on full waves; the queue is
+// flushed early only when the next chunk's relation differs (the folded
+// relation bias is per wave) and at the end.
+//
+// A candidate with more than BIG_ENTRIES bucket entries is gathered by the
+// whole wave on small launches (COOP; lane i takes entries i, i + 64, ...; a
+// butterfly sums the 16 fp64 partials): its lane would otherwise walk the
+// list alone, two dependent loads per entry, while the wave waits — on a
+// one-batch launch the scoring time is the longest such walk.  The fp64 sums
+// of exact count x record products are exact in any order, so the feature is
+// the per-lane walk's bit for bit.  Up to BIG_SLOTS per round, their features
+// staged in LDS.
+constexpr int BIG_ENTRIES = 16;
+constexpr int BIG_SLOTS = 16;
+static_assert(BIG_SLOTS * 16 <= 256, "the long-list features share a wave's 256-float score_model stage");
+
+template <bool DIGEST>
+__device__ __forceinline__ void coop_gather(const KParams &p, int beg, int cnt, float inv_scale, float *fslot,
+                                            uint64_t &csum, long long &deg, uint64_t &fp) {
+  const int lane = threadIdx.x & 63;
+  double acc[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) acc[d] = 0.0;
+  csum = 0;
+  deg = 0;
+  fp = 0;
+  for (int e = beg + lane; e < beg + cnt; e += 64) {
+    const int2 be = p.bent[e];
+    const int n = be.x;
+    const uint32_t cu = (uint32_t)be.y;
+    csum += cu;
+    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const double cd = (double)cu;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) acc[d] = fma(cd, (double)x[d], acc[d]);
+    if constexpr (DIGEST) {
+      deg += (long long)cu * p.rl.node_nrules[n];
+      fp += (uint64_t)cu * p.rl.node_fp[n];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) acc[d] += __shfl_xor(acc[d], off, 64);
+    csum += __shfl_xor(csum, off, 64);
+    if constexpr (DIGEST) {
+      deg += __shfl_xor(deg, off, 64);
+      fp += __shfl_xor(fp, off, 64);
+    }
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d)
+    if (lane == d) v = (float)(acc[d] * (double)inv_scale);
+  if (lane < 16) fslot[lane] = v;
+}
+
+// Score m <= 64 queued candidates of relation r (lane i: queue[i]); the
+// whole wave calls it (score_model on the matrix cores needs every lane).
+// COOP = false (large launches): each lane walks its own list — the
+// cooperative rounds' registers spill at the 64-VGPR cap, which costs the
+// throughput-bound launches more (RotatE step +0.8 ms) than the long walks.
+template <bool DIGEST>
+__device__ __forceinline__ void sum_score_lane(const KParams &p, const SumLds &w, const float *relb, float *stage,
+                                               bool live, const int2 it, const int4 cr, const float (&f)[16],
+                                               long long deg, uint64_t fp, float base, int r, int root) {
+  if constexpr (DIGEST)
+    if (live)
+      atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + it.x),
+                (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
+  asm volatile("" ::: "memory");  // keep the LDS weight reads inside (hoisted they pin ~200 VGPRs)
+  float x1[16];
+  sum_hidden(w, f, x1);
+  const float out = sum_mlp_mfma(x1, w, stage, relb);
+  if (!live) return;
+  sum_write_out(p, it.x, cr.x, out, base);
+  if (!DIGEST && p.ptab && cr.z <= 3) {
+    const int2 z0 = make_int2(0, 0);
+    const unsigned long long key = pair_key(p, r, root, cr.z, p.bent[cr.y], cr.z >= 2 ? p.bent[cr.y + 1] : z0,
+                                            cr.z >= 3 ? p.bent[cr.y + 2] : z0);
+    if (key != PAIR_NOKEY) pair_insert(p, key, out);
+  }
+}
+
+template <bool DIGEST, bool COOP>
+__device__ __forceinline__ void sum_chunk_flush(const KParams &p, const SumLds &w, const float *relb, float *stage,
+                                                const int2 *queue, int m, float inv_scale, int r, int root,
+                                                float *fbig) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (!COOP) {
+    const bool live = lane < m;
+    int2 it = make_int2(0, 0);
+    int4 cr = make_int4(0, 0, 0, 0);
+    float base = 0.f;
+    float f[16];
+    long long deg = 0;
+    uint64_t fp = 0;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) f[d] = 0.f;
+    if (live) {
+      it = queue[lane];
+      cr = p.cand[it.y];
+      base = sum_base(p, it.x, cr.x);  // issued before the gather: its latency hides under it
+      gather_sum<DIGEST>(p, cr.y, cr.z, inv_scale, f, deg, fp);
+    }
+    sum_score_lane<DIGEST>(p, w, relb, stage, live, it, cr, f, deg, fp, base, r, root);
+    return;
+  }
+  int2 it = make_int2(0, 0);
+  int4 cr = make_int4(0, 0, 0, 0);
+  if (lane < m) {
+    it = queue[lane];
+    cr = p.cand[it.y];
+  }
+  bool todo = lane < m;
+#pragma unroll 1
+  while (true) {
+    // this round's long-list candidates, gathered by the whole wave
+    uint64_t big = __ballot(todo && cr.z > BIG_ENTRIES);
+    int slot = -1;  // >= 0: this lane's feature is in fbig[slot]; -2: walk it here (int64 range)
+    long long bdeg = 0;
+    uint64_t bfp = 0;
+#pragma unroll 1
+    for (int nb = 0; big && nb < BIG_SLOTS; ++nb) {
+      const int owner = __builtin_ctzll(big);
+      big &= big - 1;
+      const int beg = __builtin_amdgcn_readlane(cr.y, owner), cnt = __builtin_amdgcn_readlane(cr.z, owner);
+      uint64_t csum;
+      long long deg;
+      uint64_t fp;
+      coop_gather<DIGEST>(p, beg, cnt, inv_scale, fbig + nb * 16, csum, deg, fp);
+      if (lane == owner) {
+        slot = csum >= (1ull << 23) ? -2 : nb;  // past the exact fp64 range: the lane's int64 walk
+        bdeg = deg;
+        bfp = fp;
+      }
+    }
+    wave_lds_sync();
+    const bool go = todo && (cr.z <= BIG_ENTRIES || slot != -1);
+    float base = 0.f;
+    float f[16];
+    long long deg = 0;
+    uint64_t fp = 0;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) f[d] = 0.f;
+    if (go) {
+      base = sum_base(p, it.x, cr.x);  // issued before the gather: its latency hides under it
+      if (slot >= 0) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) f[d] = fbig[slot * 16 + d];
+        deg = bdeg;
+        fp = bfp;
+      } else {
+        gather_sum<DIGEST>(p, cr.y, cr.z, inv_scale, f, deg, fp);
+      }
+    }
+    sum_score_lane<DIGEST>(p, w, relb, stage, go, it, cr, f, deg, fp, base, r, root);
+    if (go) todo = false;
+    wave_lds_sync();  // fbig is reused by the next round
+    if (__ballot(todo) == 0ull) break;
+  }
+}
+
+constexpr int SUM_CK = 8;  // chunks per dequeue on large launches
+
+template <bool DIGEST, bool COOP>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void score_sum_chunk_kernel(
+    KParams p, const float *__restrict__ W) {
+  __shared__ SumLds s_w;
+  __shared__ __attribute__((aligned(16))) float s_relb[BS / 64][128];
+  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][256];  // sum_mlp_mfma's x1 staging
+  __shared__ int2 s_queue[BS / 64][128];
+  // the COOP flush's long-list features (BIG_SLOTS x 16 floats) share the
+  // stage: they are read into registers before score_model stages x1
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+  load_sum_weights(s_w, W);
+  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum));
+  const int shift = (int)reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStrideSum)[1];
+  const float inv_scale = ldexpf(1.f, -shift);
+  __syncthreads();  // the only workgroup barrier: waves run independently from here
+  const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
+  float *relb = s_relb[wv];
+  int2 *queue = s_queue[wv];
+  int cur_r = -1, cur_root = 0, n = 0;  // wave-uniform: the queue's relation, its trie root, the queue length
+  unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
+  // chunks per dequeue: SUM_CK on large launches, fewer where that would leave
+  // waves idle (at least 8 dequeues per wave)
+  const int ck = (int)max(1ll, min((long long)SUM_CK, nchunks / ((long long)gridDim.x * (BS / 64) * 8)));
+#pragma unroll 1
+  while (true) {
+    // up to SUM_CK chunks per atomic: one counter word serialises ~10^6 single dequeues per launch
+    if (c == cend) next_chunks(&hdr[H_DEQUEUE2], nchunks, ck, c, cend);
+    const bool done = (long long)c >= nchunks;
+    int q = 0, s0 = 0, r = cur_r;
+    if (!done) {
+      const int2 ck2 = p.chunks[c];
+      q = __builtin_amdgcn_readfirstlane(ck2.x);
+      s0 = __builtin_amdgcn_readfirstlane(ck2.y);
+      r = __builtin_amdgcn_readfirstlane((int)p.all_r[q]);
+    }
+    const bool drain = done || r != cur_r;
+    // score full waves of queued candidates (all of them before a relation change / the exit)
+#pragma unroll 1
+    while (true) {
+      const int m = drain ? min(n, 64) : (n >= 64 ? 64 : 0);
+      if (m == 0) break;
+      wave_lds_sync();
+      sum_chunk_flush<DIGEST, COOP>(p, s_w, relb, s_stage[wv], queue, m, inv_scale, cur_r, cur_root, s_stage[wv]);
+      n -= m;
+      const int2 v = lane < n ? queue[m + lane] : make_int2(0, 0);
+      wave_lds_sync();
+      if (lane < n) queue[lane] = v;
+    }
+    if (done) break;
+    if (r != cur_r) {
+      wave_lds_sync();  // every lane is done with the previous relation's bias
+      relb[lane] = relation_bias(p, r, lane);
+      relb[lane + 64] = relation_bias(p, r, lane + 64);
+      cur_r = r;
+      cur_root = __builtin_amdgcn_readfirstlane(p.rl.head_root[r]);
+    }
+    const int nc = p.n_cand[q];
+    const int64_t qb = p.q_base[q];
+    const int s = s0 + lane;
+    bool queued = false;
+    if (s < nc) {
+      const int4 cr = p.cand[qb + s];
+      queued = true;
+      unsigned long long key = PAIR_NOKEY;
+      if (cr.z == 1) {
+        const int2 be = p.bent[cr.y];
+        if (be.y == 1 && p.memo) {  // one path of one leaf node: the memo
+          queued = false;
+          const float base = sum_base(p, q, cr.x);
+          if constexpr (DIGEST)
+            atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q),
+                      (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)p.rl.node_nrules[be.x] ^
+                                                                        mix64(p.rl.node_fp[be.x]))));
+          sum_write_out(p, q, cr.x, p.memo[be.x], base);
+        } else if (!DIGEST && p.ptab) {
+          key = pair_key(p, r, cur_root, 1, be, make_int2(0, 0), make_int2(0, 0));
+        }
+      } else if (!DIGEST && p.ptab && cr.z <= 3) {
+        key = pair_key(p, r, cur_root, cr.z, p.bent[cr.y], p.bent[cr.y + 1],
+                       cr.z == 3 ? p.bent[cr.y + 2] : make_int2(0, 0));
+      }
+      float out;
+      if (key != PAIR_NOKEY && pair_lookup(p, key, out)) {  // the pair memo holds these entries' output
+        queued = false;
+        sum_write_out(p, q, cr.x, out, sum_base(p, q, cr.x));
+      }
+    }
+    const uint64_t bal = __ballot(queued);
+    const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    wave_lds_sync();
+    if (queued) queue[pos] = make_int2(q, (int)(qb + s));
+    n += (int)__popcll(bal);  // < 128: the queue held < 64 before this chunk
+    ++c;
+  }
+}
+
+// ---------------------------------------------------------------- launch
+bool g_pair_memo = true;  // rnnl_debug_pair_memo (tests compare the outputs with the table off)
+
+// Packs the MLP weights behind the workspace header (layout W_* in fwd.h).
+__global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
+  const int kin = p.agg == RNNL_AGG_SUM ? 16 : 192;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < W_FLOATS; i += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (i < W_ADDB) {
+      if (i < 16 * kin) v = p.add_w[i];
+    } else if (i < W_LNW) {
+      v = p.add_b[i - W_ADDB];
+    } else if (i < W_LNB) {
+      v = p.ln_w[i - W_LNW];
+    } else if (i < W_S0X) {
+      v = p.ln_b[i - W_LNB];
+    } else if (i < W_S1W) {
+      const int k = i - W_S0X;
+      v = p.s0_w[(k / 16) * 32 + (k % 16)];
+    } else if (i < W_S1B) {
+      v = p.s1_w[i - W_S1W];
+    } else if (i == W_S1B) {
+      v = p.s1_b[0];
+    }
+    W[i] = v;
+  }
+}
+
+// The scoring pass after a grounding (K2): packs the weights, builds the
+// chunk list and launches the aggregator's chunk kernel.  `grid` caps its
+// persistent workgroups (0: the full grid); a smaller grid leaves CUs to a
+// concurrent kernel (RotatE).
+void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int grid) {
+  KParams p = p0;
+  const int nq = p.nq;
+  float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3((W_FLOATS + 255) / 256), dim3(256), 0, st, p, W);
+  launch_chunk_list(p, st);
+  if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);  // sums over chunks
+  const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * SCORE_WG_PER_CU);
+  if (p.agg != RNNL_AGG_SUM) {
+    hipLaunchKernelGGL(score_pna_chunk_kernel, dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+    return;
+  }
+  // the pair memo (not with the test digest, which needs every candidate's
+  // entries); a key needs >= 2 count bits per entry
+  const bool pair = !p.digest && g_pair_memo && p.pbc >= 2;
+  // few rows (e.g. one reference batch per call) with the pair memo on: no
+  // memo pass (one workgroup per relation, on the call's critical path); the
+  // single-path candidates take pair-memo keys instead — the same outputs
+  const bool small = nq <= MEMO_SCAN_ROWS;
+  if (small && pair)
+    p.memo = nullptr;
+  else
+    hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, (const float *)W);
+  if (pair) {
+    p.ptab = p.ptab_region;
+    (void)hipMemsetAsync(p.ptab, 0, 8ull << p.psbits, st);
+  }
+  // one reference batch per call: the wave-cooperative walk of long entry lists
+  // (bit-identical features); large launches keep the per-lane walk
+  if (p.digest && small)
+    hipLaunchKernelGGL((score_sum_chunk_kernel<true, true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+  else if (p.digest)
+    hipLaunchKernelGGL((score_sum_chunk_kernel<true, false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+  else if (small)
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+  else
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+}
+
+}  // namespace rnnl

@@ -68,9 +68,9 @@ class RotatE(torch.nn.Module):
         self._tables = None
         self._ws = None
         # DIRECT (default) evaluates the reference's arithmetic term by term;
-        # RNNL_ROTATE_MFMA=1 selects the faster expanded bf16x3 MFMA kernel
+        # mode = ROTATE_MFMA selects the faster expanded bf16x3 MFMA kernel
         # (cancellation-prone when h o r ~= t; include/rnnlogic_hip.h)
-        self.mode = _native.ROTATE_MFMA if os.environ.get("RNNL_ROTATE_MFMA") else _native.ROTATE_DIRECT
+        self.mode = _native.ROTATE_DIRECT
 
     def _device_tables(self):
         """Weight-derived tables (rotate.hip header), rebuilt when eemb/remb or

@@ -20,7 +20,6 @@ There is no CPU fallback: on a CPU tensor forward() raises.
 """
 import collections
 import ctypes
-import os
 import logging
 import math
 
@@ -32,10 +31,6 @@ from . import _native
 from .data import _DeviceHandle
 from .embedding import RotatE
 from .layers import MLP, FuncToNode, FuncToNodeSum
-
-
-# training-path LSTM input padded to one shape (RNNL_TRAIN_LSTM_PAD=0: per-relation shapes, for A/B)
-_PAD_TRAIN_LSTM = os.environ.get("RNNL_TRAIN_LSTM_PAD", "1") != "0"
 
 
 def _read_rules(input):
@@ -276,8 +271,8 @@ class Predictor(_HipGrounding, torch.nn.Module):
         self._ws_uses = {}  # per workspace pointer: launches onto it so far
         self._pf = {}  # per device: training lookahead (prefetch): side stream, workspace ring, queue
         # groundings launched ahead of the training step that needs them
-        # (TrainerPredictor.train; RNNL_PREFETCH=0 turns the lookahead off)
-        self.prefetch_depth = int(os.environ.get("RNNL_PREFETCH", "2"))
+        # (TrainerPredictor.train; 0 turns the lookahead off)
+        self.prefetch_depth = 2
         self.capacity_scale = 1
 
     def set_rules(self, input):
@@ -675,53 +670,25 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._side = {}
         self._ws_uses = {}
         self.capacity_scale = 1
-        # RotatE base score: the grounding runs on a side stream beside the
-        # RotatE kernel; rows may be split into chunks so that each chunk's
-        # scoring pass starts as soon as its RotatE rows are written (DESIGN.md
-        # "Stream overlap": 2 chunks measured 2-3 % faster than 1 but with an
-        # occasional one-step stall early in a process; 1 chunk is stable).
-        self.overlap_chunks = int(os.environ.get("RNNL_OVERLAP_CHUNKS", "1"))
-        self.overlap = os.environ.get("RNNL_OVERLAP", "1") != "0"
-        # persistent workgroups of the side-stream kernels (0 = full occupancy):
-        # fewer leave RotatE its waves (it needs ~6 per SIMD to reach its
-        # floor).  The grounding beside RotatE runs one workgroup per CU
-        # (measured 88.1 vs 91.1 ms/step at full occupancy): it finishes in
-        # ~18 ms, well inside the RotatE launch.
-        # The scoring pass beside RotatE runs 256 workgroups (1 per CU): FB15k-237
-        # 83.4-84.0 ms/step for 256-1024 vs 84.4-84.6 at full occupancy in round 2;
-        # round 3 (pair memo, atomic adds): 256 / 512 / 768 -> 80.6-80.8 /
-        # 81.25-81.27 / 81.1-81.7 ms, WN18RR 256 / 512 -> 20.05 / 20.17 ms; on
-        # another box 128 / 192 / 256 -> 80.9 / 80.9-81.3 / 81.1-81.7 ms (the
-        # box-to-box spread is ~0.5 ms; 128-256 are within it)
-        # (tools/env_ab.sh, RNNL_OVERLAP_SCORE_WG).
-        self.overlap_ground_wg = int(os.environ.get("RNNL_OVERLAP_GROUND_WG", "256"))
-        self.overlap_score_wg = int(os.environ.get("RNNL_OVERLAP_SCORE_WG", "256"))
-        # sum aggregator: the scoring pass also runs beside RotatE, writing its
-        # per-candidate outputs to the workspace; a short apply pass adds them
-        # into the finished RotatE rows (rnnl_predictorplus_apply)
-        self.overlap_deferred = os.environ.get("RNNL_OVERLAP_DEFERRED", "1") != "0"
-        # ... or, without the apply pass (default): the score rows are zeroed on
-        # side stream B beside the rule encoder, and RotatE and the deferred
-        # scoring pass both add into them atomically — fl(rotate + out) in either
-        # order, bit-identical (RNNL_OVERLAP_ATOMIC=0: the apply pass)
-        self.overlap_atomic = os.environ.get("RNNL_OVERLAP_ATOMIC", "1") != "0"
-        # with several chunks, chunk k's deferred scoring on side stream B
-        # beside chunk k + 1's grounding on A (RNNL_OVERLAP_PIPELINE=1)
-        self.overlap_pipeline = os.environ.get("RNNL_OVERLAP_PIPELINE", "0") == "1"
-        # below this many rows the forward runs on one stream (bit-identical);
-        # 0: overlap from 2 rows on (one 32-row reference batch per call: 0.78
-        # ms overlapped vs 1.02 ms on one stream, the grounding's latency then
-        # hiding behind RotatE)
-        self.overlap_min_rows = int(os.environ.get("RNNL_OVERLAP_MIN_ROWS", "0"))
+        # RotatE base score (_forward_overlap): the grounding and the scoring
+        # pass run on a side stream beside the RotatE kernel, both adding into
+        # rows zeroed beside the rule encoder
+        self.overlap = True
+        # persistent workgroups of the side-stream kernels: one per CU leaves
+        # RotatE its waves (it needs ~6 per SIMD to reach its floor); the
+        # grounding then takes ~18 ms, well inside the RotatE launch
+        # (measured 88.1 vs 91.1 ms/step at full occupancy), and the scoring
+        # pass 256 vs 512 / 768 workgroups 80.6-80.8 vs 81.25 / 81.1-81.7 ms
+        self.overlap_ground_wg = 256
+        self.overlap_score_wg = 256
         # pna aggregator: RotatE in two launches, the first over half its grid
         # (rnnl_rotate_score_pieces; bitwise the same scores).  The PNA scoring
-        # pass needs 168 VGPRs per wave and finds no room beside RotatE's waves
+        # pass needs 168+ VGPRs per wave and finds no room beside RotatE's waves
         # (6 x 76 per SIMD) until a launch boundary drains them: WN18RR step
-        # 21.0-21.1 -> 20.0-20.2 ms with the boundary at 0.4-0.6 of the grid
-        # (0.3: before the grounding ends, no gain).  The sum pass (64 VGPRs)
-        # fits beside RotatE; there the boundary only costs its drain
-        # (FB15k-237 81.2 -> 81.5 ms).  RNNL_ROT_YIELD=0 turns it off.
-        self.rotate_yield = os.environ.get("RNNL_ROT_YIELD", "1") != "0"
+        # 21.0-21.1 -> 20.0-20.2 ms with the boundary at 0.4-0.6 of the grid.
+        # The sum pass (64 VGPRs) fits beside RotatE; there the boundary only
+        # costs its drain (FB15k-237 81.2 -> 81.5 ms).
+        self.rotate_yield = True
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -899,11 +866,9 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             if events is not None else (lambda k: None)
         rec("start")
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
-        overlap = self.entity_feature == "RotatE" and self.overlap and nq >= max(2 * self.overlap_chunks,
-                                                                                  self.overlap_min_rows)
-        # atomic deferred overlap: zero the rows on side stream B beside the rule encoder
-        zero_ev = self._zero_rows(device, score) if overlap and self.overlap_deferred and self.overlap_atomic \
-            else None
+        overlap = self.entity_feature == "RotatE" and self.overlap and nq >= 2
+        # zero the rows on the side stream beside the rule encoder
+        zero_ev = self._zero_rows(device, score) if overlap else None
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -941,143 +906,94 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
-    def _chunk_workspace(self, device, k, nq, scale):
+    def _overlap_workspace(self, device, nq, scale):
         need = ctypes.c_size_t()
         _native.call("rnnl_forward_workspace_size", self.graph.device_graph(device), self.native_rules(device).ptr,
                      nq, scale, ctypes.byref(need))
-        key = (self._device_index(device), k)
+        key = self._device_index(device)
         ws = self._ws_chunks.get(key)
         if ws is None or ws.numel() < need.value:
             ws = torch.empty(need.value, dtype=torch.uint8, device=device)
             self._ws_chunks[key] = ws
         return ws
 
-    def _overlap_events(self, device, K):
-        """K (grounding, RotatE) event pairs, created once and re-recorded each
-        call (creating HIP events per call is not free)."""
-        key = (self._device_index(device), "ev")
-        evs = self._side.get(key)
-        if evs is None or len(evs[0]) < K:
-            evs = tuple([torch.cuda.Event() for _ in range(K)] for _ in range(3))
-            self._side[key] = evs
-        return evs
-
     def _side_streams(self, device):
+        """(A, B): A carries the grounding and the scoring pass, B the zero
+        fill of the score rows (beside the rule encoder)."""
         key = self._device_index(device)
         if key not in self._side:
-            # RNNL_SIDE_PRIORITY=-1: the side streams on a high-priority queue
-            # (their workgroups dispatched first as RotatE's retire; A/B)
-            prio = int(os.environ.get("RNNL_SIDE_PRIORITY", "0"))
-            self._side[key] = (torch.cuda.Stream(device, priority=prio), torch.cuda.Stream(device, priority=prio))
+            self._side[key] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
         return self._side[key]
 
     def _zero_rows(self, device, score):
         """score.zero_() on side stream B (ordered after the current stream's
         work so far); returns the event that marks it done."""
         main = torch.cuda.current_stream(device)
-        side_s = self._side_streams(device)[1]
+        side = self._side_streams(device)[1]
         key = (self._device_index(device), "zev")
         ev = self._side.get(key)
         if ev is None:
             ev = self._side[key] = torch.cuda.Event()
-        side_s.wait_stream(main)
-        with torch.cuda.stream(side_s):
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
             score.zero_()
-        ev.record(side_s)
+        ev.record(side)
         return ev
 
-    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec, zero_ev=None):
-        """RotatE entity feature: the same kernels as the one-stream path, in
-        row chunks over three streams — RotatE rows on the current stream,
-        the grounding of every chunk on side stream A (it does not read the
-        base score, and it is latency-bound where RotatE is VALU-bound), and
-        each chunk's scoring pass on side stream B once both its grounding and
-        its RotatE rows are done.  Results are bit-identical to the
-        one-stream path (same kernels, same inputs per row).  Returns the
-        (all-True) mask, filled on the current stream behind RotatE."""
+    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec, zero_ev):
+        """RotatE entity feature: the one-stream path's kernels on three
+        streams.  The grounding and then the scoring pass run on side stream A
+        beside RotatE on the current stream (the grounding does not read the
+        base score; it is latency-bound where RotatE is VALU-bound), and are
+        enqueued before RotatE so that their persistent workgroups are
+        resident before RotatE's blocks fill the chip.  The score rows were
+        zeroed on side stream B, and RotatE and the scoring pass both
+        add into them atomically (rnnl_rotate_score accumulate = 2,
+        rnnl_predictorplus_score deferred = 2): two addends on an exact zero
+        round to fl(rotate + out) in either order, so the rows are the
+        one-stream path's bit for bit.  Returns the (all-True) mask, filled on
+        the current stream behind RotatE."""
         main = torch.cuda.current_stream(device)
-        side_g, side_s = self._side_streams(device)
+        side = self._side_streams(device)[0]
         nq = all_h.numel()
-        K = self.overlap_chunks
-        bounds = [nq * k // K for k in range(K + 1)]
         agg = params.aggregator
-        deferred = self.overlap_deferred
-        atomic = deferred and zero_ev is not None  # RotatE and scoring add into zeroed rows: no apply pass
         first = True
         while True:
-            if atomic and not first:  # a retried launch starts from zeroed rows again
+            if not first:  # a retried launch starts from zeroed rows again
                 score.zero_()
                 zero_ev.record(main)
             first = False
             scale = self.capacity_scale
-            wss = [self._chunk_workspace(device, k, bounds[k + 1] - bounds[k], scale) for k in range(K)]
-            side_g.wait_stream(main)  # inputs, node aggregates, workspaces
-            side_s.wait_stream(main)
+            ws = self._overlap_workspace(device, nq, scale)
+            side.wait_stream(main)  # inputs, node aggregates, workspace
             rec("base")
-            ev_g, ev_r, ev_s = self._overlap_events(device, K)
-            pipeline = deferred and self.overlap_pipeline and K > 1
-            for k in range(K):
-                lo, hi = bounds[k], bounds[k + 1]
-                _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h[lo:].data_ptr(),
-                             all_r[lo:].data_ptr(), etr[lo:].data_ptr() if etr is not None else None, hi - lo,
-                             n_cand[lo:].data_ptr(), wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_ground_wg,
-                             side_g.cuda_stream)
-                if deferred and pipeline:
-                    # chunk k's scoring on side stream B, beside chunk k + 1's grounding
-                    ev_g[k].record(side_g)
-                    side_s.wait_event(ev_g[k])
-                if deferred:  # the score pass does not read `score`: it runs beside RotatE too
-                    ss = side_s if pipeline else side_g
-                    if atomic:
-                        ss.wait_event(zero_ev)
-                    _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
-                                 all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None,
-                                 n_cand[lo:].data_ptr(), digest[lo:].data_ptr() if digest is not None else None,
-                                 wss[k].data_ptr(), wss[k].numel(), scale, self.overlap_score_wg, 2 if atomic else 1,
-                                 ss.cuda_stream)
-                    if pipeline:
-                        ev_s[k].record(side_s)
-                if not pipeline:
-                    ev_g[k].record(side_g)
-            if atomic:
-                main.wait_event(zero_ev)
-            pieces = 2 if self.rotate_yield and agg == _native.AGG_PNA and deferred and K == 1 else 1
-            for k in range(K):
-                lo, hi = bounds[k], bounds[k + 1]
-                self.RotatE.score_into(all_h[lo:hi], all_r[lo:hi], score[lo:hi], accumulate=2 if atomic else 0,
-                                       pieces=pieces, first_share=0.5 if pieces > 1 else 0.0)
-                ev_r[k].record(main)
-            # the all-True mask (RotatE feature) is filled behind RotatE, beside the side streams' work
+            _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h.data_ptr(), all_r.data_ptr(),
+                         etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
+                         ws.numel(), scale, self.overlap_ground_wg, side.cuda_stream)
+            side.wait_event(zero_ev)
+            _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
+                         all_r.data_ptr(), nq, score.data_ptr(), None, n_cand.data_ptr(),
+                         digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
+                         self.overlap_score_wg, 2, side.cuda_stream)
+            main.wait_event(zero_ev)
+            pieces = 2 if self.rotate_yield and agg == _native.AGG_PNA else 1
+            self.RotatE.score_into(all_h, all_r, score, accumulate=2, pieces=pieces,
+                                   first_share=0.5 if pieces > 1 else 0.0)
+            # the all-True mask (RotatE feature) is filled behind RotatE, beside the side stream's work
             mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
             rec("ground")
-            for k in range(K if deferred and not atomic else 0):
-                lo, hi = bounds[k], bounds[k + 1]
-                main.wait_event(ev_s[k] if pipeline else ev_g[k])
-                _native.call("rnnl_predictorplus_apply", wss[k].data_ptr(), hi - lo, scale, n_cand[lo:].data_ptr(),
-                             params.feature, score[lo:].data_ptr(), None, self.num_entities, main.cuda_stream)
-            for k in range(0 if deferred else K):
-                lo, hi = bounds[k], bounds[k + 1]
-                side_s.wait_event(ev_g[k])
-                side_s.wait_event(ev_r[k])
-                _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h[lo:].data_ptr(),
-                             all_r[lo:].data_ptr(), hi - lo, score[lo:].data_ptr(), None, n_cand[lo:].data_ptr(),
-                             digest[lo:].data_ptr() if digest is not None else None, wss[k].data_ptr(),
-                             wss[k].numel(), scale, self.overlap_score_wg, 0, side_s.cuda_stream)
-            main.wait_stream(side_s)
-            main.wait_stream(side_g)
+            main.wait_stream(side)
             rec("end")
             # the host waits for the result anyway: drain the side streams too,
             # so no cross-stream wait is left pending into the next call
-            side_g.synchronize()
-            side_s.synchronize()
-            rcs = [_native.lib().rnnl_forward_status(ws.data_ptr(), main.cuda_stream) for ws in wss]
-            bad = [rc for rc in rcs if rc != _native.RNNL_OK]
-            if bad and all(rc == _native.RNNL_ERR_OVERFLOW for rc in bad) and self.capacity_scale < 64:
+            side.synchronize()
+            self._side_streams(device)[1].synchronize()
+            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), main.cuda_stream)
+            if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
                 logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
                 continue
-            for rc in bad:
-                _native.check(rc)
+            _native.check(rc)
             return mask
 
     # ------------------------------------------------------------------ autograd (training) path
@@ -1206,8 +1122,6 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         rows = max(self._max_rules_per_relation, 1)
         if n > rows:
             rows = (n + 511) // 512 * 512
-        if not _PAD_TRAIN_LSTM:  # A/B: one LSTM shape per relation
-            rows = n
         if rows > n:
             ridx = torch.cat([ridx, ridx.new_zeros(rows - n)])
         return self.encode_rules(tok.index_select(0, ridx))[:n]

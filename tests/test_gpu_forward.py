@@ -136,25 +136,25 @@ def test_full_test_split_digests(case, dev):
 
 @pytest.mark.parametrize("case", ["umls_emb_pna_rotate", "fb_lstm_sum_rotate"])
 def test_stream_overlap_is_bit_identical(case, dev):
-    """RotatE forwards overlap the grounding (side stream) with the RotatE
-    chunks: every chunking gives bit-identical scores, candidate counts and
-    path-count digests to the one-stream launch, on all test rows of the
-    graph at once (mixed relations, many reference batches)."""
+    """RotatE forwards overlap the grounding and the scoring pass (side
+    stream, atomic adds into zeroed rows) with RotatE: bit-identical scores,
+    candidate counts and path-count digests to the one-stream launch, on all
+    test rows of the graph at once (mixed relations, many reference
+    batches)."""
     fx = Fixture(case)
     model = build_model(fx, dev)
     test = np.asarray(graph_for(fx.dataset_path()).test_facts, dtype=np.int64)[:6000]
     h = torch.from_numpy(test[:, 0]).to(dev)
     r = torch.from_numpy(test[:, 1]).to(dev)
     outs = []
-    for chunks in (0, 1, 4, 7):  # 0: one stream, no overlap
-        model.overlap = chunks > 0
-        model.overlap_chunks = max(chunks, 1)
+    for overlap in (False, True):
+        model.overlap = overlap
         dig = torch.zeros(len(h), dtype=torch.int64, device=dev)
         with torch.no_grad():
             score, mask, n = model.forward_rows(h, r, None, return_ncand=True, digest=dig)
         torch.cuda.synchronize()
         outs.append((score.cpu().numpy(), mask.cpu().numpy(), n.cpu().numpy(), dig.cpu().numpy()))
-    model.overlap, model.overlap_chunks = True, 1
+    model.overlap = True
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             np.testing.assert_array_equal(a, b)
@@ -166,7 +166,7 @@ def test_stream_overlap_is_bit_identical(case, dev):
 
 @pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "fb_lstm_sum_rotate", "kinship_lstm_sum_none",
                                   "umls_lstm_sum_bias"])
-def test_pair_memo_is_bit_identical(case, dev, monkeypatch):
+def test_pair_memo_is_bit_identical(case, dev):
     """The SUM pair memo (score_model outputs keyed by a candidate's one or
     two bucket entries, ground.hip pair_key) reuses outputs of equal features:
     scores, masks and candidate counts equal the launch without it, one stream
@@ -176,14 +176,18 @@ def test_pair_memo_is_bit_identical(case, dev, monkeypatch):
     test = np.asarray(graph_for(fx.dataset_path()).test_facts, dtype=np.int64)[:8000]
     h = torch.from_numpy(test[:, 0]).to(dev)
     r = torch.from_numpy(test[:, 1]).to(dev)
+    from rnnlogic_amd import _native
     outs = []
-    for on, overlap in (("0", False), ("1", False), ("1", True)):
-        monkeypatch.setenv("RNNL_SCORE_PAIRMEMO", on)
-        model.overlap = overlap
-        with torch.no_grad():
-            out = model.forward_rows(h, r, None, return_ncand=True)
-        torch.cuda.synchronize()
-        outs.append([x.cpu().numpy() for x in out])
+    try:
+        for on, overlap in ((0, False), (1, False), (1, True)):
+            _native.call("rnnl_debug_pair_memo", on)
+            model.overlap = overlap
+            with torch.no_grad():
+                out = model.forward_rows(h, r, None, return_ncand=True)
+            torch.cuda.synchronize()
+            outs.append([x.cpu().numpy() for x in out])
+    finally:
+        _native.call("rnnl_debug_pair_memo", 1)
     model.overlap = True
     for o in outs[1:]:
         for a, b in zip(outs[0], o):

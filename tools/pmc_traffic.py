@@ -4,8 +4,13 @@ MI355X_MICROARCH.md §HBM prescribes (gfx950 FETCH_SIZE counts half of a
 coalesced read stream: doubled; WRITE_SIZE exact; both in KiB).  Writes
 profiles/<name>.json, which bench.py reads for roofline.traffic.
 
-Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json "workload string"
+Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json "workload string" [COMMIT]
+
+The summary is stamped with the sha256 of the kernel sources it was captured
+with (bench.csrc_fingerprint) and the commit id given (the GPU box has no
+git); bench.py reports a summary's traffic only while the stamp matches.
 """
+import os
 import collections
 import csv
 import glob
@@ -29,7 +34,11 @@ def per_kernel(root, counter):
 
 fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
 write = per_kernel(sys.argv[2], "WRITE_SIZE")
-res = {"workload": sys.argv[4],
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import csrc_fingerprint  # noqa: E402
+
+res = {"workload": sys.argv[4], "commit": sys.argv[5] if len(sys.argv) > 5 else "?",
+       "csrc_sha256": csrc_fingerprint(),
        "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes); bytes = 2 x FETCH_SIZE KiB "
                  "(gfx950 counts half of a coalesced read stream) + WRITE_SIZE KiB, per launch (mean over launches)",
        "kernels": {}}

@@ -23,3 +23,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/bfetch 
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/bwrite -o run -- \
     python3 bench.py --feature bias --steps 3 --warmup 1 --profile-only > /dev/null 2> $o/bwrite.err || { tail -5 $o/bwrite.err; exit 1; }
 cat $o/bias.json
+# per-kernel traffic summaries, stamped with the kernel sources (bench.py checks the stamp)
+python3 tools/pmc_traffic.py $o/fetch $o/write $o/traffic_rotate.json "FB15k-237 RotatE bench step (bench.py --profile-only, $tag)" "${COMMIT:-?}" > /dev/null
+python3 tools/pmc_traffic.py $o/bfetch $o/bwrite $o/traffic_bias.json "FB15k-237 bias-feature bench step: grounding + scoring in one launch (bench.py --feature bias --profile-only, $tag)" "${COMMIT:-?}" > /dev/null
+rm -rf $o/fetch $o/write $o/bfetch $o/bwrite
