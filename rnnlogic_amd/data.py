@@ -217,15 +217,17 @@ class _DeviceLists(object):
 
 class _RowTable(object):
     """A dataset's batches as one (n, 3) int64 (h, r, t) table on the device
-    with per-batch offsets, uploaded once and rebuilt when the batch list
-    changes: another list object (make_batches builds a new one) or another
-    length, or a batch object replaced or moved inside it — checked at 17
-    evenly spaced positions per call (an in-place reshuffle moves nearly every
-    batch; checking all 17,258 FB15k-237 train batches per training step cost
-    ~1 ms).  The table keeps references to the list and the batches it was
-    built from, so a recycled id cannot alias.  A single batch is then a slice
-    of the table (no host->device copy per step) and many batches one
-    gather."""
+    with per-batch offsets, uploaded once.  It is rebuilt when the batch list
+    is another object (make_batches() builds a new list) or has another
+    length, and — as a cheap guard against a reshuffle in place, which moves
+    nearly every batch — when a batch object differs at one of 17 evenly
+    spaced positions (checking all 17,258 FB15k-237 train batches per
+    training step cost ~1 ms).  Editing the list in place otherwise (one
+    batch replaced at an unchecked position) is NOT supported: assign a new
+    list, or call make_batches().  The table keeps references to the list and
+    the batches it was built from, so a recycled id cannot alias.  A single
+    batch is then a slice of the table (no host->device copy per step) and
+    many batches one gather."""
 
     def __init__(self, device):
         self.device = device

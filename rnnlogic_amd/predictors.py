@@ -273,6 +273,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         # groundings launched ahead of the training step that needs them
         # (TrainerPredictor.train; 0 turns the lookahead off)
         self.prefetch_depth = 2
+        self.prefetch_dropped = 0  # queued groundings discarded (rows not the queue's head)
         self.capacity_scale = 1
 
     def set_rules(self, input):
@@ -385,13 +386,20 @@ class Predictor(_HipGrounding, torch.nn.Module):
     def check_deferred(self):
         """Raise the scoring pass's own error (an integer range flag) of the
         last lookahead forward, whose status is read one step late so the
-        host does not wait for the scoring each step."""
+        host does not wait for the scoring each step.  The training step of
+        that forward has then already run its backward and optimizer step on
+        the flagged scores: the error names it, and a run resumed from a
+        checkpoint written after that step should not trust it."""
         d = getattr(self, "_deferred_status", None)
         if d is None:
             return
         self._deferred_status = None
         d[1].synchronize()
-        _native.check(_native.lib().rnnl_forward_status_host(d[0].data_ptr(), None))
+        rc = _native.lib().rnnl_forward_status_host(d[0].data_ptr(), None)
+        if rc != _native.RNNL_OK:
+            raise _native.NativeError(rc, "%s (scoring pass of lookahead forward #%d, read one step late: that "
+                                          "step's backward and optimizer update have already been applied)" % (
+                                              _native.lib().rnnl_last_error().decode(errors="replace"), d[2]))
 
     def _prefetched(self, device, all_h, all_r, edges_to_remove):
         """The queued grounding of exactly these row tensors, or None (a
@@ -402,6 +410,11 @@ class Predictor(_HipGrounding, torch.nn.Module):
         e = pf["queue"][0]
         if e[0] is all_h and e[1] is all_r and e[2] is edges_to_remove and e[4] == self.capacity_scale:
             return pf["queue"].popleft()
+        # other row tensors than the queue's head (e.g. a wrapper copied the
+        # inputs): the lookahead is lost — counted, so a profile can show it
+        self.prefetch_dropped += len(pf["queue"])
+        logging.debug("Predictor: lookahead queue dropped (%d groundings; %d so far)", len(pf["queue"]),
+                      self.prefetch_dropped)
         pf["queue"].clear()
         return None
 
@@ -468,7 +481,8 @@ class Predictor(_HipGrounding, torch.nn.Module):
                 dh.copy_(ws[:hb], non_blocking=True)
                 dev_ev = torch.cuda.Event()
                 dev_ev.record(main)
-                self._deferred_status = (dh, dev_ev)
+                self._lookahead_forwards = getattr(self, "_lookahead_forwards", 0) + 1
+                self._deferred_status = (dh, dev_ev, self._lookahead_forwards)
                 n_cand = n_cand_pf
             else:  # overflow (or another failure): the one-call path, with its retry
                 pre = None

@@ -282,8 +282,12 @@ def test_predictor_train_lookahead_is_bit_identical(overflow):
     """TrainerPredictor.train grounds the next batches ahead on a side stream
     (Predictor.prefetch, rnnl_predictor_ground / rnnl_predictor_score): the
     trained weights and the logged losses equal those of the one-call forward
-    (prefetch_depth 0) bit for bit — also when lowered workspace capacities
-    make prefetched groundings overflow and fall back to the retried path."""
+    (prefetch_depth 0) — also when lowered workspace capacities make
+    prefetched groundings overflow and fall back to the retried path.  The
+    weights are held to a tight tolerance, not bitwise: the backward
+    (predictor_backward_kernel) sums each node's count x gradient with fp64
+    atomics, whose order may differ between two runs, so a node's gradient
+    can differ in its last fp64 bits and, rarely, its fp32 rounding."""
     import io
     import logging
     import random
@@ -341,4 +345,4 @@ def test_predictor_train_lookahead_is_bit_identical(overflow):
     if overflow:
         assert s0 > 1 and s1 > 1, (s0, s1)
     for k in w0:
-        assert torch.equal(w0[k], w1[k]), k
+        torch.testing.assert_close(w0[k], w1[k], rtol=1e-6, atol=1e-8, msg=k)
