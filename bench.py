@@ -84,6 +84,57 @@ def shard_rows(test_set, world, rank):
     return rows, idx
 
 
+def shard_balance_line(model, test_set, dev, full_ms, worlds=(2, 4, 8), reps=3):
+    """Prediction of the N-GPU load balance on one GPU (no scaling claim):
+    each DistributedSampler(test_set, N, k) shard (the rows rank k of an
+    N-GPU bench runs, sampler padding included) timed alone on cuda:0 with
+    the same step as `value` (rule aggregates recomputed, RotatE + grounding +
+    scoring).  The N-GPU step is the slowest shard (ranks are independent
+    until the closing barrier), so the implied strong-scaling efficiency is
+    T_1 / (N x max_k T_k); the shards' RotatE and grounding times show which
+    one sets it.  Plus the DDP gradient size of the headline model's training
+    step (every trainable parameter is all-reduced each step)."""
+    out = {}
+    for world in worlds:
+        shard_ms, shard_rows_n, rot_ms, ground_ms = [], [], [], []
+        for k in range(world):
+            rows, _ = shard_rows(test_set, world, k)
+            sh = torch.from_numpy(np.ascontiguousarray(rows[:, 0])).to(dev)
+            sr = torch.from_numpy(np.ascontiguousarray(rows[:, 1])).to(dev)
+
+            def st(ev=None):
+                model.invalidate_cache()
+                with torch.no_grad():
+                    return model.forward_rows(sh, sr, None, events=ev)
+            shard_ms.append(time_forward(st, reps) * 1e3)
+            ev = {}
+            st(ev)
+            torch.cuda.synchronize(dev)
+            rot_ms.append(ev["base"].elapsed_time(ev["ground"]))
+            ground_ms.append(isolated_ground_ms(model, model.graph, sh, sr, dev))
+            shard_rows_n.append(len(rows))
+            del sh, sr
+        mx, mean = max(shard_ms), float(np.mean(shard_ms))
+        slow = int(np.argmax(shard_ms))
+        out["N=%d" % world] = {
+            "shard_ms": [round(x, 3) for x in shard_ms], "shard_rows": shard_rows_n,
+            "rotate_ms": [round(x, 3) for x in rot_ms], "ground_score_alone_ms": [round(x, 3) for x in ground_ms],
+            "max_ms": round(mx, 3), "mean_ms": round(mean, 3), "balance_mean_over_max": round(mean / mx, 4),
+            "implied_strong_efficiency": round(full_ms / (world * mx), 4),
+            "slowest_shard": slow,
+            "slowest_grounding_outlasts_rotate": bool(ground_ms[slow] > rot_ms[slow])}
+    n_grad = sum(p.numel() for p in model.parameters())
+    out["ddp_gradient"] = {
+        "parameters": int(n_grad), "bytes_per_step": int(4 * n_grad),
+        "rotate_share": round(float(model.RotatE.eemb.numel() + model.RotatE.remb.numel()) / n_grad, 4)
+        if hasattr(model, "RotatE") else 0.0,
+        "note": "fp32 gradients all-reduced by DDP each training step (trainer.py:56-60; every parameter, "
+                "find_unused_parameters=True); not measured here (no multi-GPU run from this box)"}
+    out["note"] = ("each DistributedSampler shard timed alone on one GPU (the N-GPU step is the slowest shard); "
+                   "T_1 = the full split's step on the same GPU; prediction only, not a scaling measurement")
+    return out
+
+
 def train_rows(train_set, n_rows):
     """The first train batches (sampler order of trainer.py:51-56 is a
     permutation; batch order does not matter for throughput) up to n_rows:
@@ -695,6 +746,8 @@ def main():
                                            measured="the timed forward_rows (node weights + fill + ground + score)"),
             "note": "Predictor(bias) over the test split, same rules (same grounding work as value)"}
         del pred
+        if args.feature == "RotatE":
+            extra["shard_balance"] = shard_balance_line(model, test_set, dev, elapsed / args.steps * 1e3)
         extra["wn18rr_forward"] = wn18rr_line(dev)
         extra["kinship_forward"] = kinship_line(dev)
         # end-to-end evaluate('test') (trainer.py:145-248): device rows + filter

@@ -138,7 +138,14 @@ typedef struct {
   const float *rel_emb;    /* relation_emb.weight (R x 16) */
   const float *base_row;   /* nullable: the base score every row starts from (the bias vector, E floats);
                               candidates are then written as out + base_row[t] without reading score */
+  const float *packed;     /* nullable: the weights above already packed by rnnl_pack_weights (kept by
+                              the caller while they do not change); NULL: packed per launch */
 } rnnl_predictor_params;
+/* Packs the score_model / rule_to_entity weights of p (rnnl_pack_weights_floats
+ * floats) for the scoring kernels, so that repeated launches with the same
+ * weights (one reference batch per call) skip the packing launch. */
+int rnnl_pack_weights_floats(size_t *n_floats);
+int rnnl_pack_weights(const rnnl_predictor_params *p, float *out, void *stream);
 
 /* Workspace bytes for one launch of rnnl_predictorplus_forward (host). */
 int rnnl_forward_workspace_size(rnnl_graph g, rnnl_rules r, int32_t n_queries, int32_t capacity_scale,
@@ -390,6 +397,24 @@ int rnnl_miner_create(const int32_t *hrt, int64_t n_triples, int32_t n_entities,
 int rnnl_miner_destroy(rnnl_miner m);
 int rnnl_rule_search(rnnl_miner m, int32_t max_length, uint64_t *table, int64_t table_cap, uint64_t *rules_out,
                      int64_t out_cap, uint64_t *counters, void *stream);
+
+/* ------------------------------------------------------- training loss --
+ * TrainerPredictor.train's loss (reference src/trainer.py:84-90) for a model
+ * whose mask is all True (bias / RotatE features): with
+ * target' = target * smoothing + one_hot(all_t) * (1 - smoothing),
+ * loss = -sum log(softmax(logits) + 1e-8) * target' / max(sum target', 1)
+ * over the (B, E) rows.  loss: 2 floats (the loss, then the clamped target
+ * sum the backward needs).  aux: rnnl_nll_aux_bytes(B) bytes of per-row
+ * statistics, kept for the backward.  counter: one uint32 that is zero
+ * between launches (the kernel resets it; zero it once, and use it for one
+ * launch at a time).  rnnl_nll_backward writes d loss / d logits * grad_out
+ * into grad (B, E). */
+int rnnl_nll_aux_bytes(int32_t B, size_t *bytes);
+int rnnl_nll_forward(const float *logits, const float *target, const int64_t *all_t, int32_t B, int32_t E,
+                     float smoothing, uint32_t *counter, void *aux, float *loss, void *stream);
+int rnnl_nll_backward(const float *logits, const float *target, const int64_t *all_t, int32_t B, int32_t E,
+                      float smoothing, const void *aux, const float *loss, const float *grad_out, float *grad,
+                      void *stream);
 
 #ifdef __cplusplus
 }

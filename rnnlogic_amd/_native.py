@@ -83,6 +83,11 @@ SIGNATURES = [
     ("rnnl_rotate_score_pieces", ctypes.c_int,
      [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _I32, _P, ctypes.c_size_t, _I32, _F32, _P]),
     ("rnnl_rotate_backward", ctypes.c_int, [_P, _I32, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    ("rnnl_pack_weights_floats", ctypes.c_int, [_P]),
+    ("rnnl_pack_weights", ctypes.c_int, [_P, _P, _P]),
+    ("rnnl_nll_aux_bytes", ctypes.c_int, [_I32, _P]),
+    ("rnnl_nll_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _F32, _P, _P, _P, _P]),
+    ("rnnl_nll_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _F32, _P, _P, _P, _P, _P]),
 ]
 
 
@@ -90,7 +95,7 @@ class PredictorParams(ctypes.Structure):
     """rnnl_predictor_params (include/rnnlogic_hip.h)."""
     _fields_ = [("aggregator", _I32), ("feature", _I32), ("node_w", _P), ("add_w", _P), ("add_b", _P),
                 ("ln_w", _P), ("ln_b", _P), ("s0_w", _P), ("s0_b", _P), ("s1_w", _P), ("s1_b", _P),
-                ("rel_emb", _P), ("base_row", _P)]
+                ("rel_emb", _P), ("base_row", _P), ("packed", _P)]
 
 
 class NativeError(RuntimeError):
@@ -119,7 +124,12 @@ def lib():
                                "(or __graft_entry__.build())" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
-            f = getattr(L, name)
+            # (a diagnostic build selected with RNNL_LIB may lack newer entry
+            # points: those raise when called; tests/test_host.py checks that
+            # the shipped library exports every symbol of the header)
+            f = getattr(L, name, None)
+            if f is None:
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L

@@ -75,6 +75,7 @@ struct KParams {
   const unsigned char *node_w;
   const float *add_w, *add_b, *ln_w, *ln_b, *s0_w, *s0_b, *s1_w, *s1_b, *rel_emb;
   const float *base_row;  // nullable: every row's base score (bias), read instead of score[q][t]
+  const float *packed;    // nullable: the weights packed by rnnl_pack_weights (else packed per launch)
   const int64_t *all_h, *all_r, *etr;
   int32_t nq;
   int32_t ebits;     // entity bits of the packed (trie node, entity) keys

@@ -684,9 +684,10 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
   __shared__ int s_ws[CHB / 64];
   __shared__ long long s_pb[CHB / 64], s_pt[CHB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // this block's prefix and the list total from the per-block totals
+  // this block's prefix and the list total from the per-block totals (one
+  // block, bsum == nullptr: the total is this block's own sum, below)
   long long pb = 0, pt = 0;
-  for (int k = tid; k < (int)gridDim.x; k += CHB) {
+  for (int k = tid; bsum && k < (int)gridDim.x; k += CHB) {
     const int v = bsum[k];
     pt += v;
     if (k < (int)blockIdx.x) pb += v;
@@ -723,6 +724,7 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
       total += s_pt[w];
     }
     s_pb[0] = base;
+    if (!bsum) total = acc;
     if (blockIdx.x == 0)
       *reinterpret_cast<unsigned long long *>(reinterpret_cast<unsigned int *>(p.ws) + H_CHUNKS) = total;
   }
@@ -733,6 +735,10 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
 
 void launch_chunk_list(const KParams &p, hipStream_t st) {
   const unsigned nb = (unsigned)((p.nq + CHB - 1) / CHB);
+  if (nb == 1) {  // one block (<= 256 rows, e.g. a reference batch per call): one launch
+    hipLaunchKernelGGL(chunk_fill_kernel, dim3(1), dim3(CHB), 0, st, p, (const int *)nullptr);
+    return;
+  }
   int *bsum = reinterpret_cast<int *>(p.chunks + p.chunk_cap);  // nb ints after the list (layout)
   hipLaunchKernelGGL(chunk_sum_kernel, dim3(nb), dim3(CHB), 0, st, p, bsum);
   hipLaunchKernelGGL(chunk_fill_kernel, dim3(nb), dim3(CHB), 0, st, p, (const int *)bsum);
@@ -975,6 +981,7 @@ void set_score_params(KParams &p, const rnnl_predictor_params *pp, float *score,
   p.s1_b = pp->s1_b;
   p.rel_emb = pp->rel_emb;
   p.base_row = pp->base_row;
+  p.packed = pp->packed;
   p.score = score;
   p.mask = mask;
   p.digest = digest;

@@ -1,0 +1,165 @@
+// The training loss of TrainerPredictor.train (reference src/trainer.py:84-90)
+// for models whose mask is all True (bias / RotatE entity features):
+//
+//   target' = target * smoothing + one_hot(t) * (1 - smoothing)
+//   loss    = -sum_{q,e} log(softmax(logits)_{q,e} + 1e-8) * target'_{q,e}
+//             / max(sum_{q,e} target'_{q,e}, 1)
+//
+// and its gradient with respect to the logits, in two launches instead of
+// the ~22 element-wise launches of the torch formulation (softmax, add, log,
+// products, sums and their backward) — the EM predictor's training step is
+// host-bound on its launches.  One workgroup per row, three
+// passes over the row (max, sum of exponentials, then p, the loss terms and
+// the row sums); the rows' sums are added in a fixed order by the last
+// workgroup to finish (deterministic).  Sums are fp64.
+//
+// Backward: with p = softmax(logits), u_e = target'_e p_e / (p_e + 1e-8)
+// and W = sum_e u_e per row, d loss / d logit_j = -(g / T) (u_j - p_j W),
+// T = max(sum target', 1) (the chain rule through log and softmax).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "internal.h"
+
+namespace rnnl {
+
+constexpr int LBS = 256;
+
+__device__ __forceinline__ float block_max(float v, float *s) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+  __syncthreads();
+  return v;
+}
+
+__device__ __forceinline__ double block_sum(double v, double *s) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  return v;
+}
+
+// stats per row: [0] m (max), [1] Z (sum exp(x - m), as float), [2] W; row_sums[q] = (loss term sum, target sum)
+__global__ __launch_bounds__(LBS) void nll_forward_kernel(const float *__restrict__ logits,
+                                                          const float *__restrict__ target,
+                                                          const int64_t *__restrict__ all_t, int B, int E,
+                                                          float smoothing, float *__restrict__ stats,
+                                                          double *__restrict__ row_sums, unsigned *__restrict__ done,
+                                                          float *__restrict__ loss) {
+  __shared__ float s_f[4];
+  __shared__ double s_d[4];
+  __shared__ bool s_last;
+  const int q = blockIdx.x;
+  const float *x = logits + (int64_t)q * E;
+  const float *tg = target + (int64_t)q * E;
+  const int t = (int)all_t[q];
+  const float a = smoothing, b = 1.0f - smoothing;
+  float m = -__builtin_huge_valf();
+  for (int e = threadIdx.x; e < E; e += LBS) m = fmaxf(m, x[e]);
+  m = block_max(m, s_f);
+  double z = 0.0;
+  for (int e = threadIdx.x; e < E; e += LBS) z += (double)expf(x[e] - m);
+  const float Z = (float)block_sum(z, s_d);
+  double acc = 0.0, ts = 0.0, w = 0.0;
+  for (int e = threadIdx.x; e < E; e += LBS) {
+    const float p = expf(x[e] - m) / Z;
+    const float tt = tg[e] * a + (e == t ? b : 0.0f);
+    acc += (double)(logf(p + 1e-8f) * tt);
+    ts += (double)tt;
+    w += (double)(tt * p / (p + 1e-8f));
+  }
+  acc = block_sum(acc, s_d);
+  ts = block_sum(ts, s_d);
+  w = block_sum(w, s_d);
+  if (threadIdx.x == 0) {
+    stats[3 * q] = m;
+    stats[3 * q + 1] = Z;
+    stats[3 * q + 2] = (float)w;
+    row_sums[2 * q] = acc;
+    row_sums[2 * q + 1] = ts;
+    __threadfence();
+    s_last = atomicAdd(done, 1u) == (unsigned)(B - 1);
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {  // every row's sums are visible: add them in row order
+    __threadfence();
+    double L = 0.0, T = 0.0;
+    const volatile double *rs = row_sums;  // written by other workgroups: read past L1
+    for (int k = 0; k < B; ++k) {
+      L += rs[2 * k];
+      T += rs[2 * k + 1];
+    }
+    loss[0] = (float)(-L / fmax(T, 1.0));
+    loss[1] = (float)fmax(T, 1.0);  // T, kept for the backward
+    *done = 0u;                     // ready for the next launch
+  }
+}
+
+__global__ __launch_bounds__(LBS) void nll_backward_kernel(const float *__restrict__ logits,
+                                                           const float *__restrict__ target,
+                                                           const int64_t *__restrict__ all_t, int E,
+                                                           float smoothing, const float *__restrict__ stats,
+                                                           const float *__restrict__ loss,
+                                                           const float *__restrict__ grad_out,
+                                                           float *__restrict__ grad) {
+  const int q = blockIdx.y;
+  const int e = blockIdx.x * LBS + threadIdx.x;
+  if (e >= E) return;
+  const float m = stats[3 * q], Z = stats[3 * q + 1], W = stats[3 * q + 2];
+  const float scale = -grad_out[0] / loss[1];
+  const float p = expf(logits[(int64_t)q * E + e] - m) / Z;
+  const float tt = target[(int64_t)q * E + e] * smoothing + (e == (int)all_t[q] ? 1.0f - smoothing : 0.0f);
+  grad[(int64_t)q * E + e] = scale * (tt * p / (p + 1e-8f) - p * W);
+}
+
+}  // namespace rnnl
+
+using namespace rnnl;
+
+extern "C" {
+
+int rnnl_nll_aux_bytes(int32_t B, size_t *bytes) {
+  if (B < 0 || !bytes) {
+    set_error("rnnl_nll_aux_bytes: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = (size_t)B * (2 * sizeof(double) + 3 * sizeof(float));
+  return RNNL_OK;
+}
+
+int rnnl_nll_forward(const float *logits, const float *target, const int64_t *all_t, int32_t B, int32_t E,
+                     float smoothing, uint32_t *counter, void *aux, float *loss, void *stream) {
+  if (!logits || !target || !all_t || B <= 0 || E <= 0 || !counter || !aux || !loss) {
+    set_error("rnnl_nll_forward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  double *row_sums = static_cast<double *>(aux);
+  float *stats = reinterpret_cast<float *>(row_sums + 2 * (size_t)B);
+  hipLaunchKernelGGL(nll_forward_kernel, dim3((unsigned)B), dim3(LBS), 0, (hipStream_t)stream, logits, target, all_t,
+                     B, E, smoothing, stats, row_sums, counter, loss);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_nll_backward(const float *logits, const float *target, const int64_t *all_t, int32_t B, int32_t E,
+                      float smoothing, const void *aux, const float *loss, const float *grad_out, float *grad,
+                      void *stream) {
+  if (!logits || !target || !all_t || B <= 0 || E <= 0 || !aux || !loss || !grad_out || !grad) {
+    set_error("rnnl_nll_backward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const float *stats = reinterpret_cast<const float *>(static_cast<const double *>(aux) + 2 * (size_t)B);
+  hipLaunchKernelGGL(nll_backward_kernel, dim3((unsigned)((E + LBS - 1) / LBS), (unsigned)B), dim3(LBS), 0,
+                     (hipStream_t)stream, logits, target, all_t, E, smoothing, stats, loss, grad_out, grad);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+}  // extern "C"

@@ -1002,20 +1002,46 @@ __global__ void pack_weights_kernel(KParams p, float *__restrict__ W) {
   }
 }
 
-// The scoring pass after a grounding (K2): packs the weights, builds the
+extern "C" int rnnl_pack_weights_floats(size_t *n_floats) {
+  if (!n_floats) {
+    set_error("rnnl_pack_weights_floats: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *n_floats = W_FLOATS;
+  return RNNL_OK;
+}
+
+extern "C" int rnnl_pack_weights(const rnnl_predictor_params *pp, float *out, void *stream) {
+  if (!pp || !out || (pp->aggregator != RNNL_AGG_SUM && pp->aggregator != RNNL_AGG_PNA)) {
+    set_error("rnnl_pack_weights: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  KParams p{};
+  set_score_params(p, pp, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3((W_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, p, out);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+// The scoring pass after a grounding (K2): packs the weights (unless the
+// caller passes them packed), builds the
 // chunk list and launches the aggregator's chunk kernel.  `grid` caps its
 // persistent workgroups (0: the full grid); a smaller grid leaves CUs to a
 // concurrent kernel (RotatE).
 void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int grid) {
   KParams p = p0;
   const int nq = p.nq;
-  float *W = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
-  hipLaunchKernelGGL(pack_weights_kernel, dim3((W_FLOATS + 255) / 256), dim3(256), 0, st, p, W);
+  const float *W = p.packed;
+  if (!W) {
+    float *Wp = reinterpret_cast<float *>(p.ws + HDR_WORDS_BYTES);
+    hipLaunchKernelGGL(pack_weights_kernel, dim3((W_FLOATS + 255) / 256), dim3(256), 0, st, p, Wp);
+    W = Wp;
+  }
   launch_chunk_list(p, st);
   if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);  // sums over chunks
   const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * SCORE_WG_PER_CU);
   if (p.agg != RNNL_AGG_SUM) {
-    hipLaunchKernelGGL(score_pna_chunk_kernel, dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+    hipLaunchKernelGGL(score_pna_chunk_kernel, dim3(cgrid), dim3(BS), 0, st, p, W);
     return;
   }
   // the pair memo (not with the test digest, which needs every candidate's
@@ -1028,7 +1054,7 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
   if (small && pair)
     p.memo = nullptr;
   else
-    hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, (const float *)W);
+    hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, W);
   if (pair) {
     p.ptab = p.ptab_region;
     (void)hipMemsetAsync(p.ptab, 0, 8ull << p.psbits, st);
@@ -1036,13 +1062,13 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
   // one reference batch per call: the wave-cooperative walk of long entry lists
   // (bit-identical features); large launches keep the per-lane walk
   if (p.digest && small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<true, true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<true, true>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (p.digest)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<true, false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<true, false>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false>), dim3(cgrid), dim3(BS), 0, st, p, (const float *)W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false>), dim3(cgrid), dim3(BS), 0, st, p, W);
 }
 
 }  // namespace rnnl

@@ -67,6 +67,7 @@ class RotatE(torch.nn.Module):
         self.remb = torch.nn.parameter.Parameter(torch.cat([remb, -remb], dim=0))
         self._tables = None
         self._ws = None
+        self._ws_need = {}
         # DIRECT (default) evaluates the reference's arithmetic term by term;
         # mode = ROTATE_MFMA selects the faster expanded bf16x3 MFMA kernel
         # (cancellation-prone when h o r ~= t; include/rnnlogic_hip.h)
@@ -94,9 +95,13 @@ class RotatE(torch.nn.Module):
         return self._tables[1], self._tables[2]
 
     def _workspace(self, nq):
-        need = ctypes.c_size_t()
-        _native.call("rnnl_rotate_workspace_size", nq, self.num_entities, self.emb_dim, int(self.mode),
-                     ctypes.byref(need))
+        key = (nq, int(self.mode))
+        need = self._ws_need.get(key)
+        if need is None:
+            need = ctypes.c_size_t()
+            _native.call("rnnl_rotate_workspace_size", nq, self.num_entities, self.emb_dim, int(self.mode),
+                         ctypes.byref(need))
+            self._ws_need[key] = need
         if need.value == 0:
             return None, 0
         if self._ws is None or self._ws.numel() * 4 < need.value or self._ws.device != self.eemb.device:

@@ -822,6 +822,16 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if self.entity_feature == "bias":  # the scoring kernels add bias[t] without reading the filled row
             keep.append(self.bias.detach().float().contiguous())
             p.base_row = keep[-1].data_ptr()
+        # packed once per weight version, not per launch (a diagnostic RNNL_LIB
+        # build without rnnl_pack_weights packs per launch)
+        if self.hidden_dim == 16 and getattr(_native.lib(), "rnnl_pack_weights", None) is not None:
+            n = ctypes.c_size_t()
+            _native.call("rnnl_pack_weights_floats", ctypes.byref(n))
+            packed = torch.empty(n.value, dtype=torch.float32, device=node_w.device)
+            _native.call("rnnl_pack_weights", ctypes.byref(p), packed.data_ptr(),
+                         torch.cuda.current_stream(node_w.device).cuda_stream)
+            keep.append(packed)
+            p.packed = packed.data_ptr()
         return p, keep
 
     def base_score(self, all_h, all_r, out):
@@ -921,9 +931,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
     def _overlap_workspace(self, device, nq, scale):
-        need = ctypes.c_size_t()
-        _native.call("rnnl_forward_workspace_size", self.graph.device_graph(device), self.native_rules(device).ptr,
-                     nq, scale, ctypes.byref(need))
+        sk = ("need", self._device_index(device), nq, scale)
+        need = self._ws_chunks.get(sk)
+        if need is None:  # sizes depend on (rows, scale) only: one query per shape
+            need = ctypes.c_size_t()
+            _native.call("rnnl_forward_workspace_size", self.graph.device_graph(device),
+                         self.native_rules(device).ptr, nq, scale, ctypes.byref(need))
+            self._ws_chunks[sk] = need
         key = self._device_index(device)
         ws = self._ws_chunks.get(key)
         if ws is None or ws.numel() < need.value:
@@ -1155,7 +1169,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # after the launch status (its host read), so it costs no extra sync
         mixed = None
         if all_r.is_cuda and all_r.numel():
-            mixed = torch.empty((), dtype=torch.bool, pin_memory=True)
+            key = ("mixed", self._device_index(all_r.device))
+            mixed = self._side.get(key)
+            if mixed is None:  # one pinned flag, reused: it is read before the next call writes it
+                mixed = self._side[key] = torch.empty((), dtype=torch.bool, pin_memory=True)
             mixed.copy_((all_r != all_r[0]).any(), non_blocking=True)
         score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
         if mixed is not None:

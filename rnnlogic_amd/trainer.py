@@ -13,6 +13,7 @@ the padded count — with two differences in *how*, not *what*:
     autograd on the exported path-count COO).
 """
 import collections
+import ctypes
 import logging
 import os
 from itertools import islice
@@ -46,6 +47,50 @@ class _SizedIter(object):
 
 class _Prepared(tuple):
     """A training batch already squeezed and on the device (TrainerPredictor._prepare)."""
+
+
+class _SmoothedNLL(torch.autograd.Function):
+    """trainer.py:84-90's loss for a model whose mask is all True, on the
+    device in two HIP launches (rnnl_nll_forward / rnnl_nll_backward) instead
+    of ~22 element-wise torch launches:
+        target' = target * smoothing + one_hot(all_t) * (1 - smoothing)
+        loss = -sum(log(softmax(logits) + 1e-8) * target') / max(sum(target'), 1)
+    The sums are fp64 (the reference sums fp32 in torch's order; the loss
+    agrees to ~1e-7 relative)."""
+    _counters = {}
+
+    @staticmethod
+    def forward(ctx, logits, target, all_t, smoothing):
+        dev = logits.device
+        B, E = logits.shape
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        counter = _SmoothedNLL._counters.get(key)
+        if counter is None:  # zero between launches (the kernel resets it)
+            counter = _SmoothedNLL._counters[key] = torch.zeros(1, dtype=torch.int32, device=dev)
+        nb = ctypes.c_size_t()
+        _native.call("rnnl_nll_aux_bytes", B, ctypes.byref(nb))
+        aux = torch.empty(nb.value, dtype=torch.uint8, device=dev)
+        loss = torch.empty(2, dtype=torch.float32, device=dev)
+        logits = logits.contiguous()
+        target = target.contiguous().float()
+        all_t = all_t.contiguous()
+        _native.call("rnnl_nll_forward", logits.data_ptr(), target.data_ptr(), all_t.data_ptr(), B, E,
+                     float(smoothing), counter.data_ptr(), aux.data_ptr(), loss.data_ptr(),
+                     torch.cuda.current_stream(dev).cuda_stream)
+        ctx.save_for_backward(logits, target, all_t, aux, loss)
+        ctx.smoothing = float(smoothing)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, target, all_t, aux, loss = ctx.saved_tensors
+        B, E = logits.shape
+        grad = torch.empty_like(logits)
+        g = grad_out.reshape(1).contiguous().float()
+        _native.call("rnnl_nll_backward", logits.data_ptr(), target.data_ptr(), all_t.data_ptr(), B, E,
+                     ctx.smoothing, aux.data_ptr(), loss.data_ptr(), g.data_ptr(), grad.data_ptr(),
+                     torch.cuda.current_stream(logits.device).cuda_stream)
+        return grad, None, None, None
 
 
 class TrainerPredictor(object):
@@ -189,11 +234,21 @@ class TrainerPredictor(object):
         host sync."""
         all_h, all_r, all_t, target, edges_to_remove = batch if isinstance(batch, _Prepared) else \
             self._prepare(batch)
+        logits, mask = model(all_h, all_r, edges_to_remove)
+        if getattr(getattr(model, "module", model), "mask_all_true", False) and logits.is_cuda and \
+                logits.dtype == torch.float32 and logits.dim() == 2 and logits.size(0) > 0:
+            # every element counts (the reference's logits[mask] is the whole
+            # matrix): the fused HIP loss and its backward
+            msum = mask.numel()
+            loss = _SmoothedNLL.apply(logits, target, all_t, smoothing)
+            loss.backward()
+            self.optimizer.step()
+            self.optimizer.zero_grad()
+            return (loss.item() if sync else loss), msum
         # one_hot(all_t, E) as a scatter (the same 0 / 1 values; one_hot checks
         # its index range with a host read)
         target_t = torch.zeros_like(target).scatter_(1, all_t.view(-1, 1), 1.0)
         target = target * smoothing + target_t * (1 - smoothing)
-        logits, mask = model(all_h, all_r, edges_to_remove)
         logits = (torch.softmax(logits, dim=1) + 1e-8).log()
         if getattr(getattr(model, "module", model), "mask_all_true", False):
             msum = mask.numel()

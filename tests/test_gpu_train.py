@@ -67,15 +67,20 @@ def test_train_steps_match_reference(case, dev):
         p = "s%d/" % k
         for name, got in (("h", all_h), ("r", all_r), ("t", all_t), ("etr", etr)):
             np.testing.assert_array_equal(got.numpy(), z[p + name], err_msg="%s step %d %s" % (case, k, name))
-        target_t = torch.nn.functional.one_hot(all_t, graph.entity_size)
-        target = (target * 0.2 + target_t * 0.8).to(dev)
         logits, mask = model(all_h.to(dev), all_r.to(dev), etr.to(dev))
         want = float(z[p + "loss"])
         if mask.sum().item() == 0:
             assert np.isnan(want)
             continue
-        logits = (torch.softmax(logits, dim=1) + 1e-8).log()
-        loss = -(logits[mask] * target[mask]).sum() / torch.clamp(target[mask].sum(), min=1)
+        if model.mask_all_true:
+            # TrainerPredictor.train_step's fused HIP loss (rnnl_nll_forward / _backward)
+            from rnnlogic_amd.trainer import _SmoothedNLL
+            loss = _SmoothedNLL.apply(logits, target.to(dev), all_t.to(dev), 0.2)
+        else:
+            target_t = torch.nn.functional.one_hot(all_t, graph.entity_size)
+            target = (target * 0.2 + target_t * 0.8).to(dev)
+            logits = (torch.softmax(logits, dim=1) + 1e-8).log()
+            loss = -(logits[mask] * target[mask]).sum() / torch.clamp(target[mask].sum(), min=1)
         loss.backward()
         tol = LOSS_TOL if k == 0 else LATER_LOSS_TOL
         print("%s step %d: loss %.9g, reference %.9g, relative delta %.3g" % (case, k, loss.item(), want,
@@ -107,6 +112,30 @@ def test_train_steps_match_reference(case, dev):
                 np.testing.assert_allclose(g, z[key], atol=atol, rtol=GRAD_RTOL, err_msg="%s grad %s" % (case, n))
         optim.step()
         optim.zero_grad()
+
+
+@pytest.mark.parametrize("B,E", [(32, 14541), (7, 135), (1, 40943)])
+def test_fused_loss_matches_torch(B, E, dev):
+    """_SmoothedNLL (rnnl_nll_forward / rnnl_nll_backward) against the torch
+    formulation of trainer.py:84-90 with autograd, on random logits with a
+    wide range (a near-degenerate softmax row included)."""
+    from rnnlogic_amd.trainer import _SmoothedNLL
+    g = torch.Generator().manual_seed(B * 7 + E)
+    logits = (torch.randn(B, E, generator=g) * 6).to(dev)
+    logits[0, :5] += 40.0  # a row whose softmax mass sits on five entities
+    target = (torch.rand(B, E, generator=g) < 0.001).float().to(dev)
+    all_t = torch.randint(0, E, (B,), generator=g).to(dev)
+    x1 = logits.clone().requires_grad_(True)
+    loss1 = _SmoothedNLL.apply(x1, target, all_t, 0.2)
+    (loss1 * 1.5).backward()
+    x2 = logits.double().clone().requires_grad_(True)
+    tt = target.double() * 0.2 + torch.nn.functional.one_hot(all_t, E).double() * 0.8
+    lp = (torch.softmax(x2, dim=1) + 1e-8).log()
+    loss2 = -(lp * tt).sum() / torch.clamp(tt.sum(), min=1)
+    (loss2 * 1.5).backward()
+    assert abs(loss1.item() - loss2.item()) <= 2e-6 * abs(loss2.item()), (loss1.item(), loss2.item())
+    np.testing.assert_allclose(x1.grad.cpu().numpy(), x2.grad.cpu().numpy(), rtol=1e-4,
+                               atol=1e-6 * float(x2.grad.abs().max()))
 
 
 def test_trainer_end_to_end_umls(dev):
