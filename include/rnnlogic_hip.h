@@ -214,8 +214,9 @@ int rnnl_ground_export_candidates(void *workspace, int32_t n_queries, int32_t ca
 int rnnl_ground_export_entries(void *workspace, int32_t n_queries, int32_t capacity_scale, const int32_t *n_cand,
                                const int64_t *ent_off, int32_t *out_node, int32_t *out_count, void *stream);
 /* Diagnostic: when non-NULL, later forward launches add per-phase cycle
- * counters into dev_counters (12 x uint64: prologue, grounding, candidates,
- * queries, contributions, candidates, then candidate sub-phases). */
+ * counters into dev_counters (13 x uint64: prologue, grounding, candidates,
+ * queries, contributions, candidates, then the candidate and grounding
+ * sub-phases; tools/profile_phases.py). */
 int rnnl_debug_profile(void *dev_counters);
 /* Diagnostic: when non-NULL, later RotatE launches add (shader-clock ticks,
  * 100 MHz real-time ticks) of every block into dev_counters (2 x uint64); the

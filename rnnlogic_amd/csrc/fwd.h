@@ -18,6 +18,7 @@ constexpr int GBS = 256;       // threads per grounding workgroup
 constexpr int GNW = GBS / 64;  // its waves
 constexpr int HBITS = 12;
 constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count)
+constexpr int OCC_CAP = 1024;     // phase-A occupied-slot list (fuller levels scan all HCAP slots)
 constexpr int WBITS = 11;         // phase-B entity window: WIN entities
 constexpr int WIN = 1 << WBITS;
 constexpr int MAXE_BITS = 19;
@@ -220,15 +221,17 @@ __device__ __forceinline__ int block_scan(int x, int *s_ws, int &total) {
   return res;
 }
 
-// Largest i in [0, n) with a[i] <= k (a non-decreasing, a[0] == 0 <= k).
+// Largest i in [0, n) with a[i] <= k, n <= GBS, for a non-decreasing a of
+// GBS entries with a[0] <= k and a[i] > k for every i >= n — the block
+// scans' exclusive prefixes: threads past n add nothing, so their prefix is
+// the total, > k.  Branch-free: ceil(log2 n) steps of one LDS read, a
+// compare and a select (the bisection's bounds bookkeeping cost ~7 VALU
+// instructions a step; this is the grounding's per-edge / per-item search).
 __device__ __forceinline__ int upper_idx(const int *a, int n, int k) {
-  int lo = 0, hi = n - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (a[mid] <= k)
-      lo = mid;
-    else
-      hi = mid - 1;
+  int lo = 0;
+  for (int step = n > 1 ? 1 << (31 - __clz(n - 1)) : 0; step > 0; step >>= 1) {
+    const int c = lo + step;
+    lo = a[c] <= k ? c : lo;
   }
   return lo;
 }

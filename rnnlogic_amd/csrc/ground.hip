@@ -54,6 +54,9 @@ struct __align__(16) Smem {
       uint32_t ent_c[GBS];
       int it_child[GBS], it_beg[GBS], it_flags[GBS], edge_off[GBS];
       uint32_t it_c[GBS];
+      // the hash slots occupied at this level, in insertion order (the first
+      // OCC_CAP): the level's compaction walks them instead of all HCAP slots
+      unsigned short occ[OCC_CAP];
     };
     struct {  // phase B: entity bitmap of one hash pass and its popcount prefix (candidate ranks)
       uint32_t sbits[SORT_WORDS];
@@ -61,7 +64,7 @@ struct __align__(16) Smem {
     };
   };
   int ws[GNW + 1];
-  int q, nd, np, ovf, err, root;
+  int q, nd, np, ovf, err, root, nocc;
   long long qbase;
   unsigned long long t0;
   int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
@@ -94,6 +97,10 @@ __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
 #pragma unroll 1
   for (int probe = 0; probe < 64; ++probe) {
     const int k = atomicCAS(&S.u.a.key[h], EMPTY, key);
+    if (k == EMPTY) {  // a new (node, entity): listed for the level's compaction
+      const int i = atomicAdd(&S.nocc, 1);
+      if (i < OCC_CAP) S.occ[i] = (unsigned short)h;
+    }
     if (k == EMPTY || k == key) {
       const uint32_t old = atomicAdd(&S.u.a.val[h], c);
       if (old + c < old) atomicOr(&S.err, ERR_COUNT_WIDTH);  // carry out of the u32 path count
@@ -211,19 +218,32 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
       }
     }
     // compact the hash into the next frontier and clear it
-    for (int s = tid; s < HCAP; s += GBS) {
-      const int k = S.u.a.key[s];
-      if (k != EMPTY) {
-        emit_frontier(S, sl, nxt, p.fcap, (uint32_t)k, S.u.a.val[s]);
-        S.u.a.key[s] = EMPTY;
-        S.u.a.val[s] = 0u;
+    const int nocc = S.nocc;  // uniform: read after the edge loop's barrier
+    if (nocc <= OCC_CAP) {  // the listed slots only (small frontiers: most levels)
+      for (int i = tid; i < nocc; i += GBS) {
+        const int s2 = S.occ[i];
+        emit_frontier(S, sl, nxt, p.fcap, (uint32_t)S.u.a.key[s2], S.u.a.val[s2]);
+        S.u.a.key[s2] = EMPTY;
+        S.u.a.val[s2] = 0u;
+      }
+    } else {
+      for (int s2 = tid; s2 < HCAP; s2 += GBS) {
+        const int k = S.u.a.key[s2];
+        if (k != EMPTY) {
+          emit_frontier(S, sl, nxt, p.fcap, (uint32_t)k, S.u.a.val[s2]);
+          S.u.a.key[s2] = EMPTY;
+          S.u.a.val[s2] = 0u;
+        }
       }
     }
     wg_sync_global();
     PSTAMP(6);
     n_prev = min((int64_t)S.nd, p.fcap);
     __syncthreads();
-    if (tid == 0) S.nd = 0;
+    if (tid == 0) {
+      S.nd = 0;
+      S.nocc = 0;
+    }
     cur = nxt;
     __syncthreads();
   }
@@ -581,6 +601,7 @@ __global__ __launch_bounds__(GBS) void ground_kernel(KParams p) {
       S.root = root;
       S.np = 0;
       S.nd = 0;
+      S.nocc = 0;
       S.ovf = 0;
       S.sumlog = 0ull;
     }
@@ -646,7 +667,7 @@ __global__ __launch_bounds__(GBS) void ground_kernel(KParams p) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[k], pr[k]);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
+    for (int k = 0; k < 7; ++k) atomicAdd(&p.prof[6 + k], S.tp[k]);
   }
 }
 

@@ -34,268 +34,257 @@ __device__ __forceinline__ void exact_sums(const KParams &p, int beg, int cnt, i
   }
 }
 
-// Two walks over the candidate's bucket entries, one per half of the node
-// record, each folding its features into the Linear(192, 16) sums as soon
-// as it ends: walk 1 the mean and min features (sum c x, min), walk 2 the max
-// and std ones (sum c x^2, max; std from walk 1's means).  Only one half's
-// accumulators (16 fp64 + 16 float) and the 16 sums and 16 means are live
-// in either walk instead of both halves' (one walk held ~250 VGPRs, 2
-// waves/SIMD); the entries are read twice (the second walk's loads hit L2).
-// Materialise the 16 sums here, and keep later loads below: the FMAs of one
-// Linear input complete before the next input's weights are read (a plain
-// memory clobber orders the loads but lets the scheduler hoist all of them
-// ahead of the FMAs, which spills).
-__device__ __forceinline__ void pin16(float (&x)[16]) {
-  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
-               "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
-               :
-               : "memory");
+// score_model's weights as the scoring kernels keep them in LDS: layer 0's
+// candidate half (128 x 16) as the A fragments of v_mfma_f32_16x16x16_f16,
+// each weight split into two fp16 parts, and the last layer as floats.
+struct Mlp0Lds {
+  uint2 a0[8][2][64];  // [output tile][part][lane]: lane (k, i16) holds W0[16 ot + i16][4k .. 4k + 3]
+  float s1w[128], s1b[4];
+};
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// v = hi + lo + r with hi, lo fp16 (RNE) and |r| <= 2^-22 |v| for normal
+// parts (a subnormal lo part keeps an absolute error below 2^-25)
+__device__ __forceinline__ void split_f16(float v, _Float16 &hi, _Float16 &lo) {
+  hi = (_Float16)v;
+  lo = (_Float16)(v - (float)hi);
 }
 
-// FuncToNode (pna) up to score_model: x1 = ReLU(LayerNorm(Linear(192, 16)(features)))
-__device__ __forceinline__ void pna_hidden_2walk(const KParams &p, const float *wl, int beg, int cnt,
-                                                 float mean_scale, uint64_t *dig_out, int t, float (&x1)[16]) {
-  using L = WL<RNNL_AGG_PNA>;
-  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
-  double a[16];  // exact: see the walk
-  float m[16];
+__device__ __forceinline__ void load_mlp0(Mlp0Lds &m, const float *__restrict__ W) {
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) m.s1w[i] = W[W_S1W + i];
+  if (threadIdx.x < 4) m.s1b[threadIdx.x] = threadIdx.x == 0 ? W[W_S1B] : 0.f;
+  for (int i = threadIdx.x; i < 8 * 64; i += blockDim.x) {
+    const int ot = i >> 6, l = i & 63, o = ot * 16 + (l & 15), k0 = (l >> 4) * 4;
+    f16x4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      _Float16 h, q;
+      split_f16(W[W_S0X + o * 16 + k0 + j], h, q);
+      hi[j] = h;
+      lo[j] = q;
+    }
+    m.a0[ot][0][l] = __builtin_bit_cast(uint2, hi);
+    m.a0[ot][1][l] = __builtin_bit_cast(uint2, lo);
+  }
+}
+
+// score_model (layers.py:9-51) for the wave's 64 candidates (lane = candidate,
+// x1 its FuncToNodeSum output; whole wave, dead lanes pass anything finite):
+// Linear(32, 128) with the relation half folded into relb, ReLU,
+// Linear(128, 1).  Layer 0 runs on the matrix cores as D = W0 . X1^T, 16
+// candidates x 128 outputs per round (8 output tiles of
+// v_mfma_f32_16x16x16_f16; x1 and W0 split into two fp16 parts, the three
+// part products hi.hi, hi.lo, lo.hi accumulated in fp32 onto C = relb, the
+// dropped lo.lo below 2^-22 of |w x|; x1 >= 0 is post-LayerNorm, so fp16's
+// range holds it).  D lane (k, i16) holds outputs 4k .. 4k + 3 of candidate
+// i16: ReLU and the 128 -> 1 dot stay on the VALU per lane, summed over the
+// four k-lanes of a candidate by two xor shuffles.  A candidate's output
+// depends on its own x1 only (its own D column), in a fixed order, so equal
+// inputs give bit-identical outputs whatever the other lanes hold.  On the
+// VALU this layer was 2,048 FMAs + 256 max/fma per candidate, the bulk of the
+// SUM pass's VALU instructions, which take RotatE's issue slots beside it.
+// stage: the wave's 16 x 16 floats; relb: the wave's 128 folded biases.
+__device__ __forceinline__ void split4(const float4 v, f16x4 &hi, f16x4 &lo) {
+  const float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    _Float16 h, q;
+    split_f16(xs[j], h, q);
+    hi[j] = h;
+    lo[j] = q;
+  }
+}
+
+// score_model on one 16-candidate tile whose x1 is in B layout (lane (k, i16):
+// hidden 4k .. 4k + 3 of candidate i16, as fp16 parts): the candidate's
+// output, summed over its four k-lanes (every k-lane holds it).
+__device__ __forceinline__ float mlp0_tile(const f16x4 bh, const f16x4 bl, const Mlp0Lds &w, const float *relb) {
+  const int lane = threadIdx.x & 63, k = lane >> 4;
+  float acc = 0.f;
+#pragma unroll 1
+  for (int ot = 0; ot < 8; ++ot) {
+    const f16x4 ah = __builtin_bit_cast(f16x4, w.a0[ot][0][lane]);
+    const f16x4 al = __builtin_bit_cast(f16x4, w.a0[ot][1][lane]);
+    const float4 rb = reinterpret_cast<const float4 *>(relb)[ot * 4 + k];
+    f32x4 d = {rb.x, rb.y, rb.z, rb.w};
+    d = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, d, 0, 0, 0);  // smallest products first
+    d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, d, 0, 0, 0);
+    const float4 w1 = reinterpret_cast<const float4 *>(w.s1w)[ot * 4 + k];
+    acc = fmaf(fmaxf(d[0], 0.f), w1.x, acc);
+    acc = fmaf(fmaxf(d[1], 0.f), w1.y, acc);
+    acc = fmaf(fmaxf(d[2], 0.f), w1.z, acc);
+    acc = fmaf(fmaxf(d[3], 0.f), w1.w, acc);
+  }
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  return acc + w.s1b[0];
+}
+
+__device__ __forceinline__ float score_mlp_f16(const float (&x1)[16], const Mlp0Lds &w, float *stage,
+                                               const float *relb) {
+  const int lane = threadIdx.x & 63, k = lane >> 4, i16 = lane & 15;
+  float out = 0.f;
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    if (k == t) {
+      float4 *dst = reinterpret_cast<float4 *>(stage + i16 * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = make_float4(x1[4 * j], x1[4 * j + 1], x1[4 * j + 2], x1[4 * j + 3]);
+    }
+    wave_lds_sync();
+    const float4 xv = reinterpret_cast<const float4 *>(stage)[i16 * 4 + k];  // candidate 16 t + i16, K 4k..4k+3
+    wave_lds_sync();  // the next round rewrites the stage
+    f16x4 bh, bl;
+    split4(xv, bh, bl);
+    const float o = mlp0_tile(bh, bl, w, relb);
+    if (k == t) out = o;  // lane 16 t + i16 is candidate i16 of this round
+  }
+  return out;
+}
+
+// relation half of score_model.layers.0 folded into a per-relation bias (128 lanes)
+__device__ __forceinline__ float relation_bias(const KParams &p, int r, int o) {
+  float acc = p.s0_b[o];
+  for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
+  return acc;
+}
+
+// ---------------------------------------------------------------- PNA scoring over chunks
+// FuncToNode (pna, layers.py:79-126) + score_model for one wave x one chunk of
+// <= 64 consecutive candidates of one query (lane = candidate),
+// p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue chunks independently, so a
+// query with 17k candidates (WN18RR) is spread over ~280 waves instead of
+// holding one workgroup while the rest of the grid drains; no workgroup
+// barrier per query.
+//
+// Per candidate, two walks over its bucket entries (pna_walk: sums of
+// count x record in exact fp64 and the min / max), one per half of the node
+// records, give the 64 features [mean, min, max, std] (16 dims each); the
+// degree scalers {1, s, 1/s} make 192 inputs of add_model, Linear(192, 16).
+// That layer runs on the matrix cores as D1 = W . U^T for 16 candidates at a
+// time: U[c][(f, s3)] = feature f x scaler s3 (the reference's fp32 product)
+// split into two fp16 parts (features are means, minima, maxima and standard
+// deviations of rule embeddings: bounded), W (16 x 192) the A fragments per
+// (feature block, scaler), three part products per 16-wide K step.  D1's
+// lane (k, i16) holds outputs 4k .. 4k + 3 of candidate i16, so LayerNorm's
+// mean and variance are two xor shuffles away, and after ReLU the lane holds
+// exactly score_model's B fragment (hidden 4k .. 4k + 3 of candidate i16):
+// mlp0_tile runs on it with no second staging.  On the VALU the Linear was
+// 3,072 FMAs per candidate, most of the pass's VALU instructions — which
+// take RotatE's issue slots beside it.
+
+// LDS image of the PNA weights: add_model as A fragments per (feature block
+// b, scaler s3): lane (k, i16) holds W[i16][(16 b + 4k + j) 3 + s3], j < 4;
+// its bias, LayerNorm and score_model (Mlp0Lds).
+struct PnaLds {
+  uint2 aa[4][3][2][64];  // [block][scaler][part][lane]
+  float addb[16], lnw[16], lnb[16], pad[16];
+  Mlp0Lds m;
+};
+
+__device__ __forceinline__ void load_pna_weights(PnaLds &w, const float *__restrict__ W) {
+  for (int i = threadIdx.x; i < 4 * 3 * 64; i += blockDim.x) {
+    const int b = i / 192, s3 = (i / 64) % 3, l = i & 63, o = l & 15, k0 = (l >> 4) * 4;
+    f16x4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      _Float16 h, q;
+      split_f16(W[W_ADDW + o * 192 + (b * 16 + k0 + j) * 3 + s3], h, q);
+      hi[j] = h;
+      lo[j] = q;
+    }
+    w.aa[b][s3][0][l] = __builtin_bit_cast(uint2, hi);
+    w.aa[b][s3][1][l] = __builtin_bit_cast(uint2, lo);
+  }
+  if (threadIdx.x < 16) {
+    w.addb[threadIdx.x] = W[W_ADDB + threadIdx.x];
+    w.lnw[threadIdx.x] = W[W_LNW + threadIdx.x];
+    w.lnb[threadIdx.x] = W[W_LNB + threadIdx.x];
+  }
+  load_mlp0(w.m, W);
+}
+
+// One walk over a candidate's bucket entries for one half of the node records
+// (HALF 0: sum x and min; 1: sum x^2 and max): the exact sums of count x
+// record word (fp64 is exact below a total count of 2^23; past it the int64
+// sums of exact_sums) as floats at the column's scale, and the min / max.
+// STATS (walk 1): the degree, count total and digest fingerprint too.
+template <int HALF, bool STATS>
+__device__ __forceinline__ void pna_walk(const KParams &p, int beg, int cnt, uint64_t &csum, long long &deg,
+                                         uint64_t &fp, bool want_fp, float (&sum)[16], float (&mm)[16]) {
+  double a[16];
 #pragma unroll
   for (int d = 0; d < 16; ++d) {
     a[d] = 0;
-    m[d] = __builtin_huge_valf();
+    mm[d] = HALF == 0 ? __builtin_huge_valf() : -__builtin_huge_valf();
   }
-  long long deg = 0;
-  uint64_t fp = 0, csum = 0;
 #pragma unroll 1
   for (int e = beg; e < beg + cnt; ++e) {
     const int2 be = p.bent[e];
-    const int n = be.x;
-    const long long c = (uint32_t)be.y;
     const double cd = (double)(uint32_t)be.y;
-    csum += (uint64_t)c;
-    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStridePna);
+    if constexpr (STATS) {
+      const long long c = (uint32_t)be.y;
+      csum += (uint64_t)c;
+      deg += c * p.rl.node_nrules[be.x];
+      if (want_fp) fp += (uint64_t)c * p.rl.node_fp[be.x];
+    }
+    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna) + HALF * 16;
     const float *fr = reinterpret_cast<const float *>(rec + 32);
 #pragma unroll
     for (int d = 0; d < 16; ++d) {
       a[d] = fma(cd, (double)rec[d], a[d]);
-      m[d] = fminf(m[d], fr[d]);
-    }
-    deg += c * p.rl.node_nrules[n];
-    if (dig_out) fp += (uint64_t)c * p.rl.node_fp[n];
-  }
-  if (dig_out) *dig_out = mix64((uint64_t)t ^ mix64((uint64_t)deg ^ mix64(fp)));
-  if (csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33 total count
-  // |record| < 2^30, so below a total count of 2^23 every product and partial
-  // sum is an integer under 2^53 and the fp64 FMAs are exact: a[d] is the
-  // int64 sum itself.  Past it (rare), exact int64 sums one dim at a time.
-  if (csum >> 23) exact_sums(p, beg, cnt, 0, a);
-  const double inv1 = ldexp(1.0, -(int)trailer[1]);
-  // FuncToNode (pna): mean/min/max/std x {1, s, 1/s} -> Linear(192,16) (layers.py:93-123);
-  // input j = (block * 16 + d) * 3 + s3, weights in LDS as [j][o]
-  const float degf = (float)(deg + 1);
-  const float dcl = fmaxf(degf, 1e-6f);
-  const float scale = logf(degf) / fmaxf(mean_scale, 1e-6f);
-  const float sc[3] = {1.0f, scale, 1.0f / fmaxf(scale, 1e-6f)};
-  float mean[16];
-#pragma unroll
-  for (int o = 0; o < 16; ++o) x1[o] = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    const float s = (float)(a[d] * inv1);
-    mean[d] = s / dcl;
-    const float fv[2] = {mean[d], m[d]};
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-#pragma unroll
-      for (int s3 = 0; s3 < 3; ++s3) {
-        pin16(x1);  // one input's 16 weights live at a time: its FMAs end before the next loads
-        const float v = fv[b] * sc[s3];
-        const float *w = wl + L::ADDW + ((b * 16 + d) * 3 + s3) * 16;
-#pragma unroll
-        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
-      }
+      mm[d] = HALF == 0 ? fminf(mm[d], fr[d]) : fmaxf(mm[d], fr[d]);
     }
   }
-  // walk 2: the squared half of the records and the max
+  if (csum >> 23) exact_sums(p, beg, cnt, HALF * 16, a);
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  const double inv = ldexp(1.0, -(int)trailer[HALF == 0 ? 1 : 4]);
 #pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    a[d] = 0;
-    m[d] = -__builtin_huge_valf();
-  }
-  asm volatile("" ::: "memory");
-#pragma unroll 1
-  for (int e = beg; e < beg + cnt; ++e) {
-    const int2 be = p.bent[e];
-    const double cd = (double)(uint32_t)be.y;
-    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna);
-    const float *fr = reinterpret_cast<const float *>(rec + 48);
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a[d] = fma(cd, (double)rec[16 + d], a[d]);
-      m[d] = fmaxf(m[d], fr[d]);
-    }
-  }
-  if (csum >> 23) exact_sums(p, beg, cnt, 16, a);
-  const double inv2 = ldexp(1.0, -(int)trailer[4]);
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    const float sq = (float)(a[d] * inv2);
-    const float sqm = sq / dcl;
-    const float fv[2] = {m[d], sqrtf(fmaxf(sqm - mean[d] * mean[d], 1e-6f))};
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-#pragma unroll
-      for (int s3 = 0; s3 < 3; ++s3) {
-        pin16(x1);  // one input's 16 weights live at a time: its FMAs end before the next loads
-        const float v = fv[b] * sc[s3];
-        const float *w = wl + L::ADDW + (((b + 2) * 16 + d) * 3 + s3) * 16;
-#pragma unroll
-        for (int o = 0; o < 16; ++o) x1[o] = fmaf(v, w[o], x1[o]);
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 0; o < 16; ++o) x1[o] += wl[L::ADDB + o];
-  float mu = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; ++d) mu += x1[d];
-  mu = mu / 16.0f;
-  float var = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    const float z = x1[d] - mu;
-    var = fmaf(z, z, var);
-  }
-  var = var / 16.0f;
-  const float rstd = 1.0f / sqrtf(var + 1e-5f);
-#pragma unroll
-  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * wl[L::LNW + d] + wl[L::LNB + d], 0.f);
+  for (int d = 0; d < 16; ++d) sum[d] = (float)(a[d] * inv);
 }
 
-// score_model (Linear(32, 128) with the relation half folded into relb, ReLU,
-// Linear(128, 1)) for the wave's 64 candidates at once on the bf16 matrix
-// cores: 64 x 16 hidden inputs times the 16 x 128 layer-0 weights as
-// v_mfma_f32_16x16x16_bf16 tiles, every fp32 operand split exactly into three
-// bf16 parts (v = v0 + v1 + v2) and the six part products with i + j <= 2 kept
-// (the dropped ones are below 2^-24 of |x w|), accumulated in fp32.  On the
-// VALU this layer is 2,048 FMAs per candidate — a third of the PNA pass's
-// VALU instructions, and those take RotatE's issue slots when the pass runs
-// beside it; the matrix pipe runs beside the VALU.  Tile layout
-// (lane = 16 k + i16): A row i16 (candidate rt * 16 + i16), K 4k .. 4k + 3;
-// B K 4k .. 4k + 3, column i16 (output ct * 16 + i16); D rows 4k + j, column
-// i16.  Whole-wave (EXEC full): dead lanes pass x1 = 0 and ignore the result.
-// sb: [8 column tiles][3 parts][64 lanes] B fragments (built once per block);
-// sx: the wave's [3 parts][64 candidates][4 K-groups] staging; so: [64].
-typedef short pna_s16x4 __attribute__((ext_vector_type(4)));
-typedef float pna_f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ unsigned short pna_bf16(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
-__device__ __forceinline__ void pna_split3(float v, unsigned short (&q)[3]) {
-  q[0] = pna_bf16(v);
-  const float r1 = v - __uint_as_float((unsigned)q[0] << 16);
-  q[1] = pna_bf16(r1);
-  q[2] = pna_bf16(r1 - __uint_as_float((unsigned)q[1] << 16));
-}
-__device__ __forceinline__ uint2 pna_pack4(const unsigned short (&q)[4][3], int part) {
-  return make_uint2(q[0][part] | ((unsigned)q[1][part] << 16), q[2][part] | ((unsigned)q[3][part] << 16));
-}
-// score_mlp_mfma's B fragments from the packed weights: column tile ct, lane
-// (k, i16) holds W[ct * 16 + i16][4k .. 4k + 3] as 3 bf16 parts
-__device__ __forceinline__ void build_mlp_b(const float *__restrict__ W, uint2 *sb, int tid) {
-  for (int i = tid; i < 8 * 64; i += BS) {
-    const int ct = i >> 6, l = i & 63, o = ct * 16 + (l & 15), k0 = (l >> 4) * 4;
-    unsigned short q[4][3];
+// One feature block (16 features of each of the wave's 64 candidates) into
+// the four tiles' add_model accumulators: staged, then per tile and scaler
+// one 16-wide K step (three fp16 part products).
+__device__ __forceinline__ void pna_block(const PnaLds &w, int b, const float (&v)[16], float *stage,
+                                          const float2 *sc, f32x4 (&D)[4]) {
+  const int lane = threadIdx.x & 63, k = lane >> 4, i16 = lane & 15;
+  float4 *st = reinterpret_cast<float4 *>(stage);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) pna_split3(W[W_S0X + o * 16 + k0 + kk], q[kk]);
-#pragma unroll
-    for (int part = 0; part < 3; ++part) sb[(ct * 3 + part) * 64 + l] = pna_pack4(q, part);
-  }
-}
-template <int AGG>
-__device__ __forceinline__ float score_mlp_mfma(const float (&x1)[16], const uint2 *__restrict__ sb, uint2 *sx,
-                                                float *so, const float *relb, const float *wl, int lane) {
-  using L = WL<AGG>;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    unsigned short q[4][3];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) pna_split3(x1[4 * g + kk], q[kk]);
-#pragma unroll
-    for (int part = 0; part < 3; ++part) sx[(part * 64 + lane) * 4 + g] = pna_pack4(q, part);
-  }
+  for (int j = 0; j < 4; ++j) st[lane * 4 + j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
   wave_lds_sync();
-  const int k = lane >> 4, i16 = lane & 15;
-#pragma unroll 1
-  for (int rt = 0; rt < 4; ++rt) {
-    pna_s16x4 a[3];
 #pragma unroll
-    for (int part = 0; part < 3; ++part)
-      a[part] = __builtin_bit_cast(pna_s16x4, sx[(part * 64 + rt * 16 + i16) * 4 + k]);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int ct = 0; ct < 8; ++ct) {
-      pna_s16x4 b[3];
+  for (int t = 0; t < 4; ++t) {
+    const float4 x = st[(t * 16 + i16) * 4 + k];  // candidate 16 t + i16, features 16 b + 4k .. + 3
+    const float2 c = sc[t * 16 + i16];
 #pragma unroll
-      for (int part = 0; part < 3; ++part) b[part] = __builtin_bit_cast(pna_s16x4, sb[(ct * 3 + part) * 64 + lane]);
-      const float rb = relb[ct * 16 + i16], w1 = wl[L::S1W + ct * 16 + i16];
-      pna_f32x4 d = {0.f, 0.f, 0.f, 0.f};
-      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], b[0], d, 0, 0, 0);  // smallest parts first
-      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[1], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[2], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[0], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[1], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[0], d, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = fmaf(fmaxf(d[j] + rb, 0.f), w1, acc[j]);
-    }
-    // each lane holds 8 of the 128 output terms of rows 4k + j: sum over the
-    // 16 lanes of its K-group (xor 1, 2, 4, 8 stays inside the group)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = acc[j];
-      v += __shfl_xor(v, 1);
-      v += __shfl_xor(v, 2);
-      v += __shfl_xor(v, 4);
-      v += __shfl_xor(v, 8);
-      if (i16 == 0) so[rt * 16 + 4 * k + j] = v;
+    for (int s3 = 0; s3 < 3; ++s3) {
+      const float m = s3 == 1 ? c.x : c.y;
+      const float4 u = s3 == 0 ? x : make_float4(x.x * m, x.y * m, x.z * m, x.w * m);
+      f16x4 bh, bl;
+      split4(u, bh, bl);
+      const f16x4 ah = __builtin_bit_cast(f16x4, w.aa[b][s3][0][lane]);
+      const f16x4 al = __builtin_bit_cast(f16x4, w.aa[b][s3][1][lane]);
+      D[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, D[t], 0, 0, 0);
+      D[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, D[t], 0, 0, 0);
+      D[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, D[t], 0, 0, 0);
     }
   }
-  wave_lds_sync();
-  const float out = so[lane] + wl[L::S1B];
-  wave_lds_sync();  // sx / so are rewritten by the next call
-  return out;
+  wave_lds_sync();  // the next block rewrites the stage
 }
 
-// ---------------------------------------------------------------- PNA scoring over chunks
-// The unit of work is one wave x one chunk of <= 64 consecutive candidates of
-// one query (lane = candidate), p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue
-// chunks independently, so a query with 17k candidates (WN18RR) is spread
-// over ~280 waves instead of holding one workgroup while the rest of the grid
-// drains; no workgroup barrier per query.  Each wave folds its relation's
-// half of score_model.layers.0 into its own LDS slice when the relation
-// changes.  Per candidate: pna_hidden_2walk (VALU), then score_model on the
-// matrix cores for the wave's 64 candidates at once (score_mlp_mfma).
 __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const float *__restrict__ W) {
-  using L = WL<RNNL_AGG_PNA>;
-  __shared__ __attribute__((aligned(16))) float s_w[L::N];
-  __shared__ float s_relb[BS / 64][128];
-  __shared__ uint2 s_b[8 * 3 * 64];           // score_model layer-0 B fragments (score_mlp_mfma)
-  __shared__ uint2 s_x[BS / 64][3 * 64 * 4];  // per wave: hidden inputs, 3 bf16 parts
-  __shared__ float s_o[BS / 64][64];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ PnaLds s_w;
+  __shared__ __attribute__((aligned(16))) float s_relb[BS / 64][128];
+  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][64 * 16];  // a feature block of 64 candidates
+  __shared__ float2 s_sc[BS / 64][64];                                      // their scalers (s, 1 / s)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, k = lane >> 4;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
   check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna));
-  for (int i = tid; i < L::N; i += BS) {
-    float v = 0.f;
-    if (i < L::ADDB) v = W[W_ADDW + (i % 16) * L::KIN + i / 16];  // add_w transposed: [input j][output o]
-    else if (i < L::LNW) v = W[W_ADDB + i - L::ADDB];
-    else if (i < L::LNB) v = W[W_LNW + i - L::LNW];
-    else if (i < L::S0X) v = W[W_LNB + i - L::LNB];
-    else if (i < L::S1W) v = W[W_S0X + i - L::S0X];
-    else if (i < L::S1B) v = W[W_S1W + i - L::S1W];
-    else if (i == L::S1B) v = W[W_S1B];
-    s_w[i] = v;
-  }
-  build_mlp_b(W, s_b, tid);
+  load_pna_weights(s_w, W);
   __syncthreads();  // the only workgroup barrier: waves run independently from here
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
   float *relb = s_relb[wv];
@@ -310,42 +299,86 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
     const int s0 = __builtin_amdgcn_readfirstlane(ck.y);
     const int r = __builtin_amdgcn_readfirstlane((int)p.all_r[q]);
     if (r != cur_r) {
-      // relation half of score_model.layers.0 folded into a per-wave bias
-      __builtin_amdgcn_wave_barrier();  // the previous chunk's reads of the slice are done
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int o = lane + 64 * j;
-        float acc = p.s0_b[o];
-        for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
-        relb[o] = acc;
-      }
+      wave_lds_sync();  // the previous chunk's reads of the slice are done
+      relb[lane] = relation_bias(p, r, lane);
+      relb[lane + 64] = relation_bias(p, r, lane + 64);
       wave_lds_sync();
       cur_r = r;
     }
     const int nc = p.n_cand[q];
     const int s = s0 + lane;
-    // every lane reaches the whole-wave score_model; lanes past the chunk's
-    // candidates carry x1 = 0 and store nothing
+    // every lane takes part in the matrix-core layers; lanes past the chunk's
+    // candidates carry zero features and store nothing
     const bool live = s < nc;
     int64_t qb = 0;
-    int t = 0;
-    float x1[16];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) x1[d] = 0.f;
+    int4 cr = make_int4(0, 0, 0, 0);
     if (live) {
       qb = p.q_base[q];
-      const float ms = p.q_scale[q];
-      const int4 cr = p.cand[qb + s];
-      t = cr.x;
-      uint64_t dg = 0;
-      asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop
-      pna_hidden_2walk(p, s_w, cr.y, cr.z, ms, p.digest ? &dg : nullptr, t, x1);
-      if (p.digest) atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q), (unsigned long long)dg);
+      cr = p.cand[qb + s];
     }
-    const float out = score_mlp_mfma<RNNL_AGG_PNA>(x1, s_b, s_x[wv], s_o[wv], relb, s_w, lane);
+    uint64_t csum = 0, fp = 0;
+    long long deg = 0;
+    float sum[16], mm[16], mean[16];
+    asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop
+    pna_walk<0, true>(p, cr.y, cr.z, csum, deg, fp, p.digest != nullptr, sum, mm);
+    if (p.digest && live)
+      atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q),
+                (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
+    if (live && (csum >> 33)) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33
+    // degree and scalers (layers.py:92, 103-116): degree = sum of A_fn + 1
+    const float degf = (float)(deg + 1);
+    const float dcl = fmaxf(degf, 1e-6f);
+    const float sc1 = live ? logf(degf) / fmaxf(p.q_scale[q], 1e-6f) : 1.0f;
+    s_sc[wv][lane] = make_float2(sc1, 1.0f / fmaxf(sc1, 1e-6f));
+    f32x4 D[4];
+    {
+      const float4 ab = reinterpret_cast<const float4 *>(s_w.addb)[k];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) D[t] = (f32x4){ab.x, ab.y, ab.z, ab.w};
+    }
+#pragma unroll
+    for (int d = 0; d < 16; ++d) mean[d] = sum[d] / dcl;
+    pna_block(s_w, 0, mean, s_stage[wv], s_sc[wv], D);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) mm[d] = live ? mm[d] : 0.f;  // (an empty walk's min is +inf)
+    pna_block(s_w, 1, mm, s_stage[wv], s_sc[wv], D);
+    pna_walk<1, false>(p, cr.y, cr.z, csum, deg, fp, false, sum, mm);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) mm[d] = live ? mm[d] : 0.f;
+    pna_block(s_w, 2, mm, s_stage[wv], s_sc[wv], D);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) sum[d] = sqrtf(fmaxf(sum[d] / dcl - mean[d] * mean[d], 1e-6f));
+    pna_block(s_w, 3, sum, s_stage[wv], s_sc[wv], D);
+    // LayerNorm over each candidate's 16 outputs (four k-lanes), ReLU, score_model
+    float out = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float s4 = (D[t][0] + D[t][1]) + (D[t][2] + D[t][3]);
+      s4 += __shfl_xor(s4, 16, 64);
+      s4 += __shfl_xor(s4, 32, 64);
+      const float mu = s4 / 16.0f;
+      float z[4], v4 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        z[j] = D[t][j] - mu;
+        v4 = fmaf(z[j], z[j], v4);
+      }
+      v4 += __shfl_xor(v4, 16, 64);
+      v4 += __shfl_xor(v4, 32, 64);
+      const float rstd = 1.0f / sqrtf(v4 / 16.0f + 1e-5f);
+      const float4 lw = reinterpret_cast<const float4 *>(s_w.lnw)[k];
+      const float4 lb = reinterpret_cast<const float4 *>(s_w.lnb)[k];
+      const float4 x1 = make_float4(fmaxf(z[0] * rstd * lw.x + lb.x, 0.f), fmaxf(z[1] * rstd * lw.y + lb.y, 0.f),
+                                    fmaxf(z[2] * rstd * lw.z + lb.z, 0.f), fmaxf(z[3] * rstd * lw.w + lb.w, 0.f));
+      f16x4 bh, bl;
+      split4(x1, bh, bl);
+      const float o = mlp0_tile(bh, bl, s_w.m, relb);
+      if (k == t) out = o;  // lane 16 t + i16 is candidate i16 of tile t
+    }
     if (!live) continue;
+    const int t = cr.x;
     const int64_t idx = (int64_t)q * p.g.E + t;
-    if (p.atomic_out) {  // deferred beside RotatE: added into the zeroed row (see deferred_add)
+    if (p.atomic_out) {  // deferred beside RotatE: added into the zeroed row (see sum_write_out)
       unsafeAtomicAdd(p.score + idx, out);
       continue;
     }
@@ -429,46 +462,20 @@ __device__ __forceinline__ void gather_sum(const KParams &p, int beg, int cnt, f
 }
 
 // LDS image of the SUM scoring weights: FuncToNodeSum's Linear(16, 16) and
-// LayerNorm and score_model's last layer as floats (VALU), and
-// score_model.layers.0's candidate half (128 x 16) as the A fragments of
-// v_mfma_f32_16x16x16_f16, each weight split into two fp16 parts.
+// LayerNorm as floats (VALU) and score_model (Mlp0Lds).
 struct SumLds {
-  float addw[256], addb[16], lnw[16], lnb[16], s1w[128], s1b[4];
-  uint2 a0[8][2][64];  // [output tile][part][lane]: lane (k, i16) holds W0[16 ot + i16][4k .. 4k + 3]
+  float addw[256], addb[16], lnw[16], lnb[16];
+  Mlp0Lds m;
 };
-
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// v = hi + lo + r with hi, lo fp16 (RNE) and |r| <= 2^-22 |v| for normal
-// parts (a subnormal lo part keeps an absolute error below 2^-25)
-__device__ __forceinline__ void split_f16(float v, _Float16 &hi, _Float16 &lo) {
-  hi = (_Float16)v;
-  lo = (_Float16)(v - (float)hi);
-}
 
 __device__ __forceinline__ void load_sum_weights(SumLds &w, const float *__restrict__ W) {
   for (int i = threadIdx.x; i < 256; i += blockDim.x) w.addw[i] = W[W_ADDW + i];
-  for (int i = threadIdx.x; i < 128; i += blockDim.x) w.s1w[i] = W[W_S1W + i];
   if (threadIdx.x < 16) {
     w.addb[threadIdx.x] = W[W_ADDB + threadIdx.x];
     w.lnw[threadIdx.x] = W[W_LNW + threadIdx.x];
     w.lnb[threadIdx.x] = W[W_LNB + threadIdx.x];
   }
-  if (threadIdx.x < 4) w.s1b[threadIdx.x] = threadIdx.x == 0 ? W[W_S1B] : 0.f;
-  for (int i = threadIdx.x; i < 8 * 64; i += blockDim.x) {
-    const int ot = i >> 6, l = i & 63, o = ot * 16 + (l & 15), k0 = (l >> 4) * 4;
-    f16x4 hi, lo;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      _Float16 h, q;
-      split_f16(W[W_S0X + o * 16 + k0 + j], h, q);
-      hi[j] = h;
-      lo[j] = q;
-    }
-    w.a0[ot][0][l] = __builtin_bit_cast(uint2, hi);
-    w.a0[ot][1][l] = __builtin_bit_cast(uint2, lo);
-  }
+  load_mlp0(w.m, W);
 }
 
 // FuncToNodeSum tail: x1 = ReLU(LayerNorm(Linear(16, 16)(f)))   (layers.py:53-77)
@@ -496,76 +503,6 @@ __device__ __forceinline__ void sum_hidden(const SumLds &w, const float f[16], f
   for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * w.lnw[d] + w.lnb[d], 0.f);
 }
 
-// score_model (layers.py:9-51) for the wave's 64 candidates (lane = candidate,
-// x1 its FuncToNodeSum output; whole wave, dead lanes pass anything finite):
-// Linear(32, 128) with the relation half folded into relb, ReLU,
-// Linear(128, 1).  Layer 0 runs on the matrix cores as D = W0 . X1^T, 16
-// candidates x 128 outputs per round (8 output tiles of
-// v_mfma_f32_16x16x16_f16; x1 and W0 split into two fp16 parts, the three
-// part products hi.hi, hi.lo, lo.hi accumulated in fp32 onto C = relb, the
-// dropped lo.lo below 2^-22 of |w x|; x1 >= 0 is post-LayerNorm, so fp16's
-// range holds it).  D lane (k, i16) holds outputs 4k .. 4k + 3 of candidate
-// i16: ReLU and the 128 -> 1 dot stay on the VALU per lane, summed over the
-// four k-lanes of a candidate by two xor shuffles.  A candidate's output
-// depends on its own x1 only (its own D column), in a fixed order, so equal
-// inputs give bit-identical outputs whatever the other lanes hold.  On the
-// VALU this layer was 2,048 FMAs + 256 max/fma per candidate, the bulk of the
-// SUM pass's VALU instructions, which take RotatE's issue slots beside it.
-// stage: the wave's 16 x 16 floats; relb: the wave's 128 folded biases.
-__device__ __forceinline__ float sum_mlp_mfma(const float (&x1)[16], const SumLds &w, float *stage,
-                                              const float *relb) {
-  const int lane = threadIdx.x & 63, k = lane >> 4, i16 = lane & 15;
-  float out = 0.f;
-#pragma unroll 1
-  for (int t = 0; t < 4; ++t) {
-    if (k == t) {
-      float4 *dst = reinterpret_cast<float4 *>(stage + i16 * 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dst[j] = make_float4(x1[4 * j], x1[4 * j + 1], x1[4 * j + 2], x1[4 * j + 3]);
-    }
-    wave_lds_sync();
-    const float4 xv = reinterpret_cast<const float4 *>(stage)[i16 * 4 + k];  // candidate 16 t + i16, K 4k..4k+3
-    wave_lds_sync();  // the next round rewrites the stage
-    f16x4 bh, bl;
-    {
-      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        _Float16 h, q;
-        split_f16(xs[j], h, q);
-        bh[j] = h;
-        bl[j] = q;
-      }
-    }
-    float acc = 0.f;
-#pragma unroll 1
-    for (int ot = 0; ot < 8; ++ot) {
-      const f16x4 ah = __builtin_bit_cast(f16x4, w.a0[ot][0][lane]);
-      const f16x4 al = __builtin_bit_cast(f16x4, w.a0[ot][1][lane]);
-      const float4 rb = reinterpret_cast<const float4 *>(relb)[ot * 4 + k];
-      f32x4 d = {rb.x, rb.y, rb.z, rb.w};
-      d = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, d, 0, 0, 0);  // smallest products first
-      d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, d, 0, 0, 0);
-      const float4 w1 = reinterpret_cast<const float4 *>(w.s1w)[ot * 4 + k];
-      acc = fmaf(fmaxf(d[0], 0.f), w1.x, acc);
-      acc = fmaf(fmaxf(d[1], 0.f), w1.y, acc);
-      acc = fmaf(fmaxf(d[2], 0.f), w1.z, acc);
-      acc = fmaf(fmaxf(d[3], 0.f), w1.w, acc);
-    }
-    acc += __shfl_xor(acc, 16, 64);
-    acc += __shfl_xor(acc, 32, 64);
-    if (k == t) out = acc + w.s1b[0];  // lane 16 t + i16 is candidate i16 of this round
-  }
-  return out;
-}
-
-// relation half of score_model.layers.0 folded into a per-relation bias (128 lanes)
-__device__ __forceinline__ float relation_bias(const KParams &p, int r, int o) {
-  float acc = p.s0_b[o];
-  for (int i = 0; i < 16; ++i) acc = fmaf(p.s0_w[o * 32 + 16 + i], p.rel_emb[r * 16 + i], acc);
-  return acc;
-}
 
 // ---------------------------------------------------------------- single-path memo
 // 38 % of the FB15k-237 test candidates are reached by exactly one path of
@@ -573,12 +510,12 @@ __device__ __forceinline__ float relation_bias(const KParams &p, int r, int o) {
 // record itself, so their score_model output depends on (head relation, n)
 // only: memo_sum_kernel computes it once per launch for every leaf node of
 // every head (131,883 MLPs instead of ~22 M), with the full path's own
-// arithmetic (the single entry's gather, then sum_hidden and sum_mlp_mfma).
+// arithmetic (the single entry's gather, then sum_hidden and score_mlp_f16).
 // Launches with at most this many rows skip it (pair-memo keys instead).
 constexpr int MEMO_SCAN_ROWS = 2048;
 
 // One workgroup per head relation with rules: memo[n] for its leaf nodes
-// (whole waves: score_model runs on the matrix cores, sum_mlp_mfma).
+// (whole waves: score_model runs on the matrix cores, score_mlp_f16).
 __global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__restrict__ W) {
   __shared__ SumLds s_w;
   __shared__ __attribute__((aligned(16))) float s_relb[128];
@@ -605,7 +542,7 @@ __global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__
     }
     float x1[16];
     sum_hidden(s_w, f, x1);
-    const float out = sum_mlp_mfma(x1, s_w, s_stage[wv], s_relb);
+    const float out = score_mlp_f16(x1, s_w.m, s_stage[wv], s_relb);
     if (n >= 0) p.memo[n] = out;
   }
 }
@@ -784,7 +721,7 @@ __device__ __forceinline__ void sum_score_lane(const KParams &p, const SumLds &w
   asm volatile("" ::: "memory");  // keep the LDS weight reads inside (hoisted they pin ~200 VGPRs)
   float x1[16];
   sum_hidden(w, f, x1);
-  const float out = sum_mlp_mfma(x1, w, stage, relb);
+  const float out = score_mlp_f16(x1, w.m, stage, relb);
   if (!live) return;
   sum_write_out(p, it.x, cr.x, out, base);
   if (!DIGEST && p.ptab && cr.z <= 3) {
@@ -881,7 +818,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     KParams p, const float *__restrict__ W) {
   __shared__ SumLds s_w;
   __shared__ __attribute__((aligned(16))) float s_relb[BS / 64][128];
-  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][256];  // sum_mlp_mfma's x1 staging
+  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][256];  // score_mlp_f16's x1 staging
   __shared__ int2 s_queue[BS / 64][128];
   // the COOP flush's long-list features (BIG_SLOTS x 16 floats) share the
   // stage: they are read into registers before score_model stages x1

@@ -31,7 +31,7 @@ def main():
     r = torch.from_numpy(rows[:, 1]).to(dev)
     with torch.no_grad():
         model.forward_rows(h, r, None)
-        prof = torch.zeros(12, dtype=torch.int64, device=dev)
+        prof = torch.zeros(13, dtype=torch.int64, device=dev)
         _native.call("rnnl_debug_profile", prof.data_ptr())
         ev = {}
         model.forward_rows(h, r, None, events=ev)
@@ -43,7 +43,7 @@ def main():
     for name, v in zip(["prologue", "grounding(A)", "candidates(B)"], p[:3]):
         print("  %-14s %10.0f cycles/query" % (name, v / nq))
     for name, v in zip(["B mark+slots", "B count+records", "B scatter", "A node+scan", "A item+scan",
-                        "A edges"], p[6:12]):
+                        "A edges", "A compaction"], p[6:13]):
         print("  %-14s %10.0f cycles/query" % (name, v / nq))
     print("events ms: nodes %.3f base %.3f ground %.3f" % (ev["start"].elapsed_time(ev["base"]),
           ev["base"].elapsed_time(ev["ground"]), ev["ground"].elapsed_time(ev["end"])))
