@@ -14,8 +14,7 @@
 namespace rnnl {
 
 constexpr int BS = 256;        // threads per workgroup (scoring kernels)
-constexpr int GBS = 256;       // threads per grounding workgroup
-constexpr int GNW = GBS / 64;  // its waves
+constexpr int GBS = 256;       // threads per grounding workgroup (WIDE_ROWS launches: 1024)
 constexpr int HBITS = 12;
 constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count)
 constexpr int OCC_CAP = 1024;     // phase-A occupied-slot list (fuller levels scan all HCAP slots)
@@ -29,10 +28,11 @@ constexpr int WG_PER_CU = 3;           // grounding workgroups per CU (LDS-bound
 constexpr int NUM_CU = 256;
 constexpr int SCORE_WG_PER_CU = 8;     // scoring workgroups per CU (full grid)
 constexpr int EMPTY = -1;
+constexpr int WIDE_ROWS = 256;  // launches of at most this many rows ground with 1024-lane workgroups
 // Phase-B hash passes rank their candidates by entity through an LDS bitmap
 // over the pass's entity range (it shares phase A's per-thread arrays, 36 B
-// per thread): ranges up to SORT_WORDS x 32 entities (49,152 at GBS = 256).
-constexpr int SORT_WORDS = (9 * GBS * 4 / 6) & ~(GBS - 1);
+// per thread): ranges up to sort_words(G) x 32 entities (49,152 at G = 256).
+constexpr int sort_words(int G) { return (9 * G * 4 / 6) & ~(G - 1); }
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
 enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6, H_NCAND = 8 };
@@ -194,8 +194,10 @@ inline Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   return L;
 }
 
-// Exclusive block scan of one int per thread (GBS threads); `total` gets the block sum.
+// Exclusive block scan of one int per thread (G threads); `total` gets the block sum.
+template <int G>
 __device__ __forceinline__ int block_scan(int x, int *s_ws, int &total) {
+  constexpr int GNW = G / 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int v = x;
 #pragma unroll
@@ -221,8 +223,8 @@ __device__ __forceinline__ int block_scan(int x, int *s_ws, int &total) {
   return res;
 }
 
-// Largest i in [0, n) with a[i] <= k, n <= GBS, for a non-decreasing a of
-// GBS entries with a[0] <= k and a[i] > k for every i >= n — the block
+// Largest i in [0, n) with a[i] <= k, n <= G, for a non-decreasing a of
+// G entries (the workgroup's lanes) with a[0] <= k and a[i] > k for every i >= n — the block
 // scans' exclusive prefixes: threads past n add nothing, so their prefix is
 // the total, > k.  Branch-free: ceil(log2 n) steps of one LDS read, a
 // compare and a select (the bisection's bounds bookkeeping cost ~7 VALU

@@ -29,7 +29,8 @@ namespace rnnl {
 unsigned long long *g_prof = nullptr;
 int64_t g_fcap_base = FCAP_BASE, g_pcap_base = PCAP_BASE, g_pool_per_query = POOL_PER_QUERY;
 
-struct __align__(16) Smem {
+template <int G>
+struct __align__(16) SmemT {
   union {
     struct {
       int key[HCAP];
@@ -50,20 +51,20 @@ struct __align__(16) Smem {
   } u;
   union {
     struct {  // phase A: per-thread frontier items and edge batches
-      int ent_v[GBS], ent_fch[GBS], item_off[GBS];
-      uint32_t ent_c[GBS];
-      int it_child[GBS], it_beg[GBS], it_flags[GBS], edge_off[GBS];
-      uint32_t it_c[GBS];
+      int ent_v[G], ent_fch[G], item_off[G];
+      uint32_t ent_c[G];
+      int it_child[G], it_beg[G], it_flags[G], edge_off[G];
+      uint32_t it_c[G];
       // the hash slots occupied at this level, in insertion order (the first
       // OCC_CAP): the level's compaction walks them instead of all HCAP slots
       unsigned short occ[OCC_CAP];
     };
     struct {  // phase B: entity bitmap of one hash pass and its popcount prefix (candidate ranks)
-      uint32_t sbits[SORT_WORDS];
-      unsigned short spre[SORT_WORDS];
+      uint32_t sbits[sort_words(G)];
+      unsigned short spre[sort_words(G)];
     };
   };
-  int ws[GNW + 1];
+  int ws[(G / 64) + 1];
   int q, nd, np, ovf, err, root, nocc;
   long long qbase;
   unsigned long long t0;
@@ -72,7 +73,8 @@ struct __align__(16) Smem {
   unsigned long long tp[8];  // diagnostic sub-phase cycles (thread 0)
 };
 
-__device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pcap, uint32_t key, uint32_t c) {
+template <int G>
+__device__ __forceinline__ void emit_contrib(SmemT<G> &S, const Slot &sl, int64_t pcap, uint32_t key, uint32_t c) {
   const int pos = atomicAdd(&S.np, 1);
   if (pos < pcap) {
     sl.ct[pos] = Ent{key, c};
@@ -81,7 +83,8 @@ __device__ __forceinline__ void emit_contrib(Smem &S, const Slot &sl, int64_t pc
   }
 }
 
-__device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, int64_t fcap, uint32_t key,
+template <int G>
+__device__ __forceinline__ void emit_frontier(SmemT<G> &S, const Slot &sl, int buf, int64_t fcap, uint32_t key,
                                               uint32_t c) {
   const int pos = atomicAdd(&S.nd, 1);
   if (pos < fcap) {
@@ -92,7 +95,8 @@ __device__ __forceinline__ void emit_frontier(Smem &S, const Slot &sl, int buf, 
 }
 
 // (node, entity) += c in the phase-A hash; false if the table is full.
-__device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
+template <int G>
+__device__ __forceinline__ bool hash_add(SmemT<G> &S, int key, uint32_t c) {
   uint32_t h = hash32((uint32_t)key) >> (32 - HBITS);
 #pragma unroll 1
   for (int probe = 0; probe < 64; ++probe) {
@@ -115,7 +119,8 @@ __device__ __forceinline__ bool hash_add(Smem &S, int key, uint32_t c) {
 // run longer than kWatchdogTicks of the 100 MHz real-time clock; thread 0
 // then flags S.err.  Guarantees every wave reaches the kernel exit.
 constexpr unsigned long long kWatchdogTicks = 200000000ull;  // 2 s
-__device__ __forceinline__ bool watchdog(Smem &S) {
+template <int G>
+__device__ __forceinline__ bool watchdog(SmemT<G> &S) {
   if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - S.t0 > kWatchdogTicks) atomicOr(&S.err, ERR_WATCHDOG);
   __syncthreads();
   return S.err != 0;
@@ -131,7 +136,8 @@ __device__ __forceinline__ bool watchdog(Smem &S) {
   } while (0)
 
 // ---------------------------------------------------------------- phase A
-__device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, int r, int root, int rm_src,
+template <int G>
+__device__ void ground_query(const KParams &p, SmemT<G> &S, const Slot &sl, int h, int r, int root, int rm_src,
                              int rm_dst) {
   const int tid = threadIdx.x;
   const int depth = p.rl.head_depth[r];
@@ -144,9 +150,9 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
   int cur = 0, n_prev = 1;
   for (int d = 1; d <= depth; ++d) {
     const int nxt = cur ^ 1;
-    for (int cb = 0; cb < n_prev; cb += GBS) {
+    for (int cb = 0; cb < n_prev; cb += G) {
       if (watchdog(S)) break;
-      const int ne = min(GBS, n_prev - cb);
+      const int ne = min(G, n_prev - cb);
       int nch = 0;
       if (tid < ne) {
         const Ent fe = sl.f(cur)[cb + tid];
@@ -158,11 +164,11 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
         nch = ni.z;
       }
       int NI;
-      const int ioff = block_scan(nch, S.ws, NI);
+      const int ioff = block_scan<G>(nch, S.ws, NI);
       S.item_off[tid] = ioff;
       __syncthreads();
       PSTAMP(3);
-      for (int ib = 0; ib < NI; ib += GBS) {
+      for (int ib = 0; ib < NI; ib += G) {
         const int k = ib + tid;
         int deg = 0;
         if (k < NI) {
@@ -189,15 +195,15 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
                             (rel == r && v == rm_src ? 4 : 0);
         }
         int NE;
-        const int eoff = block_scan(deg, S.ws, NE);
+        const int eoff = block_scan<G>(deg, S.ws, NE);
         S.edge_off[tid] = eoff;
         __syncthreads();
         PSTAMP(4);
-        const int nit = min(GBS, NI - ib);
+        const int nit = min(G, NI - ib);
         // one edge per lane per pass: the edge -> item map is a binary search of
         // the items' edge offsets (2 / 4 edges per lane measured no faster: the
         // loop is bound by its barriers and dependent loads)
-        for (int eb = 0; eb < NE; eb += GBS) {
+        for (int eb = 0; eb < NE; eb += G) {
           const int j = eb + tid;
           if (j < NE) {
             const int it = upper_idx(S.edge_off, nit, j);
@@ -220,14 +226,14 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
     // compact the hash into the next frontier and clear it
     const int nocc = S.nocc;  // uniform: read after the edge loop's barrier
     if (nocc <= OCC_CAP) {  // the listed slots only (small frontiers: most levels)
-      for (int i = tid; i < nocc; i += GBS) {
+      for (int i = tid; i < nocc; i += G) {
         const int s2 = S.occ[i];
         emit_frontier(S, sl, nxt, p.fcap, (uint32_t)S.u.a.key[s2], S.u.a.val[s2]);
         S.u.a.key[s2] = EMPTY;
         S.u.a.val[s2] = 0u;
       }
     } else {
-      for (int s2 = tid; s2 < HCAP; s2 += GBS) {
+      for (int s2 = tid; s2 < HCAP; s2 += G) {
         const int k = S.u.a.key[s2];
         if (k != EMPTY) {
           emit_frontier(S, sl, nxt, p.fcap, (uint32_t)k, S.u.a.val[s2]);
@@ -251,15 +257,17 @@ __device__ void ground_query(const KParams &p, Smem &S, const Slot &sl, int h, i
 
 // ---------------------------------------------------------------- phase B
 // PNA degree += count x rules at the node (u32 in LDS), carry-checked.
-__device__ __forceinline__ void degree_add(Smem &S, uint32_t *cell, uint32_t c, int nrules) {
+template <int G>
+__device__ __forceinline__ void degree_add(SmemT<G> &S, uint32_t *cell, uint32_t c, int nrules) {
   const uint64_t v = (uint64_t)c * (uint32_t)nrules;
   const uint32_t old = atomicAdd(cell, (uint32_t)v);
   if ((v >> 32) || old + (uint32_t)v < old) atomicOr(&S.err, ERR_COUNT_WIDTH);
 }
 
 // Exclusive scan of WIN ints in place (PER consecutive per thread); returns the total.
+template <int G>
 __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
-  constexpr int PER = WIN / GBS;
+  constexpr int PER = WIN / G;
   const int tid = threadIdx.x;
   int loc[PER];
   int sum = 0;
@@ -269,7 +277,7 @@ __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
     sum += loc[j];
   }
   int total;
-  int base = block_scan(sum, s_ws, total);
+  int base = block_scan<G>(sum, s_ws, total);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     a[tid * PER + j] = base;
@@ -283,19 +291,20 @@ __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
 // candidate records for it are written at pool indices cbase + [0, nc) and
 // its buckets at pool indices qbase + beg + [0, end - beg).  degree_only (PNA
 // sweep 1) accumulates sum log(degree) instead.  Returns nc.
-__device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, int beg, int end, int64_t cbase,
+template <int G>
+__device__ int window_pass(const KParams &p, SmemT<G> &S, const Slot &sl, int lo, int beg, int end, int64_t cbase,
                            bool degree_only) {
   const int tid = threadIdx.x;
   const Ent *w = sl.f(0);  // window-sorted contributions: a = entity, b = node, c = count
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
-  for (int i = tid; i < WIN; i += GBS) S.u.b.map[i] = 0;
+  for (int i = tid; i < WIN; i += G) S.u.b.map[i] = 0;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) S.u.b.map[(int)(w[i].k & p.emask) - lo] = 1;  // mark present entities
+  for (int i = beg + tid; i < end; i += G) S.u.b.map[(int)(w[i].k & p.emask) - lo] = 1;  // mark present entities
   __syncthreads();
-  for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = S.u.b.map[i];
+  for (int i = tid; i < WIN; i += G) S.u.b.cnt[i] = S.u.b.map[i];
   __syncthreads();
-  const int nc = scan_win(S.u.b.cnt, S.ws);  // slots in ascending entity order
-  for (int i = tid; i < WIN; i += GBS) {
+  const int nc = scan_win<G>(S.u.b.cnt, S.ws);  // slots in ascending entity order
+  for (int i = tid; i < WIN; i += G) {
     if (S.u.b.map[i]) {
       const int slot = S.u.b.cnt[i];
       S.u.b.map[i] = slot;
@@ -303,37 +312,37 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
     }
   }
   __syncthreads();
-  for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = 0;
+  for (int i = tid; i < WIN; i += G) S.u.b.cnt[i] = 0;
   __syncthreads();
   PSTAMP(0);
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
-    for (int i = beg + tid; i < end; i += GBS)
+    for (int i = beg + tid; i < end; i += G)
       degree_add(S, reinterpret_cast<uint32_t *>(&S.u.b.cnt[S.u.b.map[(int)(w[i].k & p.emask) - lo]]), w[i].c,
                  p.rl.node_nrules[S.root + (int)(w[i].k >> p.ebits)]);
     __syncthreads();
-    for (int s2 = tid; s2 < nc; s2 += GBS) {
+    for (int s2 = tid; s2 < nc; s2 += G) {
       const float degf = (float)((double)(uint32_t)S.u.b.cnt[s2] + 1.0);
       atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
     }
     __syncthreads();
     return nc;
   }
-  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.b.cnt[S.u.b.map[(int)(w[i].k & p.emask) - lo]], 1);  // bucket sizes
+  for (int i = beg + tid; i < end; i += G) atomicAdd(&S.u.b.cnt[S.u.b.map[(int)(w[i].k & p.emask) - lo]], 1);  // bucket sizes
   __syncthreads();
-  for (int i = tid; i < WIN; i += GBS) S.u.b.off[i] = S.u.b.cnt[i];
+  for (int i = tid; i < WIN; i += G) S.u.b.off[i] = S.u.b.cnt[i];
   __syncthreads();
-  scan_win(S.u.b.off, S.ws);
+  scan_win<G>(S.u.b.off, S.ws);
   // candidate records
   const int64_t qb = S.qbase;
-  for (int s2 = tid; s2 < nc; s2 += GBS) {
+  for (int s2 = tid; s2 < nc; s2 += G) {
     p.cand[cbase + s2] = make_int4(S.u.b.st[s2], (int32_t)(qb + beg + S.u.b.off[s2]), S.u.b.cnt[s2], 0);
   }
   __syncthreads();
-  for (int i = tid; i < WIN; i += GBS) S.u.b.cnt[i] = 0;
+  for (int i = tid; i < WIN; i += G) S.u.b.cnt[i] = 0;
   __syncthreads();
   PSTAMP(1);
-  for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
+  for (int i = beg + tid; i < end; i += G) {  // scatter (node, count) into the buckets
     const int s2 = S.u.b.map[(int)(w[i].k & p.emask) - lo];
     const int64_t pos = qb + beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
     p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
@@ -350,10 +359,11 @@ __device__ int window_pass(const KParams &p, Smem &S, const Slot &sl, int lo, in
 // through an LDS bitmap of the pass's entity range, as window_pass's slots
 // are), so a query's candidate records — and the scoring pass's score
 // accesses, one lane per candidate — run along the score row; a range wider
-// than SORT_WORDS x 32 entities keeps the hash order (nothing downstream
+// than sort_words(G) x 32 entities keeps the hash order (nothing downstream
 // depends on the order for correctness: scores scatter by entity, PNA's mean
 // and the digests are order-independent sums).
-__device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
+template <int G>
+__device__ __forceinline__ int hb_slot(SmemT<G> &S, int t, bool insert) {
   uint32_t h = hash32((uint32_t)t) >> (32 - WBITS);
 #pragma unroll 1
   for (int probe = 0; probe < HB; ++probe) {
@@ -364,7 +374,8 @@ __device__ __forceinline__ int hb_slot(Smem &S, int t, bool insert) {
   return -1;  // unreachable: at most HB_LOAD < HB distinct keys
 }
 
-__device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int end, int64_t cbase,
+template <int G>
+__device__ int hash_pass(const KParams &p, SmemT<G> &S, const Ent *w, int beg, int end, int64_t cbase,
                          bool degree_only, int lo, int hi) {
   // w: contributions (a = entity, b = node, c = count), window-sorted or raw;
   // every entity lies in [lo, hi)
@@ -372,34 +383,34 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
   const int w0 = lo >> 5, nw = ((hi - 1) >> 5) - w0 + 1;
   // candidates in ascending entity order (the reference's nonzero order, and
   // neighbouring lanes of the scoring pass then touch neighbouring score entries)
-  const bool by_rank = !degree_only && nw <= SORT_WORDS;
-  for (int i = tid; i < HB; i += GBS) {
+  const bool by_rank = !degree_only && nw <= sort_words(G);
+  for (int i = tid; i < HB; i += G) {
     S.u.c.key[i] = EMPTY;
     S.u.c.cnt[i] = 0;
     S.u.c.off[i] = 0;
   }
   if (by_rank)
-    for (int i = tid; i < nw; i += GBS) S.sbits[i] = 0u;
+    for (int i = tid; i < nw; i += G) S.sbits[i] = 0u;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) atomicAdd(&S.u.c.cnt[hb_slot(S, (int)(w[i].k & p.emask), true)], 1);
+  for (int i = beg + tid; i < end; i += G) atomicAdd(&S.u.c.cnt[hb_slot(S, (int)(w[i].k & p.emask), true)], 1);
   __syncthreads();
-  constexpr int PER = HB / GBS;
+  constexpr int PER = HB / G;
   int loc[PER];
   int nc;
   if (by_rank) {
-    for (int i = tid; i < HB; i += GBS) {
+    for (int i = tid; i < HB; i += G) {
       const int k = S.u.c.key[i];
       if (k != EMPTY) atomicOr(&S.sbits[(k >> 5) - w0], 1u << (k & 31));
     }
     __syncthreads();
     // rank of a bit = popcounts of the words before it + of its word below it
-    const int per = (nw + GBS - 1) / GBS;
+    const int per = (nw + G - 1) / G;
     int sum = 0;
     for (int j = 0; j < per; ++j) {
       const int i = tid * per + j;
       if (i < nw) sum += __popc(S.sbits[i]);
     }
-    int base = block_scan(sum, S.ws, nc);
+    int base = block_scan<G>(sum, S.ws, nc);
     for (int j = 0; j < per; ++j) {
       const int i = tid * per + j;
       if (i < nw) {
@@ -408,7 +419,7 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
       }
     }
     __syncthreads();
-    for (int i = tid; i < HB; i += GBS) {
+    for (int i = tid; i < HB; i += G) {
       const int k = S.u.c.key[i];
       if (k != EMPTY) {
         const int kk = k - (w0 << 5), wd = kk >> 5;
@@ -426,7 +437,7 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
       s2 += loc[j];
     }
     int tot;
-    int run = block_scan(s2, S.ws, tot);
+    int run = block_scan<G>(s2, S.ws, tot);
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       S.u.c.off[tid * PER + j] = run;
@@ -443,7 +454,7 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
       sum += loc[j];
     }
     int total;
-    int run = block_scan(sum, S.ws, total);
+    int run = block_scan<G>(sum, S.ws, total);
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int sidx = tid * PER + j;
@@ -456,13 +467,13 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
   }
   if (degree_only) {
     // PNA sweep 1: degree = 1 + sum_rho count (layers.py:99) per candidate
-    for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
+    for (int i = tid; i < HB; i += G) S.u.c.cnt[i] = 0;
     __syncthreads();
-    for (int i = beg + tid; i < end; i += GBS)
+    for (int i = beg + tid; i < end; i += G)
       degree_add(S, reinterpret_cast<uint32_t *>(&S.u.c.cnt[hb_slot(S, (int)(w[i].k & p.emask), false)]), w[i].c,
                  p.rl.node_nrules[S.root + (int)(w[i].k >> p.ebits)]);
     __syncthreads();
-    for (int i = tid; i < HB; i += GBS) {
+    for (int i = tid; i < HB; i += G) {
       if (S.u.c.key[i] != EMPTY) {
         const float degf = (float)((double)(uint32_t)S.u.c.cnt[i] + 1.0);
         atomicAdd(&S.sumlog, (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
@@ -473,7 +484,7 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
   }
   // bucket start of hash slot i: off is indexed by rank (by_rank) or by slot
   const int64_t qb = S.qbase;
-  for (int i = tid; i < HB; i += GBS) {
+  for (int i = tid; i < HB; i += G) {
     if (S.u.c.key[i] != EMPTY) {
       const int cid = S.u.c.cid[i];
       const int64_t c = cbase + cid;
@@ -481,9 +492,9 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
     }
   }
   __syncthreads();
-  for (int i = tid; i < HB; i += GBS) S.u.c.cnt[i] = 0;
+  for (int i = tid; i < HB; i += G) S.u.c.cnt[i] = 0;
   __syncthreads();
-  for (int i = beg + tid; i < end; i += GBS) {  // scatter (node, count) into the buckets
+  for (int i = beg + tid; i < end; i += G) {  // scatter (node, count) into the buckets
     const int sl2 = hb_slot(S, (int)(w[i].k & p.emask), false);
     const int64_t pos = qb + beg + S.u.c.off[by_rank ? S.u.c.cid[sl2] : sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
     p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
@@ -494,16 +505,17 @@ __device__ int hash_pass(const KParams &p, Smem &S, const Ent *w, int beg, int e
 
 // Counting sort of the contributions by entity window into fn/fv/fc[0]
 // (free during phase B), then window_pass over every non-empty window.
-__device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P, bool degree_only, bool sorted) {
+template <int G>
+__device__ int candidates_phase(const KParams &p, SmemT<G> &S, const Slot &sl, int P, bool degree_only, bool sorted) {
   const int tid = threadIdx.x;
   // all contributions fit one hash pass: no window sort (it exists only to
   // bound the hash load) — one read of the raw list instead of a sorted copy
   if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only, 0, p.g.E) : 0;
   const int nwin = (p.g.E + WIN - 1) >> WBITS;
   if (!sorted) {
-    for (int i = tid; i < nwin; i += GBS) S.whist[i] = 0;
+    for (int i = tid; i < nwin; i += G) S.whist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < P; i += GBS) atomicAdd(&S.whist[(int)(sl.ct[i].k & p.emask) >> WBITS], 1);
+    for (int i = tid; i < P; i += G) atomicAdd(&S.whist[(int)(sl.ct[i].k & p.emask) >> WBITS], 1);
     __syncthreads();
     if (tid == 0) {
       int acc = 0;
@@ -516,7 +528,7 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
       S.wbeg[nwin] = acc;
     }
     __syncthreads();
-    for (int i = tid; i < P; i += GBS) {
+    for (int i = tid; i < P; i += G) {
       const Ent ce = sl.ct[i];
       const int t = (int)(ce.k & p.emask);
       const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
@@ -544,7 +556,8 @@ __device__ int candidates_phase(const KParams &p, Smem &S, const Slot &sl, int P
   return ncand;
 }
 
-__device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, Smem &S, int q) {
+template <int G>
+__device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, SmemT<G> &S, int q) {
   atomicOr(&hdr[H_STATUS], S.err ? 2u : 1u);
   if (S.err) {
     atomicOr(&hdr[H_ERRBITS], (unsigned)S.err);
@@ -553,14 +566,14 @@ __device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, 
   if (p.n_cand) p.n_cand[q] = S.err ? -2 : -1;
 }
 
-template <int AGG>
-__global__ __launch_bounds__(GBS) void ground_kernel(KParams p) {
-  __shared__ Smem S;
+template <int AGG, int G>
+__global__ __launch_bounds__(G) void ground_kernel(KParams p) {
+  __shared__ SmemT<G> S;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
   unsigned long long *pool_ctr = reinterpret_cast<unsigned long long *>(p.ws + 64);
   const Slot sl = make_slot(p.slots, blockIdx.x, p.fcap, p.pcap);
-  for (int s = tid; s < HCAP; s += GBS) {
+  for (int s = tid; s < HCAP; s += G) {
     S.u.a.key[s] = EMPTY;
     S.u.a.val[s] = 0u;
   }
@@ -624,7 +637,7 @@ __global__ __launch_bounds__(GBS) void ground_kernel(KParams p) {
     }
     __syncthreads();
     if (S.ovf || P > p.pcap || S.err) {
-      for (int s = tid; s < HCAP; s += GBS) {  // leave the LDS hash clean for the next query
+      for (int s = tid; s < HCAP; s += G) {  // leave the LDS hash clean for the next query
         S.u.a.key[s] = EMPTY;
         S.u.a.val[s] = 0u;
       }
@@ -657,7 +670,7 @@ __global__ __launch_bounds__(GBS) void ground_kernel(KParams p) {
         pr[5] += ncand;
       }
     }
-    for (int s = tid; s < HCAP; s += GBS) {  // restore the phase-A hash (phase B reused its LDS)
+    for (int s = tid; s < HCAP; s += G) {  // restore the phase-A hash (phase B reused its LDS)
       S.u.a.key[s] = EMPTY;
       S.u.a.val[s] = 0u;
     }
@@ -981,10 +994,18 @@ int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all
 // default occupancy); a smaller grid leaves CUs to a concurrent kernel.
 void launch_ground(const KParams &p, int agg, hipStream_t st, int grid) {
   const unsigned g = (unsigned)(grid > 0 ? std::min(grid, p.nslots) : p.nslots);
-  if (agg == RNNL_AGG_SUM)
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(g), dim3(GBS), 0, st, p);
+  // few rows (a reference batch per call): one 1024-lane workgroup per query,
+  // so the batch's heaviest query — the launch's critical path — expands
+  // four times the frontier items and edges per pass
+  const bool wide = p.nq <= WIDE_ROWS;
+  if (agg == RNNL_AGG_SUM && wide)
+    hipLaunchKernelGGL((ground_kernel<RNNL_AGG_SUM, 1024>), dim3(g), dim3(1024), 0, st, p);
+  else if (agg == RNNL_AGG_SUM)
+    hipLaunchKernelGGL((ground_kernel<RNNL_AGG_SUM, GBS>), dim3(g), dim3(GBS), 0, st, p);
+  else if (wide)
+    hipLaunchKernelGGL((ground_kernel<RNNL_AGG_PNA, 1024>), dim3(g), dim3(1024), 0, st, p);
   else
-    hipLaunchKernelGGL(ground_kernel<RNNL_AGG_PNA>, dim3(g), dim3(GBS), 0, st, p);
+    hipLaunchKernelGGL((ground_kernel<RNNL_AGG_PNA, GBS>), dim3(g), dim3(GBS), 0, st, p);
 }
 
 void set_score_params(KParams &p, const rnnl_predictor_params *pp, float *score, uint8_t *mask,
@@ -1145,7 +1166,7 @@ int rnnl_ground(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t 
   RNNL_HIP_CHECK(hipMemsetAsync(ws, 0, HDR_WORDS_BYTES, st));
   if (nq == 0) return RNNL_OK;
   p.agg = RNNL_AGG_SUM;
-  hipLaunchKernelGGL(ground_kernel<RNNL_AGG_SUM>, dim3(p.nslots), dim3(GBS), 0, st, p);
+  launch_ground(p, RNNL_AGG_SUM, st);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
