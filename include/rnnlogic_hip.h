@@ -194,6 +194,14 @@ int rnnl_forward_status_totals(void *workspace, void *stream, int64_t *totals);
  * for rnnl_forward_status_totals (nullable). */
 int rnnl_forward_header_bytes(size_t *bytes);
 int rnnl_forward_status_host(const void *header, int64_t *totals);
+/* The status with the launch's flags from the same read-back (totals and
+ * flags nullable): flags bit 0 (RNNL_FLAG_MIXED) = the rows hold more than one
+ * relation — the reference forward's one-relation-per-batch assertion
+ * (predictors.py:54-55, 211-212) without a separate reduction.  The _host
+ * form decodes the flags of a header copy. */
+#define RNNL_FLAG_MIXED 1
+int rnnl_forward_status_flags(void *workspace, void *stream, int64_t *totals, uint32_t *flags);
+int rnnl_forward_flags_host(const void *header, uint32_t *flags);
 /* Grounding only (reference data.py:136-173 for every rule of every row,
  * predictors.py:221-244): fills the workspace's COO of the stacked rule_count
  * matrix and n_cand (per row candidate count, -1/-2 on overflow/error; check
@@ -361,6 +369,16 @@ int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const
  * of row_keys[i] in a CSR map (keys ascending, offs n_keys + 1, vals int32).
  * A key not in the map gives a zero row.  With keys = r * |E| + h and the
  * hr2o lists this is TrainDataset's `target`. */
+/* One training batch (TrainDataset.__getitem__, data.py:201-219) in one
+ * launch: rows row0 .. row0 + n_rows - 1 of the (n, 3) int64 (h, r, t) table
+ * into out_h / out_r / out_t, each row's own relation-local edge id into
+ * out_etr (the sorted edge keys (r |E| + t) |E| + h and their ids:
+ * relation2ht2index), and the multi-hot target over hr2o (the CSR of
+ * rnnl_multi_hot) into out_target (n_rows x n_entities floats). */
+int rnnl_train_batch(const int64_t *table, int64_t row0, int32_t n_rows, const int64_t *keys, const int64_t *offs,
+                     const int32_t *vals, int64_t n_keys, const int64_t *edge_keys, const int64_t *edge_ids,
+                     int64_t n_edges, int32_t n_entities, int64_t *out_h, int64_t *out_r, int64_t *out_t,
+                     int64_t *out_etr, float *out_target, void *stream);
 int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
                    const int64_t *row_keys, int32_t n_rows, int32_t width, float *out, void *stream);
 

@@ -18,6 +18,7 @@ RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL
 AGG_SUM, AGG_PNA = 0, 1
 FEATURE_ADD, FEATURE_NONE = 0, 1
 ROTATE_DIRECT, ROTATE_MFMA = 0, 1
+FLAG_MIXED = 1
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -50,6 +51,8 @@ SIGNATURES = [
     ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_forward_header_bytes", ctypes.c_int, [_P]),
     ("rnnl_forward_status_host", ctypes.c_int, [_P, _P]),
+    ("rnnl_forward_status_flags", ctypes.c_int, [_P, _P, _P, _P]),
+    ("rnnl_forward_flags_host", ctypes.c_int, [_P, _P]),
     ("rnnl_ground", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _P]),
     ("rnnl_ground_export_candidates", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     ("rnnl_ground_export_entries", ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
@@ -73,6 +76,8 @@ SIGNATURES = [
     ("rnnl_rotate_relation_table", ctypes.c_int, [_P, _I32, _I32, _F32, _P, _P]),
     ("rnnl_rotate_workspace_size", ctypes.c_int, [_I32, _I32, _I32, _I32, _P]),
     ("rnnl_multi_hot", ctypes.c_int, [_P, _P, _P, _I64, _P, _I32, _I32, _P, _P]),
+    ("rnnl_train_batch", ctypes.c_int,
+     [_P, _I64, _I32, _P, _P, _P, _I64, _P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P]),
     ("rnnl_filter_flags", ctypes.c_int, [_P, _P, _P, _I64, _P, _I32, _I32, _P, _P]),
     ("rnnl_filtered_ranks", ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _P, _P, _P]),
     ("rnnl_miner_create", ctypes.c_int, [_P, _I64, _I32, _I32, _P]),

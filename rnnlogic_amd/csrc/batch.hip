@@ -103,7 +103,80 @@ __global__ __launch_bounds__(256) void filtered_ranks_kernel(const float *__rest
   }
 }
 
+// First index in [0, n) with a[i] >= k (n if none).
+__device__ __forceinline__ int64_t lower_bound64(const int64_t *__restrict__ a, int64_t n, int64_t k) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// One TrainDataset batch (data.py:201-219) from the device row table in one
+// launch: row i of the batch is table[row0 + i] = (h, r, t); out_h / out_r /
+// out_t receive it, out_etr the relation-local id of its own edge (key
+// (r |E| + t) |E| + h in the sorted edge-key table, as torch.searchsorted
+// with the index clamped), and out_target row i the multi-hot row of hr2o.
+__global__ __launch_bounds__(256) void train_batch_kernel(const int64_t *__restrict__ table, int64_t row0,
+                                                          const int64_t *__restrict__ keys,
+                                                          const int64_t *__restrict__ offs,
+                                                          const int32_t *__restrict__ vals, int64_t n_keys,
+                                                          const int64_t *__restrict__ edge_keys,
+                                                          const int64_t *__restrict__ edge_ids, int64_t n_edges,
+                                                          int32_t E, int64_t *__restrict__ out_h,
+                                                          int64_t *__restrict__ out_r, int64_t *__restrict__ out_t,
+                                                          int64_t *__restrict__ out_etr,
+                                                          float *__restrict__ out_target) {
+  __shared__ int64_t s_beg, s_end;
+  const int row = blockIdx.x;
+  float *o = out_target + (int64_t)row * E;
+  for (int i = threadIdx.x; i < E; i += blockDim.x) o[i] = 0.f;
+  if (threadIdx.x == 0) {
+    const int64_t *hrt = table + 3 * (row0 + row);
+    const int64_t h = hrt[0], r = hrt[1], t = hrt[2];
+    out_h[row] = h;
+    out_r[row] = r;
+    out_t[row] = t;
+    const int64_t k = r * E + h;
+    const int64_t lo = lower_bound64(keys, n_keys, k);
+    const bool hit = lo < n_keys && keys[lo] == k;
+    s_beg = hit ? offs[lo] : 0;
+    s_end = hit ? offs[lo + 1] : 0;
+    const int64_t pos = min(lower_bound64(edge_keys, n_edges, (r * E + t) * E + h), max(n_edges - 1, (int64_t)0));
+    out_etr[row] = n_edges > 0 ? edge_ids[pos] : 0;
+  }
+  // the fill must land before another wave's store to the same address
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int64_t i = s_beg + threadIdx.x; i < s_end; i += blockDim.x) {
+    const int v = vals[i];
+    if (v >= 0 && v < E) o[v] = 1.f;
+  }
+}
+
 extern "C" {
+
+int rnnl_train_batch(const int64_t *table, int64_t row0, int32_t n_rows, const int64_t *keys, const int64_t *offs,
+                     const int32_t *vals, int64_t n_keys, const int64_t *edge_keys, const int64_t *edge_ids,
+                     int64_t n_edges, int32_t n_entities, int64_t *out_h, int64_t *out_r, int64_t *out_t,
+                     int64_t *out_etr, float *out_target, void *stream) {
+  if (!table || row0 < 0 || n_rows < 0 || n_entities <= 0 || n_keys < 0 || n_edges < 0 ||
+      (n_keys > 0 && (!keys || !offs || !vals)) || (n_edges > 0 && (!edge_keys || !edge_ids)) ||
+      (n_rows > 0 && (!out_h || !out_r || !out_t || !out_etr || !out_target))) {
+    set_error("rnnl_train_batch: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (n_rows == 0) return RNNL_OK;
+  hipLaunchKernelGGL(train_batch_kernel, dim3(n_rows), dim3(256), 0, (hipStream_t)stream, table, row0, keys, offs,
+                     vals, n_keys, edge_keys, edge_ids, n_edges, n_entities, out_h, out_r, out_t, out_etr,
+                     out_target);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
 
 int rnnl_multi_hot(const int64_t *keys, const int64_t *offs, const int32_t *vals, int64_t n_keys,
                    const int64_t *row_keys, int32_t n_rows, int32_t width, float *out, void *stream) {

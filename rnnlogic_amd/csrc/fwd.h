@@ -35,7 +35,11 @@ constexpr int WIDE_ROWS = 256;  // launches of at most this many rows ground wit
 constexpr int sort_words(int G) { return (9 * G * 4 / 6) & ~(G - 1); }
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
-enum { H_STATUS = 0, H_DEQUEUE = 1, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6, H_NCAND = 8 };
+enum { H_STATUS = 0, H_DEQUEUE = 1, H_FLAGS = 2, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6, H_NCAND = 8 };
+// H_FLAGS bit 0: the launch's rows hold more than one relation (the
+// reference forward's one-relation-per-batch check, predictors.py:54-55 /
+// 211-212, read back with the status instead of a separate reduction)
+enum { FLAG_MIXED = 1 };
 // (64-bit words: H_CHUNKS the scoring chunk total, H_NCAND the candidate total of the grounding)
 // H_ERRBITS: 4 watchdog, 8 a path count or PNA degree reached 2^32 (the u32
 // sums would wrap), 16 the node-weight table is out of its fixed-point range

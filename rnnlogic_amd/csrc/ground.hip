@@ -591,6 +591,7 @@ __global__ __launch_bounds__(G) void ground_kernel(KParams p) {
     const int h = (int)p.all_h[q];
     const int r = (int)p.all_r[q];
     const int root = p.rl.head_root[r];
+    if (tid == 0 && r != (int)p.all_r[0]) atomicOr(&hdr[H_FLAGS], (unsigned)FLAG_MIXED);
     if (root < 0) {
       if (tid == 0) {
         p.n_cand[q] = 0;
@@ -1269,6 +1270,27 @@ static int status_from_header(const unsigned int *st, int64_t *totals) {
 }
 
 int rnnl_forward_status(void *ws, void *stream) { return forward_status(ws, stream, nullptr); }
+
+int rnnl_forward_status_flags(void *ws, void *stream, int64_t *totals, uint32_t *flags) {
+  if (!ws) {
+    set_error("rnnl_forward_status_flags: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  unsigned int st[STATUS_WORDS] = {0};
+  RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (flags) *flags = st[H_FLAGS];
+  return status_from_header(st, totals);
+}
+
+int rnnl_forward_flags_host(const void *header, uint32_t *flags) {
+  if (!header || !flags) {
+    set_error("rnnl_forward_flags_host: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *flags = static_cast<const unsigned int *>(header)[H_FLAGS];
+  return RNNL_OK;
+}
 
 int rnnl_forward_header_bytes(size_t *bytes) {
   if (!bytes) {

@@ -303,16 +303,17 @@ class DeviceTrainBatches(object):
         return len(self.train_set)
 
     def __getitem__(self, idx):
-        g = self.train_set.graph
-        E = g.entity_size
-        all_h, all_r, all_t = self.table.batch(self.train_set.batches, idx)
-        B = all_h.numel()
+        E = self.train_set.graph.entity_size
+        tab, lens, off = self.table.get(self.train_set.batches)
+        B = int(lens[idx])
+        out = torch.empty((4, B), dtype=torch.int64, device=self.device)  # h, r, t, edges_to_remove
         target = torch.empty((B, E), dtype=torch.float32, device=self.device)
-        self.hr2o.rows("rnnl_multi_hot", (all_r * E + all_h).contiguous(), E, target)
-        ekey = (all_r * E + all_t) * E + all_h
-        pos = torch.searchsorted(self.edge_keys, ekey).clamp(max=max(self.edge_keys.numel() - 1, 0))
-        etr = self.edge_ids[pos]
-        return all_h, all_r, all_t, target, etr
+        L = self.hr2o
+        _native.call("rnnl_train_batch", tab.data_ptr(), int(off[idx]), B, L.keys.data_ptr(), L.offs.data_ptr(),
+                     L.vals.data_ptr(), L.keys.numel(), self.edge_keys.data_ptr(), self.edge_ids.data_ptr(),
+                     self.edge_keys.numel(), E, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+                     out[3].data_ptr(), target.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+        return out[0], out[1], out[2], target, out[3]
 
 
     def rows(self, idx):

@@ -113,6 +113,21 @@ class _HipGrounding(object):
         etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
         return device, all_h, all_r, etr
 
+    def _status(self, ws, stream, totals=None):
+        """The launch's status (rnnl_forward_status_flags: one read-back), with
+        the grounding's candidate / bucket-entry totals into `totals`
+        (int64[2] numpy array, nullable) and its flags kept in self._flags
+        (bit 0: the rows hold more than one relation)."""
+        rc = _native.lib().rnnl_forward_status_flags(
+            ws.data_ptr(), stream, totals.ctypes.data_as(ctypes.c_void_p) if totals is not None else None,
+            self._flags.ctypes.data_as(ctypes.c_void_p))
+        return rc
+
+    def _check_one_relation(self):
+        """The reference forward's one-relation-per-batch assertion
+        (predictors.py:54-55, 211-212), from the last launch's flags."""
+        assert not (int(self._flags[0]) & _native.FLAG_MIXED), "a batch must hold one relation (predictors.py:54-55)"
+
     def _launch(self, device, nq, run, totals=None):
         """run(ws, scale) launches onto the workspace; retried with a doubled
         capacity_scale while the launch reports overflow.  Returns (ws, scale).
@@ -123,11 +138,7 @@ class _HipGrounding(object):
             scale = self.capacity_scale
             ws = self._workspace(device, nq, scale)
             run(ws, scale)
-            if totals is not None:
-                rc = _native.lib().rnnl_forward_status_totals(ws.data_ptr(), stream,
-                                                             totals.ctypes.data_as(ctypes.c_void_p))
-            else:
-                rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
+            rc = self._status(ws, stream, totals)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
                 logging.info("%s: workspace overflow, capacity_scale -> %d", type(self).__name__,
@@ -269,6 +280,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         self._lin_cache = {}
         self._roots = {}
         self._ws_uses = {}  # per workspace pointer: launches onto it so far
+        self._flags = np.zeros(1, dtype=np.uint32)  # the last launch's header flags (_status)
         self._pf = {}  # per device: training lookahead (prefetch): side stream, workspace ring, queue
         # groundings launched ahead of the training step that needs them
         # (TrainerPredictor.train; 0 turns the lookahead off)
@@ -360,13 +372,12 @@ class Predictor(_HipGrounding, torch.nn.Module):
         _native.call("rnnl_predictor_ground", g, nr.ptr, h.data_ptr(), r.data_ptr(),
                      etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(), ws.numel(),
                      scale, side.cuda_stream)
-        # the grounding's status / totals and the one-relation check, copied to the
+        # the grounding's status / totals and the one-relation flag, copied to the
         # host behind it: the forward reads them without waiting for the current stream
         hb = self._header_bytes()
-        hdr = torch.empty(hb + 1, dtype=torch.uint8, pin_memory=True)
+        hdr = torch.empty(hb, dtype=torch.uint8, pin_memory=True)
         with torch.cuda.stream(side):
-            hdr[:hb].copy_(ws[:hb], non_blocking=True)
-            hdr[hb:].copy_((r != r[0]).any().view(1).to(torch.uint8), non_blocking=True)
+            hdr.copy_(ws[:hb], non_blocking=True)  # status, totals and the one-relation flag
         ev = torch.cuda.Event()
         ev.record(side)
         # the side stream's use of these blocks outlives a dropped queue entry or a
@@ -383,23 +394,25 @@ class Predictor(_HipGrounding, torch.nn.Module):
             self._hdr_bytes = n.value
         return self._hdr_bytes
 
-    def check_deferred(self):
+    def check_deferred(self, keep=0):
         """Raise the scoring pass's own error (an integer range flag) of the
-        last lookahead forward, whose status is read one step late so the
-        host does not wait for the scoring each step.  The training step of
-        that forward has then already run its backward and optimizer step on
-        the flagged scores: the error names it, and a run resumed from a
-        checkpoint written after that step should not trust it."""
-        d = getattr(self, "_deferred_status", None)
-        if d is None:
-            return
-        self._deferred_status = None
-        d[1].synchronize()
-        rc = _native.lib().rnnl_forward_status_host(d[0].data_ptr(), None)
-        if rc != _native.RNNL_OK:
-            raise _native.NativeError(rc, "%s (scoring pass of lookahead forward #%d, read one step late: that "
-                                          "step's backward and optimizer update have already been applied)" % (
-                                              _native.lib().rnnl_last_error().decode(errors="replace"), d[2]))
+        lookahead forwards, whose status is read late so the host does not
+        wait for the scoring: every pending status but the newest `keep`
+        (the training step checks the forward before last, which has long
+        finished; train() checks them all at its end).  The training steps of
+        those forwards have then already run their backward and optimizer
+        step on the flagged scores: the error names the forward, and a run
+        resumed from a checkpoint written after it should not trust it."""
+        q = getattr(self, "_deferred_status", None)
+        while q and len(q) > keep:
+            dh, ev, n = q.popleft()
+            ev.synchronize()
+            rc = _native.lib().rnnl_forward_status_host(dh.data_ptr(), None)
+            if rc != _native.RNNL_OK:
+                q.clear()
+                raise _native.NativeError(rc, "%s (scoring pass of lookahead forward #%d, read late: that step's "
+                                              "backward and optimizer update have already been applied)" % (
+                                                  _native.lib().rnnl_last_error().decode(errors="replace"), n))
 
     def _prefetched(self, device, all_h, all_r, edges_to_remove):
         """The queued grounding of exactly these row tensors, or None (a
@@ -432,12 +445,8 @@ class Predictor(_HipGrounding, torch.nn.Module):
             return (torch.empty((0, E), dtype=torch.float32, device=device),
                     torch.empty((0, E), dtype=torch.bool, device=device),
                     torch.empty(0, dtype=torch.int32, device=device), None, None, 0)
-        self.check_deferred()
+        self.check_deferred(keep=1)
         pre = self._prefetched(device, *raw)
-        mixed = None
-        if single_relation and pre is None:
-            mixed = torch.empty((), dtype=torch.bool, pin_memory=True)
-            mixed.copy_((all_r != all_r[0]).any(), non_blocking=True)
         g, nr = self.graph.device_graph(device), self.native_rules(device)
         node_w = self.node_weights(device)
         stream = torch.cuda.current_stream(device).cuda_stream
@@ -467,8 +476,9 @@ class Predictor(_HipGrounding, torch.nn.Module):
             ev.synchronize()  # that grounding and its header copy, not the later side-stream work
             hb = self._header_bytes()
             rc = _native.lib().rnnl_forward_status_host(hdr.data_ptr(), totals.ctypes.data_as(ctypes.c_void_p))
+            _native.call("rnnl_forward_flags_host", hdr.data_ptr(), self._flags.ctypes.data_as(ctypes.c_void_p))
             if single_relation:
-                assert not bool(hdr[hb]), "a batch must hold one relation (predictors.py:54-55)"
+                self._check_one_relation()
             if rc == _native.RNNL_OK:
                 fill()
                 main = torch.cuda.current_stream(device)
@@ -482,14 +492,16 @@ class Predictor(_HipGrounding, torch.nn.Module):
                 dev_ev = torch.cuda.Event()
                 dev_ev.record(main)
                 self._lookahead_forwards = getattr(self, "_lookahead_forwards", 0) + 1
-                self._deferred_status = (dh, dev_ev, self._lookahead_forwards)
+                if getattr(self, "_deferred_status", None) is None:
+                    self._deferred_status = collections.deque()
+                self._deferred_status.append((dh, dev_ev, self._lookahead_forwards))
                 n_cand = n_cand_pf
             else:  # overflow (or another failure): the one-call path, with its retry
                 pre = None
         if pre is None:
             ws, scale = self._launch(device, nq, run, totals)
-        if mixed is not None:
-            assert not bool(mixed), "a batch must hold one relation (predictors.py:54-55)"
+            if single_relation:
+                self._check_one_relation()
         mask = torch.ones((nq, E), dtype=torch.bool, device=device) if bias_mode else mask8.bool()
         return score, mask, n_cand, ws, scale, int(totals[0])
 
@@ -683,6 +695,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._ws_chunks = {}
         self._side = {}
         self._ws_uses = {}
+        self._flags = np.zeros(1, dtype=np.uint32)  # the last launch's header flags (_status)
         self.capacity_scale = 1
         # RotatE base score (_forward_overlap): the grounding and the scoring
         # pass run on a side stream beside the RotatE kernel, both adding into
@@ -916,7 +929,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                          digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
                          stream)
             rec("end")
-            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), stream)
+            rc = self._status(ws, stream)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
                 logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
@@ -1016,7 +1029,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             # so no cross-stream wait is left pending into the next call
             side.synchronize()
             self._side_streams(device)[1].synchronize()
-            rc = _native.lib().rnnl_forward_status(ws.data_ptr(), main.cuda_stream)
+            rc = self._status(ws, main.cuda_stream)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
                 logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
@@ -1165,19 +1178,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
             assert n_other == 0
             return self.forward_autograd(all_h, all_r, edges_to_remove, query_r=query_r)
-        # eval: the check is copied to pinned memory before the launch and read
-        # after the launch status (its host read), so it costs no extra sync
-        mixed = None
-        if all_r.is_cuda and all_r.numel():
-            key = ("mixed", self._device_index(all_r.device))
-            mixed = self._side.get(key)
-            if mixed is None:  # one pinned flag, reused: it is read before the next call writes it
-                mixed = self._side[key] = torch.empty((), dtype=torch.bool, pin_memory=True)
-            mixed.copy_((all_r != all_r[0]).any(), non_blocking=True)
+        # eval: the grounding kernel flags rows of another relation in the
+        # launch header, read back with the status (no extra reduction or sync)
+        self._flags[0] = 0
         score, mask, n_cand = self.forward_rows(all_h, all_r, edges_to_remove, return_ncand=True)
-        if mixed is not None:
-            torch.cuda.current_stream(all_r.device).synchronize()  # no-op after the status read
-            assert not bool(mixed), "a batch must hold one relation (predictors.py:211-212)"
+        self._check_one_relation()
         if self.entity_feature not in ("bias", "RotatE"):
             # reference early return `mask - float('-inf')` (predictors.py:236-237): +inf
             # where the batch has no candidate (mask all False), without a host read

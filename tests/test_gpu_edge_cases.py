@@ -119,3 +119,32 @@ def test_empty_row_set(kind, umls):
         score, mask = model.forward_rows(e, e, None)
     torch.cuda.synchronize()
     assert tuple(score.shape) == (0, g.entity_size) and tuple(mask.shape) == (0, g.entity_size)
+
+
+def test_mixed_relation_batch_fails_like_the_reference(umls):
+    """forward() keeps the reference's one-relation-per-batch assertion
+    (predictors.py:54-55, 211-212), now read from the grounding launch's
+    header flag: PredictorPlus (fused and overlapped RotatE-free path) and
+    the EM Predictor raise on a batch mixing relations and accept a
+    single-relation batch; forward_rows accepts mixed rows."""
+    from rnnlogic_amd.predictors import Predictor
+    path, graph, _ = umls
+    dev = torch.device("cuda:0")
+    facts = np.asarray(graph.test_facts, dtype=np.int64)
+    r0, r1 = int(facts[0, 1]), int(next(f[1] for f in facts if f[1] != facts[0, 1]))
+    one = facts[facts[:, 1] == r0][:6]
+    mixed = np.concatenate([one[:3], facts[facts[:, 1] == r1][:3]])
+    torch.manual_seed(0)
+    plus = PredictorPlus(graph, type="emb", entity_feature="bias", aggregator="sum")
+    plus.set_rules(datasets.rule_file("umls"))
+    pred = Predictor(graph, entity_feature="bias")
+    pred.set_rules(datasets.rule_file("umls"))
+    plus, pred = plus.to(dev).eval(), pred.to(dev).eval()
+    t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    with torch.no_grad():
+        for model in (plus, pred):
+            model(t(one[:, 0]), t(one[:, 1]), None)
+            with pytest.raises(AssertionError):
+                model(t(mixed[:, 0]), t(mixed[:, 1]), None)
+            model(t(one[:, 0]), t(one[:, 1]), None)  # the flag does not stick
+        plus.forward_rows(t(mixed[:, 0]), t(mixed[:, 1]), None)
