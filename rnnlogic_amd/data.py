@@ -80,6 +80,7 @@ class KnowledgeGraph(object):
             self.relation2adjacency.append([index, torch.ones(index.size(1))])
             self.relation2outdegree.append(torch.from_numpy(np.bincount(sel[:, 2], minlength=E).astype(np.int64)))
         self._device_graphs = {}
+        self._grounders = {}  # (r, rule body) -> one-rule HIP grounder (grounding())
         print("Data loading | DONE!")
 
     # data.py:110-122
@@ -114,18 +115,37 @@ class KnowledgeGraph(object):
 
     # ------------------------------------------------------------ reference API
     def grounding(self, h, r, rule, edges_to_remove):
-        """Path counts (B, |E|) int64 of `rule` from each h (data.py:136-147).
+        """Path counts (B, |E|) int64 of `rule` from each h (data.py:136-147),
+        row i's edge edges_to_remove[i] of relation r removed on every hop of
+        relation r.
 
-        Auxiliary API (the PredictorPlus hot path grounds all rules of a batch
-        in one HIP launch instead); kept for callers such as Predictor."""
+        HIP: the rule becomes a one-rule trie under head r and runs through
+        the grounding kernel (rnnl_ground + COO export, the PredictorPlus
+        forward's own grounding), the counts are scattered into the dense
+        result.  The PredictorPlus / Predictor forwards ground all rules of a
+        batch in one launch instead of calling this per rule.  No CPU path."""
+        if h.device.type != "cuda":
+            raise RuntimeError("KnowledgeGraph.grounding runs on the HIP path: move h to a GPU")
+        r = int(r)
+        rule = [int(b) for b in rule]
+        h = h.to(torch.int64).contiguous()
+        if not rule:  # no hop: the one-hot start vectors
+            return torch.nn.functional.one_hot(h, self.entity_size)
+        key = (r, tuple(rule))
+        gr = self._grounders.pop(key, None)
+        if gr is None:
+            from .predictors import _RuleGrounder
+            gr = _RuleGrounder(self, r, rule)
+        self._grounders[key] = gr  # most recently used last
+        while len(self._grounders) > 64:
+            self._grounders.pop(next(iter(self._grounders)))
         with torch.no_grad():
-            x = torch.nn.functional.one_hot(h, self.entity_size).transpose(0, 1).unsqueeze(-1)
-            for r_body in rule:
-                x = self.propagate(x, r_body, edges_to_remove if r_body == r else None)
-        return x.squeeze(-1).transpose(0, 1)
+            return gr.counts(h, edges_to_remove)
 
     def propagate(self, x, relation, edges_to_remove=None):
-        """data.py:149-173 with the scatter-sum done by index_add_."""
+        """data.py:149-173 with the scatter-sum done by index_add_ (a generic
+        scatter over any (|E|, B, D) tensor, on x's device; the grounding
+        above and the forwards do not use it)."""
         device = x.device
         node_in = self.relation2adjacency[relation][0][1].to(device)
         node_out = self.relation2adjacency[relation][0][0].to(device)

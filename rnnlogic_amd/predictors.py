@@ -209,6 +209,31 @@ class _HipGrounding(object):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
 
+class _RuleGrounder(_HipGrounding):
+    """One rule as a one-rule trie under its head relation: the HIP grounding
+    behind KnowledgeGraph.grounding (reference data.py:136-147)."""
+
+    def __init__(self, graph, head, body):
+        self.graph = graph
+        self.rules = [(head, list(body))]
+        self._native_rules = {}
+        self._ws = {}
+        self._ws_uses = {}
+        self._flags = np.zeros(1, dtype=np.uint32)
+        self.capacity_scale = 1
+
+    def counts(self, h, edges_to_remove):
+        """(B, |E|) int64 path counts of the rule from each h."""
+        device = h.device
+        B = h.numel()
+        all_r = torch.full((B,), self.rules[0][0], dtype=torch.int64, device=device)
+        row, ent, ce, node, count = self.ground_coo(h, all_r, edges_to_remove)
+        out = torch.zeros((B, self.graph.entity_size), dtype=torch.int64, device=device)
+        # one rule = one trie node, but a hash overflow in the kernel may leave
+        # a (candidate, node) pair split over several entries: add them
+        return out.index_put_((row[ce], ent[ce]), count, accumulate=True)
+
+
 class _PredictorLinear(torch.autograd.Function):
     """Predictor.forward under autograd (predictors.py:53-80): the HIP forward
     (rnnl_predictor_forward) and its backward (rnnl_predictor_backward: per

@@ -99,24 +99,15 @@ def test_predictorplus_state_dict_and_seeded_init(case, fixtures):
         np.testing.assert_array_equal(sd[k].numpy(), fx.sd[k], err_msg=k)
 
 
-def test_grounding_api_matches_golden_counts(fixtures):
-    """KnowledgeGraph.grounding (auxiliary torch path) == reference counts."""
+def test_grounding_api_needs_gpu(fixtures):
+    """KnowledgeGraph.grounding is the HIP grounding (no CPU path): CPU
+    inputs raise.  Its counts are checked on the GPU in
+    tests/test_gpu_graph_api.py."""
     from rnnlogic_amd.data import KnowledgeGraph
     fx = fixtures("umls_lstm_sum_bias")
     g = KnowledgeGraph(fx.dataset_path())
-    from oracle import reference_np as ref
-    rules = ref.Rules(fx.rule_path(), g.relation_size)
-    for k in (0, fx.ncalls - 1):
-        c = fx.call(k)
-        q = int(c["r"][0])
-        h = torch.from_numpy(c["h"])
-        etr = torch.from_numpy(c["etr"]) if c["etr"] is not None else None
-        got = []
-        for i, (hd, body) in rules.relation2rules[q]:
-            x = g.grounding(h, hd, body, etr).numpy()
-            b, e = np.nonzero(x)
-            got.append(np.stack([np.full_like(b, i), b, e, x[b, e]], 1))
-        np.testing.assert_array_equal(np.concatenate(got), c["coo"].astype(np.int64))
+    with pytest.raises(RuntimeError, match="HIP path"):
+        g.grounding(torch.zeros(2, dtype=torch.int64), 0, [1, 2], None)
 
 
 def test_device_train_batches_tables():
