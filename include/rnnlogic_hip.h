@@ -85,17 +85,23 @@ int rnnl_rules_head_roots(rnnl_rules r, int32_t *head_root, int32_t *max_head_no
 
 /* Per-node aggregate of rule embeddings (device): rule_emb is n_rules x H
  * (row stride `ld` floats), H == 16.  Writes node_w: n_nodes records of
- * info5[3 + aggregator] bytes.
- *   SUM record: int32 fix_s(sum x)[16], members summed in rule-id order (f32),
- *               then one shift s for the whole table (|fix| < 2^30; stored
- *               in a trailer after the records)
- *   PNA record: int64 fix(sum x)[16] | int64 fix(sum x^2)[16] | f32 min x[16] | f32 max x[16]
- * where fix(v) = round(v * 2^28).  The forward accumulates both in exact
- * int64 arithmetic, so a score does not depend on the order in which the
- * kernel meets a candidate's (node, count) entries.  Buffer size:
- * rnnl_node_weights_size. */
-int rnnl_node_weights(rnnl_rules r, const float *rule_emb, int32_t ld, int32_t aggregator, void *node_w,
-                      void *stream);
+ * info5[3 + aggregator] bytes, then a trailer.
+ *   SUM record: int32 fix_s(W . sum x)[16] — the members' embeddings summed
+ *               in rule-id order (f32), times W = add_w (16 x 16 row-major,
+ *               rule_to_entity.add_model.layers.0.weight, required for SUM;
+ *               f32, inputs in ascending order), then one shift s for the
+ *               whole table (|fix| < 2^30).  The Linear commutes with the
+ *               candidate's sum of count x record (layers.py:70-74), so the
+ *               scoring pass adds only its bias.
+ *   PNA record: int32 fix(sum x)[16] | int32 fix(sum x^2)[16] | f32 min x[16] | f32 max x[16]
+ *               (one shift per column; add_w unused, nullable)
+ * The forward accumulates the fixed-point words exactly (fp64 below a total
+ * count of 2^23, int64 past it), so a score does not depend on the order in
+ * which the kernel meets a candidate's (node, count) entries.  Buffer size:
+ * rnnl_node_weights_size.  Replaces the per-candidate sums of
+ * FuncToNodeSum / FuncToNode (reference src/layers.py:53-126). */
+int rnnl_node_weights(rnnl_rules r, const float *rule_emb, int32_t ld, int32_t aggregator, const float *add_w,
+                      void *node_w, void *stream);
 int rnnl_node_weights_size(rnnl_rules r, int32_t aggregator, size_t *bytes);
 
 /* Rule encoder (reference src/predictors.py:201-208, type 'lstm'): for each

@@ -37,7 +37,7 @@ SIGNATURES = [
     ("rnnl_rules_info", ctypes.c_int, [_P, _P]),
     ("rnnl_rules_node_of_rule", ctypes.c_int, [_P, _P]),
     ("rnnl_rules_head_roots", ctypes.c_int, [_P, _P, _P]),
-    ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P]),
+    ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P]),
     ("rnnl_node_weights_size", ctypes.c_int, [_P, _I32, _P]),
     ("rnnl_lstm_encode", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _I32, _P]),
     ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),

@@ -226,6 +226,11 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
       return RNNL_ERR_INVALID;
     }
   }
+  // the scoring kernels address node records with 32-bit byte offsets
+  if ((int64_t)node_rel.size() * kStridePna >= ((int64_t)1 << 32)) {
+    set_error("rnnl_rules_create: more trie nodes than 32-bit record offsets address");
+    return RNNL_ERR_INVALID;
+  }
   // leaves per head (nodes where rules end), in node-id order
   const int n_nodes_total = (int)node_rel.size();
   std::vector<int32_t> head_leaf_ptr(R + 1, 0), head_leaf_node, node_leaf(n_nodes_total, -1);

@@ -783,8 +783,13 @@ void launch_chunk_list(const KParams &p, hipStream_t st) {
 // Grid-stride over (node, dim) pairs; the table-wide max |s1| (the SUM table's
 // shift) is reduced per thread, per wave and per block before one atomic per
 // block (one atomic per lane on a single word serialised at ~0.5 ms).
+// SUM: the record is FuncToNodeSum's Linear(16, 16) weight times the node's
+// sum, y[o] = sum_i add_w[o][i] x[i] (fp32, i ascending; x from the node's 16
+// lanes by width-16 shuffles): the Linear commutes with the candidate's sum of
+// count x record, so the scoring pass adds only its bias.
 __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, int ld,
-                                                          int agg, unsigned char *__restrict__ out) {
+                                                          int agg, const float *__restrict__ add_w,
+                                                          unsigned char *__restrict__ out) {
   const int64_t total = (int64_t)rl.n_nodes * 16;
   unsigned int m = 0, m2 = 0;
   for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
@@ -799,9 +804,13 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
       mx = fmaxf(mx, x);
     }
     if (agg == RNNL_AGG_SUM) {
-      // f32 sum for now; node_fix_kernel turns it into int32 fixed point
-      reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = s1;
-      m = max(m, __float_as_uint(fabsf(s1)));
+      // the node's 16 lanes are one aligned width-16 group (total is a multiple of 16)
+      float y = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) y = fmaf(__shfl(s1, i, 16), add_w[d * 16 + i], y);
+      // f32 for now; node_fix_kernel turns it into int32 fixed point
+      reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = y;
+      m = max(m, __float_as_uint(fabsf(y)));
     } else {
       // f32 sums for now; pna_fix_kernel turns them into int32 fixed point with
       // one shift per column (max |sum x| bits -> trailer[0], max |sum x^2| -> trailer[3])
@@ -1053,8 +1062,10 @@ using namespace rnnl;
 
 extern "C" {
 
-int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, void *node_w, void *stream) {
-  if (!r || !emb || !node_w || (agg != RNNL_AGG_SUM && agg != RNNL_AGG_PNA) || ld < 16) {
+int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, const float *add_w, void *node_w,
+                      void *stream) {
+  if (!r || !emb || !node_w || (agg != RNNL_AGG_SUM && agg != RNNL_AGG_PNA) || ld < 16 ||
+      (agg == RNNL_AGG_SUM && !add_w)) {
     set_error("rnnl_node_weights: bad arguments");
     return RNNL_ERR_INVALID;
   }
@@ -1065,7 +1076,7 @@ int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, v
   if (n == 0) return RNNL_OK;
   const int bs = 256;
   hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 2048)), dim3(bs), 0,
-                     (hipStream_t)stream, r->d, emb, ld, agg, out);
+                     (hipStream_t)stream, r->d, emb, ld, agg, add_w, out);
   if (agg == RNNL_AGG_PNA)
     hipLaunchKernelGGL(pna_fix_kernel, dim3((unsigned)std::min<int64_t>((2 * n + bs - 1) / bs, 4096)), dim3(bs), 0,
                        (hipStream_t)stream, r->d.n_nodes, out);

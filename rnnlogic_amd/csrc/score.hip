@@ -3,9 +3,10 @@
 // After the grounding (ground.hip) every candidate of a query has a bucket of
 // (trie node, path count) entries.  Its score (ref src/predictors.py:238-271):
 //   rule_to_entity (layers.py:53-126): FuncToNodeSum — the exact sum of
-//       count x node record (int32 fixed point, one shift per table; summed in
-//       fp64, which is exact below 2^23 total count, else int64), then
-//       Linear(16, 16), LayerNorm, ReLU; FuncToNode (pna) — sums of x and x^2,
+//       count x node record (the node's rule-embedding sum times the
+//       Linear(16, 16) weight, int32 fixed point with one shift per table;
+//       summed in fp64, which is exact below 2^23 total count, else int64),
+//       then the Linear's bias, LayerNorm, ReLU; FuncToNode (pna) — sums of x and x^2,
 //       min and max per node, degree scalers, Linear(192, 16), LayerNorm, ReLU
 //   score_model (layers.py:9-51): Linear(32, 128) (the relation half folded
 //       into a per-relation bias), ReLU, Linear(128, 1)
@@ -18,6 +19,10 @@
 
 namespace rnnl {
 
+// Byte offset of node n's record: 32-bit (rnnl_rules_create bounds the node
+// count), so the loads take the scalar-base + 32-bit-offset form
+__device__ __forceinline__ uint32_t rec_off(int n, int stride) { return (uint32_t)n * (uint32_t)stride; }
+
 // Exact int64 sums of count x record word (off + d) over a candidate's bucket
 // entries, one dim at a time (few registers), as a double: the fallback of
 // pna_hidden_2walk's fp64 sums past a total count of 2^23.
@@ -28,7 +33,7 @@ __device__ __forceinline__ void exact_sums(const KParams &p, int beg, int cnt, i
 #pragma unroll 1
     for (int e = beg; e < beg + cnt; ++e) {
       const int2 be = p.bent[e];
-      acc += (long long)(uint32_t)be.y * reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna)[off + d];
+      acc += (long long)(uint32_t)be.y * reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna))[off + d];
     }
     a[d] = (double)acc;
   }
@@ -44,6 +49,10 @@ struct Mlp0Lds {
 
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ReLU as one v_med3_f32 (fmaxf(x, 0) compiles to a canonicalize + max pair);
+// the same value for every non-NaN x
+__device__ __forceinline__ float relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_huge_valf()); }
 
 // v = hi + lo + r with hi, lo fp16 (RNE) and |r| <= 2^-22 |v| for normal
 // parts (a subnormal lo part keeps an absolute error below 2^-25)
@@ -113,10 +122,10 @@ __device__ __forceinline__ float mlp0_tile(const f16x4 bh, const f16x4 bl, const
     d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, d, 0, 0, 0);
     d = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, d, 0, 0, 0);
     const float4 w1 = reinterpret_cast<const float4 *>(w.s1w)[ot * 4 + k];
-    acc = fmaf(fmaxf(d[0], 0.f), w1.x, acc);
-    acc = fmaf(fmaxf(d[1], 0.f), w1.y, acc);
-    acc = fmaf(fmaxf(d[2], 0.f), w1.z, acc);
-    acc = fmaf(fmaxf(d[3], 0.f), w1.w, acc);
+    acc = fmaf(relu(d[0]), w1.x, acc);
+    acc = fmaf(relu(d[1]), w1.y, acc);
+    acc = fmaf(relu(d[2]), w1.z, acc);
+    acc = fmaf(relu(d[3]), w1.w, acc);
   }
   acc += __shfl_xor(acc, 16, 64);
   acc += __shfl_xor(acc, 32, 64);
@@ -231,12 +240,12 @@ __device__ __forceinline__ void pna_walk(const KParams &p, int beg, int cnt, uin
       deg += c * p.rl.node_nrules[be.x];
       if (want_fp) fp += (uint64_t)c * p.rl.node_fp[be.x];
     }
-    const int *rec = reinterpret_cast<const int *>(p.node_w + (int64_t)be.x * kStridePna) + HALF * 16;
+    const int *rec = reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna)) + HALF * 16;
     const float *fr = reinterpret_cast<const float *>(rec + 32);
 #pragma unroll
     for (int d = 0; d < 16; ++d) {
       a[d] = fma(cd, (double)rec[d], a[d]);
-      mm[d] = HALF == 0 ? fminf(mm[d], fr[d]) : fmaxf(mm[d], fr[d]);
+      mm[d] = __builtin_amdgcn_fmed3f(mm[d], fr[d], HALF == 0 ? -__builtin_huge_valf() : __builtin_huge_valf());  // min / max
     }
   }
   if (csum >> 23) exact_sums(p, beg, cnt, HALF * 16, a);
@@ -368,8 +377,8 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
       const float rstd = 1.0f / sqrtf(v4 / 16.0f + 1e-5f);
       const float4 lw = reinterpret_cast<const float4 *>(s_w.lnw)[k];
       const float4 lb = reinterpret_cast<const float4 *>(s_w.lnb)[k];
-      const float4 x1 = make_float4(fmaxf(z[0] * rstd * lw.x + lb.x, 0.f), fmaxf(z[1] * rstd * lw.y + lb.y, 0.f),
-                                    fmaxf(z[2] * rstd * lw.z + lb.z, 0.f), fmaxf(z[3] * rstd * lw.w + lb.w, 0.f));
+      const float4 x1 = make_float4(relu(z[0] * rstd * lw.x + lb.x), relu(z[1] * rstd * lw.y + lb.y),
+                                    relu(z[2] * rstd * lw.z + lb.z), relu(z[3] * rstd * lw.w + lb.w));
       f16x4 bh, bl;
       split4(x1, bh, bl);
       const float o = mlp0_tile(bh, bl, s_w.m, relb);
@@ -417,7 +426,7 @@ __device__ __forceinline__ void gather_sum_int64(const KParams &p, int beg, int 
     const uint32_t cu = (uint32_t)be.y;
     const long long c = cu;
     csum += cu;
-    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const int *x = reinterpret_cast<const int *>(p.node_w + rec_off(n, kStrideSum));
 #pragma unroll
     for (int d = 0; d < 16; ++d) acc[d] += c * x[d];
     if constexpr (DIGEST) {
@@ -444,7 +453,7 @@ __device__ __forceinline__ void gather_sum(const KParams &p, int beg, int cnt, f
     const int n = be.x;
     const uint32_t cu = (uint32_t)be.y;
     csum += cu;
-    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const int *x = reinterpret_cast<const int *>(p.node_w + rec_off(n, kStrideSum));
     const double cd = (double)cu;
 #pragma unroll
     for (int d = 0; d < 16; ++d) accd[d] = fma(cd, (double)x[d], accd[d]);
@@ -461,15 +470,14 @@ __device__ __forceinline__ void gather_sum(const KParams &p, int beg, int cnt, f
   for (int d = 0; d < 16; ++d) f[d] = (float)(accd[d] * (double)inv_scale);
 }
 
-// LDS image of the SUM scoring weights: FuncToNodeSum's Linear(16, 16) and
+// LDS image of the SUM scoring weights: FuncToNodeSum's Linear bias and
 // LayerNorm as floats (VALU) and score_model (Mlp0Lds).
 struct SumLds {
-  float addw[256], addb[16], lnw[16], lnb[16];
+  float addb[16], lnw[16], lnb[16];
   Mlp0Lds m;
 };
 
 __device__ __forceinline__ void load_sum_weights(SumLds &w, const float *__restrict__ W) {
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) w.addw[i] = W[W_ADDW + i];
   if (threadIdx.x < 16) {
     w.addb[threadIdx.x] = W[W_ADDB + threadIdx.x];
     w.lnw[threadIdx.x] = W[W_LNW + threadIdx.x];
@@ -478,15 +486,12 @@ __device__ __forceinline__ void load_sum_weights(SumLds &w, const float *__restr
   load_mlp0(w.m, W);
 }
 
-// FuncToNodeSum tail: x1 = ReLU(LayerNorm(Linear(16, 16)(f)))   (layers.py:53-77)
+// FuncToNodeSum tail: x1 = ReLU(LayerNorm(Linear(16, 16)(f)))   (layers.py:53-77);
+// the node records carry the Linear's weight already (node_weights_kernel), so
+// f is W . (sum of count x node sum) and only the bias is added here
 __device__ __forceinline__ void sum_hidden(const SumLds &w, const float f[16], float (&x1)[16]) {
 #pragma unroll
-  for (int o = 0; o < 16; ++o) {
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc = fmaf(f[i], w.addw[o * 16 + i], acc);
-    x1[o] = acc + w.addb[o];
-  }
+  for (int o = 0; o < 16; ++o) x1[o] = f[o] + w.addb[o];
   float mu = 0.f;
 #pragma unroll
   for (int d = 0; d < 16; ++d) mu += x1[d];
@@ -500,7 +505,7 @@ __device__ __forceinline__ void sum_hidden(const SumLds &w, const float f[16], f
   var = var / 16.0f;
   const float rstd = 1.0f / sqrtf(var + 1e-5f);
 #pragma unroll
-  for (int d = 0; d < 16; ++d) x1[d] = fmaxf((x1[d] - mu) * rstd * w.lnw[d] + w.lnb[d], 0.f);
+  for (int d = 0; d < 16; ++d) x1[d] = relu((x1[d] - mu) * rstd * w.lnw[d] + w.lnb[d]);
 }
 
 
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(BS) void memo_sum_kernel(KParams p, const float *__
 #pragma unroll
     for (int d = 0; d < 16; ++d) f[d] = 0.f;
     if (n >= 0) {
-      const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+      const int *x = reinterpret_cast<const int *>(p.node_w + rec_off(n, kStrideSum));
 #pragma unroll
       for (int d = 0; d < 16; ++d) f[d] = (float)((double)x[d] * (double)inv_scale);  // gather_sum of (n, 1)
     }
@@ -679,7 +684,7 @@ __device__ __forceinline__ void coop_gather(const KParams &p, int beg, int cnt, 
     const int n = be.x;
     const uint32_t cu = (uint32_t)be.y;
     csum += cu;
-    const int *x = reinterpret_cast<const int *>(p.node_w + (int64_t)n * kStrideSum);
+    const int *x = reinterpret_cast<const int *>(p.node_w + rec_off(n, kStrideSum));
     const double cd = (double)cu;
 #pragma unroll
     for (int d = 0; d < 16; ++d) acc[d] = fma(cd, (double)x[d], acc[d]);
@@ -813,8 +818,11 @@ __device__ __forceinline__ void sum_chunk_flush(const KParams &p, const SumLds &
 
 constexpr int SUM_CK = 8;  // chunks per dequeue on large launches
 
-template <bool DIGEST, bool COOP>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void score_sum_chunk_kernel(
+// WPE: waves per SIMD the register budget is sized for — 8 (64 VGPRs) when
+// the pass has the chip to itself, 4 (128 VGPRs, no spills in the entry walk)
+// beside RotatE, where its capped grid puts one wave on a SIMD anyway
+template <bool DIGEST, bool COOP, int WPE>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void score_sum_chunk_kernel(
     KParams p, const float *__restrict__ W) {
   __shared__ SumLds s_w;
   __shared__ __attribute__((aligned(16))) float s_relb[BS / 64][128];
@@ -999,13 +1007,17 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
   // one reference batch per call: the wave-cooperative walk of long entry lists
   // (bit-identical features); large launches keep the per-lane walk
   if (p.digest && small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<true, true>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<true, true, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (p.digest)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<true, false>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<true, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
+  else if (p.atomic_out && small)
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 4>), dim3(cgrid), dim3(BS), 0, st, p, W);
+  else if (p.atomic_out)
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, 4>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
 }
 
 }  // namespace rnnl

@@ -810,20 +810,25 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         """Per-trie-node aggregates of the rule embeddings (HIP), cached until a
         source parameter changes (optimizer steps bump `_version`)."""
         nr = self.native_rules(device)
-        key = (self._device_index(device), self.aggregator,
-               tuple((p.data_ptr(), p._version) for p in self._embedding_sources()))
+        # SUM records carry FuncToNodeSum's Linear weight (rnnl_node_weights)
+        srcs = self._embedding_sources() + ([self.rule_to_entity.add_model.layers[0].weight]
+                                            if self.aggregator == "sum" else [])
+        key = (self._device_index(device), self.aggregator, tuple((p.data_ptr(), p._version) for p in srcs))
         hit = self._node_cache.get(device)
         if hit is not None and hit[0] == key:
             return hit[1]
         with torch.no_grad():
             emb = self.all_rule_embeddings().detach().float().contiguous()
         agg = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
+        add_w = self.rule_to_entity.add_model.layers[0].weight.detach().float().contiguous() \
+            if self.aggregator == "sum" else None
         nbytes = ctypes.c_size_t()
         _native.call("rnnl_node_weights_size", nr.ptr, agg, ctypes.byref(nbytes))
         w = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
-        _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg, w.data_ptr(),
+        _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg,
+                     add_w.data_ptr() if add_w is not None else None, w.data_ptr(),
                      torch.cuda.current_stream(device).cuda_stream)
-        self._node_cache[device] = (key, w, emb)
+        self._node_cache[device] = (key, w, emb, add_w)
         return w
 
     def _params(self, device, node_w):

@@ -279,6 +279,74 @@ __global__ void k_direct_sgpr(float *out, unsigned long long *clk, float x) {
   stamp(clk, 1);
 }
 
+// the SUM scoring gather's per-element arithmetic: fp64 FMA chains, the
+// int32 -> fp64 conversion + FMA pair, and the int64 multiply-add form
+__global__ void k_f64fma(float *out, unsigned long long *clk, float x) {
+  stamp(clk, 0);
+  double a[8];
+  for (int j = 0; j < 8; ++j) a[j] = x + threadIdx.x + j;
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = fma(a[j], 0.999, 0.001);
+  double s = 0; for (int j = 0; j < 8; ++j) s += a[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+  stamp(clk, 1);
+}
+__global__ void k_cvt_fma(float *out, unsigned long long *clk, float x) {
+  stamp(clk, 0);
+  double a[8];
+  int v[8];
+  for (int j = 0; j < 8; ++j) { a[j] = 0; v[j] = (int)x + threadIdx.x + j; }
+  const double c = x;
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = fma(c, (double)v[j], a[j]); v[j] += 3; }
+  double s = 0; for (int j = 0; j < 8; ++j) s += a[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+  stamp(clk, 1);
+}
+__global__ void k_mad64(float *out, unsigned long long *clk, float x) {
+  stamp(clk, 0);
+  long long a[8];
+  int v[8];
+  for (int j = 0; j < 8; ++j) { a[j] = 0; v[j] = (int)x + threadIdx.x + j; }
+  const long long c = (long long)x + threadIdx.x;
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] += c * v[j]; v[j] += 3; }
+  long long s = 0; for (int j = 0; j < 8; ++j) s += a[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+  stamp(clk, 1);
+}
+__global__ void k_madi64(float *out, unsigned long long *clk, float x) {
+  stamp(clk, 0);
+  long long a[8];
+  int v[8];
+  for (int j = 0; j < 8; ++j) { a[j] = 0; v[j] = (int)x + threadIdx.x + j; }
+  const int c = (int)x + threadIdx.x;
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      unsigned long long carry;
+      asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(a[j]), "=s"(carry) : "v"(c), "v"(v[j]));
+      v[j] += 3;
+    }
+  long long s = 0; for (int j = 0; j < 8; ++j) s += a[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+  stamp(clk, 1);
+}
+__global__ void k_add32(float *out, unsigned long long *clk, float x) {
+  stamp(clk, 0);
+  int v[8];
+  for (int j = 0; j < 8; ++j) v[j] = (int)x + threadIdx.x + j;
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += 3;
+  int s = 0; for (int j = 0; j < 8; ++j) s += v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+  stamp(clk, 1);
+}
+
 template <typename K>
 double run(K kern, float *out, unsigned long long *clk, int blocks, int threads, double *ghz) {
   hipEvent_t e0, e1;
@@ -344,6 +412,16 @@ int main() {
   printf("bf16 16x16x16+4(sqrt+add) NT4: %.3f ms %.2f GHz -> %.2f cyc/wave-term\n", t, g, cyc(t, g, ITERS / 4 * 4 * 4.0));
   t = run(k_bf16k16_sqrt<8>, out, clk, blocks, threads, &g);
   printf("bf16 16x16x16+4(sqrt+add) NT8: %.3f ms %.2f GHz -> %.2f cyc/wave-term\n", t, g, cyc(t, g, ITERS / 4 * 8 * 4.0));
+  t = run(k_f64fma, out, clk, blocks, threads, &g);
+  printf("fma_f64:        %.3f ms %.2f GHz -> %.2f cyc/wave-instr/SIMD\n", t, g, cyc(t, g, ITERS * 8.0));
+  t = run(k_cvt_fma, out, clk, blocks, threads, &g);
+  printf("cvt_f64_i32+fma_f64+add: %.3f ms %.2f GHz -> %.2f cyc/element/SIMD\n", t, g, cyc(t, g, ITERS * 8.0));
+  t = run(k_mad64, out, clk, blocks, threads, &g);
+  printf("int64 += i64*i32 +add: %.3f ms %.2f GHz -> %.2f cyc/element/SIMD\n", t, g, cyc(t, g, ITERS * 8.0));
+  t = run(k_madi64, out, clk, blocks, threads, &g);
+  printf("v_mad_i64_i32+add: %.3f ms %.2f GHz -> %.2f cyc/element/SIMD\n", t, g, cyc(t, g, ITERS * 8.0));
+  t = run(k_add32, out, clk, blocks, threads, &g);
+  printf("add_u32:        %.3f ms %.2f GHz -> %.2f cyc/wave-instr/SIMD\n", t, g, cyc(t, g, ITERS * 8.0));
   hipLaunchKernelGGL((k_mfma_sqrt<8, true>), dim3(blocks / 2), dim3(threads), 0, 0, out, clk, 1.0f);
   t = run(k_mfma_sqrt<8, true>, out, clk, blocks / 4, threads, &g);
   printf("mfma+4(sqrt+add) NT8 1 block/CU: %.3f ms %.2f GHz -> %.2f cyc/wave-term\n", t, g,
