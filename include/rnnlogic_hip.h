@@ -16,7 +16,9 @@
  *   - handles (rnnl_graph, rnnl_rules) are immutable after creation and may be
  *     used from several streams at once; one set per GPU / rank.
  *   - all launches are asynchronous on `stream` and capture-safe (no
- *     allocation or synchronisation inside), except the *_create calls.
+ *     allocation or synchronisation inside), except the *_create calls, the
+ *     status reads (rnnl_forward_status*: one header read-back and wait) and
+ *     rnnl_predictorplus_forward_rotate (which ends with that read).
  */
 #ifndef RNNLOGIC_HIP_H
 #define RNNLOGIC_HIP_H
@@ -357,6 +359,42 @@ int rnnl_rotate_score_pieces(const float *eemb, const void *entity_table, const 
                              float gamma, const int64_t *all_h, const int64_t *all_r, int32_t n_queries,
                              int32_t n_entities, float *score, int32_t accumulate, int32_t mode, void *workspace,
                              size_t workspace_bytes, int32_t pieces, float first_share, void *stream);
+
+/* PredictorPlus.forward with the RotatE entity feature (reference
+ * src/predictors.py:210-271 with embedding.py:64-70 as the base score) in one
+ * host call: rnnl_predictorplus_ground and rnnl_predictorplus_score
+ * (deferred 2) on a side stream beside rnnl_rotate_score_pieces
+ * (accumulate 2) on `stream`, into score rows zeroed on a second side
+ * stream; mask (nullable, n_queries x E bytes) is filled with 1; then one
+ * header read-back, the result as rnnl_forward_status_flags (RNNL_ERR_OVERFLOW:
+ * call again with zeroed 0 and a doubled capacity_scale).  zeroed: 0 = the
+ * call zeroes the rows first; 1 = rnnl_forward_rotate_zero(score, ...) was
+ * issued earlier on this thread (e.g. before the rule encoder, so the fill
+ * runs beside it).  The side streams and events are the library's own (per
+ * host thread and device).
+ * events (nullable, 3 hipEvent_t, each nullable): recorded on `stream` before
+ * the launches, after RotatE and the mask, and after the side stream's work
+ * (timing).  Same scores as the one-stream path, bit for bit. */
+typedef struct {
+  const float *eemb;       /* RotatE.eemb (n_entities x 2 dim) */
+  const void *etab;        /* rnnl_rotate_entity_table */
+  const float *rtab;       /* rnnl_rotate_relation_table */
+  int32_t dim, n_entities;
+  float gamma;
+  int32_t mode;            /* RNNL_ROTATE_* */
+  void *workspace;         /* rnnl_rotate_workspace_size bytes (nullable when 0) */
+  size_t workspace_bytes;
+  int32_t pieces;          /* as rnnl_rotate_score_pieces */
+  float first_share;
+} rnnl_rotate_args;
+int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p,
+                                      const rnnl_rotate_args *rotate, const int64_t *all_h, const int64_t *all_r,
+                                      const int64_t *edges_to_remove, int32_t n_queries, float *score, uint8_t *mask,
+                                      int32_t *n_cand, uint64_t *digest, void *workspace, size_t workspace_bytes,
+                                      int32_t capacity_scale, int32_t ground_workgroups, int32_t score_workgroups,
+                                      int32_t zeroed, void *const *events, void *stream, int64_t *totals,
+                                      uint32_t *flags);
+int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream);
 
 /* Backward of the RotatE score (training; embedding.py:45-70 under autograd):
  * for grad = dL/dscore (n_queries x E, row-major), hr = h o r per query

@@ -47,6 +47,10 @@ SIGNATURES = [
      [_P, _P, _I32, _P, _P, _P, _I32, _P, _P, ctypes.c_size_t, _I32, _I32, _P]),
     ("rnnl_predictorplus_score", ctypes.c_int,
      [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _I32, _I32, _P]),
+    ("rnnl_predictorplus_forward_rotate", ctypes.c_int,
+     [_P, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _I32, _I32, _I32, _P, _P, _P,
+      _P]),
+    ("rnnl_forward_rotate_zero", ctypes.c_int, [_P, ctypes.c_size_t, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_forward_header_bytes", ctypes.c_int, [_P]),
@@ -101,6 +105,13 @@ class PredictorParams(ctypes.Structure):
     _fields_ = [("aggregator", _I32), ("feature", _I32), ("node_w", _P), ("add_w", _P), ("add_b", _P),
                 ("ln_w", _P), ("ln_b", _P), ("s0_w", _P), ("s0_b", _P), ("s1_w", _P), ("s1_b", _P),
                 ("rel_emb", _P), ("base_row", _P), ("packed", _P)]
+
+
+class RotateArgs(ctypes.Structure):
+    """rnnl_rotate_args (include/rnnlogic_hip.h)."""
+    _fields_ = [("eemb", _P), ("etab", _P), ("rtab", _P), ("dim", _I32), ("n_entities", _I32), ("gamma", _F32),
+                ("mode", _I32), ("workspace", _P), ("workspace_bytes", ctypes.c_size_t), ("pieces", _I32),
+                ("first_share", _F32)]
 
 
 class NativeError(RuntimeError):

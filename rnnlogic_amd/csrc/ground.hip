@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <map>
 #include <cstring>
 #include <string>
 
@@ -1243,10 +1244,44 @@ constexpr int STATUS_WORDS = 18;  // header words 0..17: status, ..., H_NCAND, t
 
 static int status_from_header(const unsigned int *st, int64_t *totals);
 
+// Per (host thread, device) resources of the host side of a forward: a pinned
+// copy of the launch header (a status read is one small DMA + one wait) and
+// the side streams / events of the RotatE overlap
+// (rnnl_predictorplus_forward_rotate).  Created on first use, kept.
+struct HostSide {
+  unsigned int *pinned = nullptr;
+  hipStream_t a = nullptr, b = nullptr;
+  hipEvent_t in = nullptr, zero = nullptr, side = nullptr;
+};
+
+static HostSide *host_side() {
+  thread_local std::map<int, HostSide> all;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  HostSide &h = all[dev];
+  if (!h.pinned && hipHostMalloc(reinterpret_cast<void **>(&h.pinned), 256, hipHostMallocDefault) != hipSuccess) {
+    h.pinned = nullptr;
+    return nullptr;
+  }
+  return &h;
+}
+
+// The launch header's status words into st (one read-back on `stream`).
+static int read_header(void *ws, void *stream, unsigned int (&st)[STATUS_WORDS]) {
+  HostSide *h = host_side();
+  if (!h) {
+    set_error("rnnl_forward_status: no pinned header buffer");
+    return RNNL_ERR_HIP;
+  }
+  RNNL_HIP_CHECK(hipMemcpyAsync(h->pinned, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  memcpy(st, h->pinned, sizeof(st));
+  return RNNL_OK;
+}
+
 static int forward_status(void *ws, void *stream, int64_t *totals) {
   unsigned int st[STATUS_WORDS] = {0};
-  RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
-  RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (int rc = read_header(ws, stream, st)) return rc;
   return status_from_header(st, totals);
 }
 
@@ -1288,10 +1323,100 @@ int rnnl_forward_status_flags(void *ws, void *stream, int64_t *totals, uint32_t 
     return RNNL_ERR_INVALID;
   }
   unsigned int st[STATUS_WORDS] = {0};
-  RNNL_HIP_CHECK(hipMemcpyAsync(st, ws, sizeof(st), hipMemcpyDeviceToHost, (hipStream_t)stream));
-  RNNL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (int rc = read_header(ws, stream, st)) return rc;
   if (flags) *flags = st[H_FLAGS];
   return status_from_header(st, totals);
+}
+
+// PredictorPlus forward with the RotatE entity feature in one host call: the
+// stream choreography of the overlap without a Python step per
+// launch.  Side stream B zeroes the score rows; side stream A grounds, then
+// (after the zero fill) scores with atomic adds; the caller's stream runs
+// RotatE with atomic adds after the zero fill, fills the all-True mask and
+// waits for A; then the header is read back (the only wait).  Ground is
+// enqueued before RotatE so its persistent workgroups are resident first.
+// The side streams / events of the overlap, created on first use.
+static HostSide *overlap_side(const char *who) {
+  HostSide *h = host_side();
+  if (!h) {
+    set_error(std::string(who) + ": no host resources");
+    return nullptr;
+  }
+  if (!h->a) {
+    if (hipStreamCreateWithFlags(&h->a, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->b, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->zero, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->side, hipEventDisableTiming) != hipSuccess) {
+      set_error(std::string(who) + ": side stream / event creation failed");
+      h->a = nullptr;
+      return nullptr;
+    }
+  }
+  return h;
+}
+
+// Zero fill of the score rows on side stream B, ordered after `stream`'s work
+// so far: issued before the rule encoder, it runs beside it instead of
+// lengthening the window before RotatE starts.  The next
+// rnnl_predictorplus_forward_rotate with zeroed = 1 waits for it.
+int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream) {
+  if (!score) {
+    set_error("rnnl_forward_rotate_zero: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  HostSide *h = overlap_side("rnnl_forward_rotate_zero");
+  if (!h) return RNNL_ERR_HIP;
+  RNNL_HIP_CHECK(hipEventRecord(h->in, (hipStream_t)stream));
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->b, h->in, 0));
+  RNNL_HIP_CHECK(hipMemsetAsync(score, 0, sizeof(float) * n_floats, h->b));
+  RNNL_HIP_CHECK(hipEventRecord(h->zero, h->b));
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp,
+                                      const rnnl_rotate_args *rot, const int64_t *all_h, const int64_t *all_r,
+                                      const int64_t *etr, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
+                                      uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t ground_wg,
+                                      int32_t score_wg, int32_t zeroed, void *const *events, void *stream,
+                                      int64_t *totals, uint32_t *flags) {
+  if (bad_params(pp, score) || !rot || !n_cand || !ws || nq < 0 || pp->feature != RNNL_FEATURE_ADD) {
+    set_error("rnnl_predictorplus_forward_rotate: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  HostSide *h = overlap_side("rnnl_predictorplus_forward_rotate");
+  if (!h) return RNNL_ERR_HIP;
+  hipStream_t main = (hipStream_t)stream;
+  const int32_t E = rot->n_entities;
+  // events[0..2] (nullable, timing): before the launches, after RotatE and the
+  // mask, after the side stream's work (PredictorPlus.forward_rows `events`)
+  auto mark = [&](int k) -> hipError_t {
+    return events && events[k] ? hipEventRecord((hipEvent_t)events[k], main) : hipSuccess;
+  };
+  if (!zeroed)
+    if (int rc = rnnl_forward_rotate_zero(score, (size_t)nq * (size_t)E, main)) return rc;
+  RNNL_HIP_CHECK(hipEventRecord(h->in, main));
+  RNNL_HIP_CHECK(mark(0));
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->in, 0));
+  if (int rc = rnnl_predictorplus_ground(g, r, pp->aggregator, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
+                                         ground_wg, h->a))
+    return rc;
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->zero, 0));
+  if (int rc = rnnl_predictorplus_score(g, r, pp, all_h, all_r, nq, score, nullptr, n_cand, digest, ws, ws_bytes,
+                                        scale, score_wg, 2, h->a))
+    return rc;
+  RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->zero, 0));
+  if (int rc = rnnl_rotate_score_pieces(rot->eemb, rot->etab, rot->rtab, rot->dim, rot->gamma, all_h, all_r, nq, E,
+                                        score, 2, rot->mode, rot->workspace, rot->workspace_bytes, rot->pieces,
+                                        rot->first_share, main))
+    return rc;
+  if (mask) RNNL_HIP_CHECK(hipMemsetAsync(mask, 1, (size_t)nq * (size_t)E, main));
+  RNNL_HIP_CHECK(mark(1));
+  RNNL_HIP_CHECK(hipEventRecord(h->side, h->a));
+  RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->side, 0));
+  RNNL_HIP_CHECK(mark(2));
+  return rnnl_forward_status_flags(ws, main, totals, flags);
 }
 
 int rnnl_forward_flags_host(const void *header, uint32_t *flags) {

@@ -68,6 +68,7 @@ class RotatE(torch.nn.Module):
         self._tables = None
         self._ws = None
         self._ws_need = {}
+        self._args = None  # (key, rnnl_rotate_args) of native_args
         # DIRECT (default) evaluates the reference's arithmetic term by term;
         # mode = ROTATE_MFMA selects the faster expanded bf16x3 MFMA kernel
         # (cancellation-prone when h o r ~= t; include/rnnlogic_hip.h)
@@ -107,6 +108,26 @@ class RotatE(torch.nn.Module):
         if self._ws is None or self._ws.numel() * 4 < need.value or self._ws.device != self.eemb.device:
             self._ws = torch.empty((need.value + 3) // 4, dtype=torch.float32, device=self.eemb.device)
         return self._ws.data_ptr(), need.value
+
+    def native_args(self, nq, pieces=1, first_share=0.0):
+        """rnnl_rotate_args for a launch over nq rows (the one-call forward,
+        rnnl_predictorplus_forward_rotate): the weight tables and workspace
+        of score_into, rebuilt only when the weights or the row count change."""
+        if not self.eemb.is_cuda:
+            raise RuntimeError("RotatE.forward runs on the HIP path; move the module to a GPU")
+        if not self.eemb.is_contiguous():
+            raise RuntimeError("RotatE.eemb must be contiguous")
+        etab, rtab = self._device_tables()
+        ws, ws_bytes = self._workspace(nq)
+        key = (etab.data_ptr(), rtab.data_ptr(), self.eemb.data_ptr(), ws, ws_bytes, int(self.mode), int(pieces),
+               float(first_share))
+        a = self._args
+        if a is None or a[0] != key:
+            args = _native.RotateArgs(self.eemb.data_ptr(), etab.data_ptr(), rtab.data_ptr(), self.emb_dim,
+                                      self.num_entities, float(self.gamma), int(self.mode), ws, ws_bytes, int(pieces),
+                                      float(first_share))
+            self._args = a = (key, args)
+        return a[1]
 
     def score_into(self, all_h, all_r, out, accumulate=False, pieces=1, first_share=0.0):
         """out (B, |E|) (+)= gamma - dist(h o r, e) for every entity (HIP);

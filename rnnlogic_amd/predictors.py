@@ -934,16 +934,16 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         rec("start")
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
         overlap = self.entity_feature == "RotatE" and self.overlap and nq >= 2
-        # zero the rows on the side stream beside the rule encoder
-        zero_ev = self._zero_rows(device, score) if overlap else None
+        if overlap:  # zero the rows on a side stream beside the rule encoder
+            _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(),
+                         torch.cuda.current_stream(device).cuda_stream)
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
         none_mode = params.feature == _native.FEATURE_NONE
         n_cand = torch.empty(nq, dtype=torch.int32, device=device)
         if overlap:
-            mask = self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec,
-                                         zero_ev)
+            mask = self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events)
             del keep
             return (score, mask, n_cand) if return_ncand else (score, mask)
         while True:
@@ -988,80 +988,43 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self._ws_chunks[key] = ws
         return ws
 
-    def _side_streams(self, device):
-        """(A, B): A carries the grounding and the scoring pass, B the zero
-        fill of the score rows (beside the rule encoder)."""
-        key = self._device_index(device)
-        if key not in self._side:
-            self._side[key] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
-        return self._side[key]
-
-    def _zero_rows(self, device, score):
-        """score.zero_() on side stream B (ordered after the current stream's
-        work so far); returns the event that marks it done."""
+    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events):
+        """RotatE entity feature: one host call (rnnl_predictorplus_forward_rotate)
+        runs the one-stream path's kernels on three streams.  The grounding and
+        then the scoring pass run on a side stream beside RotatE on the current
+        stream (the grounding does not read the base score; it is latency-bound
+        where RotatE is VALU-bound), and are enqueued before RotatE so that
+        their persistent workgroups are resident before RotatE's blocks fill
+        the chip.  The score rows were zeroed on a second side stream
+        (rnnl_forward_rotate_zero, before the rule encoder), and RotatE and the
+        scoring pass both add into them atomically: two addends on an exact
+        zero round to fl(rotate + out) in either order, so the rows are the
+        one-stream path's bit for bit.  Returns the (all-True) mask, filled
+        on the current stream behind RotatE."""
         main = torch.cuda.current_stream(device)
-        side = self._side_streams(device)[1]
-        key = (self._device_index(device), "zev")
-        ev = self._side.get(key)
-        if ev is None:
-            ev = self._side[key] = torch.cuda.Event()
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            score.zero_()
-        ev.record(side)
-        return ev
-
-    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, rec, zero_ev):
-        """RotatE entity feature: the one-stream path's kernels on three
-        streams.  The grounding and then the scoring pass run on side stream A
-        beside RotatE on the current stream (the grounding does not read the
-        base score; it is latency-bound where RotatE is VALU-bound), and are
-        enqueued before RotatE so that their persistent workgroups are
-        resident before RotatE's blocks fill the chip.  The score rows were
-        zeroed on side stream B, and RotatE and the scoring pass both
-        add into them atomically (rnnl_rotate_score accumulate = 2,
-        rnnl_predictorplus_score deferred = 2): two addends on an exact zero
-        round to fl(rotate + out) in either order, so the rows are the
-        one-stream path's bit for bit.  Returns the (all-True) mask, filled on
-        the current stream behind RotatE."""
-        main = torch.cuda.current_stream(device)
-        side = self._side_streams(device)[0]
         nq = all_h.numel()
-        agg = params.aggregator
-        first = True
+        pieces = 2 if self.rotate_yield and params.aggregator == _native.AGG_PNA else 1
+        rot = self.RotatE.native_args(nq, pieces, 0.5 if pieces > 1 else 0.0)
+        mask = torch.empty((nq, self.num_entities), dtype=torch.bool, device=device)
+        ev = None
+        if events is not None:  # timing: before the launches, after RotatE, after the side stream
+            evs = [events.setdefault(k, torch.cuda.Event(enable_timing=True)) for k in ("base", "ground", "end")]
+            for e in evs:  # torch creates an event's handle on its first record
+                e.record(main)
+            ev = (ctypes.c_void_p * 3)(*[e.cuda_event for e in evs])
+        zeroed = 1
         while True:
-            if not first:  # a retried launch starts from zeroed rows again
-                score.zero_()
-                zero_ev.record(main)
-            first = False
             scale = self.capacity_scale
             ws = self._overlap_workspace(device, nq, scale)
-            side.wait_stream(main)  # inputs, node aggregates, workspace
-            rec("base")
-            _native.call("rnnl_predictorplus_ground", g, nr.ptr, agg, all_h.data_ptr(), all_r.data_ptr(),
-                         etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
-                         ws.numel(), scale, self.overlap_ground_wg, side.cuda_stream)
-            side.wait_event(zero_ev)
-            _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
-                         all_r.data_ptr(), nq, score.data_ptr(), None, n_cand.data_ptr(),
-                         digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
-                         self.overlap_score_wg, 2, side.cuda_stream)
-            main.wait_event(zero_ev)
-            pieces = 2 if self.rotate_yield and agg == _native.AGG_PNA else 1
-            self.RotatE.score_into(all_h, all_r, score, accumulate=2, pieces=pieces,
-                                   first_share=0.5 if pieces > 1 else 0.0)
-            # the all-True mask (RotatE feature) is filled behind RotatE, beside the side stream's work
-            mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
-            rec("ground")
-            main.wait_stream(side)
-            rec("end")
-            # the host waits for the result anyway: drain the side streams too,
-            # so no cross-stream wait is left pending into the next call
-            side.synchronize()
-            self._side_streams(device)[1].synchronize()
-            rc = self._status(ws, main.cuda_stream)
+            rc = _native.lib().rnnl_predictorplus_forward_rotate(
+                g, nr.ptr, ctypes.byref(params), ctypes.byref(rot), all_h.data_ptr(), all_r.data_ptr(),
+                etr.data_ptr() if etr is not None else None, nq, score.data_ptr(), mask.data_ptr(), n_cand.data_ptr(),
+                digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
+                self.overlap_ground_wg, self.overlap_score_wg, zeroed, ev, main.cuda_stream, None,
+                self._flags.ctypes.data_as(ctypes.c_void_p))
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
+                zeroed = 0  # the retried launch starts from zeroed rows again
                 logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
                 continue
             _native.check(rc)

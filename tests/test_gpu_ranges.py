@@ -149,16 +149,21 @@ def test_em_predictor_weights_out_of_range_fail_loudly(dev):
     assert ei.value.code == _native.RNNL_ERR_RANGE, str(ei.value)
 
 
-@pytest.mark.parametrize("case", [("umls", "lstm", "sum"), ("kinship", "emb", "pna")])
+@pytest.mark.parametrize("case", [("umls", "lstm", "sum", "bias"), ("kinship", "emb", "pna", "bias"),
+                                  ("umls", "lstm", "sum", "RotatE")])
 def test_workspace_overflow_retry_is_bit_identical(case, dev):
-    data, typ, agg = case
+    """The RotatE case retries inside the one-call overlap forward
+    (rnnl_predictorplus_forward_rotate, rows re-zeroed)."""
+    data, typ, agg, feature = case
     path = datasets.materialize(data)
     graph = KnowledgeGraph(path)
     torch.manual_seed(0)
-    model = PredictorPlus(graph, type=typ, entity_feature="bias", aggregator=agg)
+    model = PredictorPlus(graph, type=typ, entity_feature=feature, aggregator=agg,
+                          embedding_path=datasets.rotate_path(data) if feature == "RotatE" else None)
     model.set_rules(datasets.rule_file(data))
-    with torch.no_grad():
-        model.bias.normal_()
+    if feature == "bias":
+        with torch.no_grad():
+            model.bias.normal_()
     model = model.to(dev).eval()
     rows = np.asarray(graph.test_facts[:512], dtype=np.int64)
     h = torch.from_numpy(rows[:, 0]).to(dev)
@@ -169,7 +174,7 @@ def test_workspace_overflow_retry_is_bit_identical(case, dev):
     _native.call("rnnl_debug_capacity", 1024, 1024, 64)
     try:
         model.capacity_scale = 1
-        model._ws = {}
+        model._ws, model._ws_chunks = {}, {}
         with torch.no_grad():
             got, gmask, gnc = model.forward_rows(h, r, None, return_ncand=True)
         torch.cuda.synchronize()
@@ -177,7 +182,7 @@ def test_workspace_overflow_retry_is_bit_identical(case, dev):
     finally:
         _native.call("rnnl_debug_capacity", 0, 0, 0)
         model.capacity_scale = 1
-        model._ws = {}
+        model._ws, model._ws_chunks = {}, {}
     assert retried > 1, "the lowered capacities did not overflow"
     assert torch.equal(gnc, wnc)
     assert torch.equal(gmask, wmask)
