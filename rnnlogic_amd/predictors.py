@@ -399,11 +399,11 @@ class Predictor(_HipGrounding, torch.nn.Module):
                      scale, side.cuda_stream)
         # the grounding's status / totals and the one-relation flag, copied to the
         # host behind it: the forward reads them without waiting for the current stream
-        hb = self._header_bytes()
-        hdr = torch.empty(hb, dtype=torch.uint8, pin_memory=True)
+        # (pinned buffer and event of the ring slot: the slot's previous entry was
+        # consumed, or dropped behind the same side stream, before it comes round)
+        hdr, ev = self._host_slot(pf, "pf", slot, self.prefetch_depth + 1)
         with torch.cuda.stream(side):
-            hdr.copy_(ws[:hb], non_blocking=True)  # status, totals and the one-relation flag
-        ev = torch.cuda.Event()
+            hdr.copy_(ws[:hdr.numel()], non_blocking=True)  # status, totals and the one-relation flag
         ev.record(side)
         # the side stream's use of these blocks outlives a dropped queue entry or a
         # grown ring slot: the caching allocator must not hand them out before it ends
@@ -411,6 +411,16 @@ class Predictor(_HipGrounding, torch.nn.Module):
             t.record_stream(side)
         self._ws_touch(ws)
         pf["queue"].append((all_h, all_r, edges_to_remove, ws, scale, n_cand, ev, (h, r, etr), hdr))
+
+    def _host_slot(self, pf, name, k, n):
+        """(pinned header buffer, event) number k % n of a ring kept in pf:
+        reused instead of a pinned allocation and an event creation per step."""
+        ring = pf.get(name)
+        if ring is None or len(ring) != n:
+            hb = self._header_bytes()
+            ring = pf[name] = [(torch.empty(hb, dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
+                               for _ in range(n)]
+        return ring[k % n]
 
     def _header_bytes(self):
         if getattr(self, "_hdr_bytes", None) is None:
@@ -511,12 +521,12 @@ class Predictor(_HipGrounding, torch.nn.Module):
                 _native.call("rnnl_predictor_score", g, nr.ptr, node_w.data_ptr(), feature, all_h.data_ptr(),
                              all_r.data_ptr(), nq, score.data_ptr(), mask8.data_ptr() if mask8 is not None else None,
                              n_cand_pf.data_ptr(), ws.data_ptr(), ws.numel(), scale, stream)
-                # the scoring pass's range flag: copied behind it, read at the next forward
-                dh = torch.empty(hb, dtype=torch.uint8, pin_memory=True)
-                dh.copy_(ws[:hb], non_blocking=True)
-                dev_ev = torch.cuda.Event()
-                dev_ev.record(main)
+                # the scoring pass's range flag: copied behind it, read two forwards
+                # later (a ring of 4 pinned buffers / events: at most 2 are pending)
                 self._lookahead_forwards = getattr(self, "_lookahead_forwards", 0) + 1
+                dh, dev_ev = self._host_slot(self._pf[self._device_index(device)], "dev", self._lookahead_forwards, 4)
+                dh.copy_(ws[:hb], non_blocking=True)
+                dev_ev.record(main)
                 if getattr(self, "_deferred_status", None) is None:
                     self._deferred_status = collections.deque()
                 self._deferred_status.append((dh, dev_ev, self._lookahead_forwards))
