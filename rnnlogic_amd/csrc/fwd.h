@@ -285,10 +285,12 @@ __device__ __forceinline__ void flag_acc_range(const KParams &p) {
 // represented (a non-finite sum — its |x| bits are >= those of +inf — or
 // |sum| >= 2^30, which would need a negative shift): the records are zeroed
 // and the scoring kernels report ERR_NODE_RANGE.
-__device__ __forceinline__ int fix_shift(unsigned int *trailer, bool &bad) {
+// `pre_bits`: the max |x| bits of values the records were derived from (the
+// SUM table's member sums before the folded Linear), held to the same 2^30.
+__device__ __forceinline__ int fix_shift(unsigned int *trailer, bool &bad, unsigned int pre_bits = 0u) {
   const unsigned int bits = trailer[0];
   int e = 0;
-  bad = bits >= 0x7f800000u;
+  bad = bits >= 0x7f800000u || pre_bits >= 0x4e800000u;  // 0x4e800000 = 2^30 as f32
   if (!bad && bits) frexpf(__uint_as_float(bits), &e);  // max < 2^e
   bad = bad || e > 30;
   const int shift = bad ? 0 : min(30 - e, 60);

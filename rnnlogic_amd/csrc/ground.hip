@@ -812,6 +812,7 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
       // f32 for now; node_fix_kernel turns it into int32 fixed point
       reinterpret_cast<float *>(out + (int64_t)n * kStrideSum)[d] = y;
       m = max(m, __float_as_uint(fabsf(y)));
+      m2 = max(m2, __float_as_uint(fabsf(s1)));  // the node aggregate itself (range guard, §3.13)
     } else {
       // f32 sums for now; pna_fix_kernel turns them into int32 fixed point with
       // one shift per column (max |sum x| bits -> trailer[0], max |sum x^2| -> trailer[3])
@@ -842,7 +843,7 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
     m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
     m2 = max(max(s_m2[0], s_m2[1]), max(s_m2[2], s_m2[3]));
     if (m) atomicMax(trailer, m);
-    if (m2 && agg != RNNL_AGG_SUM) atomicMax(trailer + 3, m2);
+    if (m2) atomicMax(trailer + 3, m2);  // PNA: max |sum x^2| bits; SUM: max |sum x| bits (pre-Linear)
   }
 }
 
@@ -911,11 +912,14 @@ __global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent
 // SUM records -> int32 fixed point with one shift for the whole table:
 // |fix| < 2^30 for the largest |sum|, so a candidate's int64 sum of
 // count x fix is exact (deterministic in any entry order) with ~2^-30
-// relative resolution.  Trailer: u32 max|x| bits, i32 shift (fix_shift).
+// relative resolution.  Trailer: u32 max|x| bits, i32 shift (fix_shift), bad flag, u32 max|sum x| bits
+// before the Linear fold (range-checked as well).
 __global__ void node_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
   unsigned int *trailer = reinterpret_cast<unsigned int *>(out + (int64_t)n_nodes * kStrideSum);
   bool bad;
-  const int shift = fix_shift(trailer, bad);
+  // trailer[3]: max |sum x| bits before the folded Linear — an aggregate of
+  // 2^30 or more fails the launch as it did before the fold
+  const int shift = fix_shift(trailer, bad, trailer[3]);
   const float sc = ldexpf(1.f, shift);
   const int64_t n = (int64_t)n_nodes * 16;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
