@@ -817,10 +817,20 @@ __device__ __forceinline__ void sum_chunk_flush(const KParams &p, const SumLds &
 }
 
 constexpr int SUM_CK = 8;  // chunks per dequeue on large launches
+// Register budget (waves per SIMD) of the scoring pass that runs beside RotatE
+// (atomic_out); a compile-time knob for A/B builds (tools/build_variants.sh).
+// 5 (96 VGPRs, 120 B of spills): the pass is launched when the grounding ends,
+// into a chip RotatE keeps full, and its workgroups must fit the space a
+// grounding workgroup (106 -> 112 VGPRs per wave) frees.  At 4 (127 VGPRs)
+// they did not, and trickled in as RotatE's waves retired: the scoring chain
+// took 79 ms instead of 34 and often ended after RotatE (FB15k-237 step 82.0 /
+// 82.4 ms vs 80.2 / 80.1 at 5, tools/interference.py).
+#ifndef RNNL_OVERLAP_WPE
+#define RNNL_OVERLAP_WPE 5
+#endif
 
 // WPE: waves per SIMD the register budget is sized for — 8 (64 VGPRs) when
-// the pass has the chip to itself, 4 (128 VGPRs, no spills in the entry walk)
-// beside RotatE, where its capped grid puts one wave on a SIMD anyway
+// the pass has the chip to itself, RNNL_OVERLAP_WPE beside RotatE (above)
 template <bool DIGEST, bool COOP, int WPE>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void score_sum_chunk_kernel(
     KParams p, const float *__restrict__ W) {
@@ -1011,9 +1021,9 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
   else if (p.digest)
     hipLaunchKernelGGL((score_sum_chunk_kernel<true, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (p.atomic_out && small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 4>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (p.atomic_out)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, 4>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (small)
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else

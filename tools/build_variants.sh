@@ -3,7 +3,7 @@
 # into rnnlogic_amd/_build/variants/<name>.so, for A/B runs selected at run
 # time with RNNL_LIB (e.g. VAR=RNNL_LIB VALS="rnnlogic_amd/_build/variants/a.so ..."
 # bash tools/env_ab.sh, or tools/bench_rotate.py).
-# Usage: tools/build_variants.sh ground.hip|rotate.hip name "flags" [name "flags" ...]
+# Usage: tools/build_variants.sh <source>.hip name "flags" [name "flags" ...]
 set -e
 src=$1
 shift
@@ -14,7 +14,7 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 B="--offload-arch=gfx950 -O3 -fPIC -std=c++17"
 [ "$src" = rotate.hip ] && B="$B -mllvm -amdgpu-mfma-vgpr-form"
 others=""
-for f in graph.cpp ground.hip rotate.hip encode.hip batch.hip mine.hip; do
+for f in graph.cpp ground.hip score.hip predictor.hip rotate.hip encode.hip batch.hip mine.hip loss.hip; do
   [ "$f" = "$src" ] || others="$others ../_build/$f.o"
 done
 make -s -C . $others
