@@ -567,9 +567,16 @@ __device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, 
   if (p.n_cand) p.n_cand[q] = S.err ? -2 : -1;
 }
 
+#define RNNL_STR2(x) #x
+#define RNNL_STR(x) RNNL_STR2(x)
 template <int AGG, int G>
 __global__ __launch_bounds__(G) void ground_kernel(KParams p) {
   __shared__ SmemT<G> S;
+#ifdef RNNL_GROUND_PNA_VGPRS
+  // A/B knob: allocate the PNA grounding's waves as many registers as the PNA
+  // scoring pass needs, so a scoring workgroup fits where a grounding one retires
+  if constexpr (AGG == RNNL_AGG_PNA) asm volatile("" ::: "v" RNNL_STR(RNNL_GROUND_PNA_VGPRS));
+#endif
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
   unsigned long long *pool_ctr = reinterpret_cast<unsigned long long *>(p.ws + 64);

@@ -665,7 +665,10 @@ __device__ __forceinline__ void pair_insert(const KParams &p, unsigned long long
 // of exact count x record products are exact in any order, so the feature is
 // the per-lane walk's bit for bit.  Up to BIG_SLOTS per round, their features
 // staged in LDS.
-constexpr int BIG_ENTRIES = 16;
+#ifndef RNNL_BIG_ENTRIES
+#define RNNL_BIG_ENTRIES 24
+#endif
+constexpr int BIG_ENTRIES = RNNL_BIG_ENTRIES;
 constexpr int BIG_SLOTS = 16;
 static_assert(BIG_SLOTS * 16 <= 256, "the long-list features share a wave's 256-float score_model stage");
 
@@ -827,6 +830,15 @@ constexpr int SUM_CK = 8;  // chunks per dequeue on large launches
 // 82.4 ms vs 80.2 / 80.1 at 5, tools/interference.py).
 #ifndef RNNL_OVERLAP_WPE
 #define RNNL_OVERLAP_WPE 5
+#endif
+#ifndef RNNL_OVERLAP_COOP
+#define RNNL_OVERLAP_COOP true
+#endif
+#ifndef RNNL_SOLO_WPE
+#define RNNL_SOLO_WPE 4
+#endif
+#ifndef RNNL_SOLO_COOP
+#define RNNL_SOLO_COOP true
 #endif
 
 // WPE: waves per SIMD the register budget is sized for — 8 (64 VGPRs) when
@@ -1023,11 +1035,11 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
   else if (p.atomic_out && small)
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (p.atomic_out)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, RNNL_OVERLAP_COOP, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (small)
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, RNNL_SOLO_COOP, RNNL_SOLO_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
 }
 
 }  // namespace rnnl

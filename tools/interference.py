@@ -1,5 +1,6 @@
 """Where the FB15k-237 RotatE pass loses time beside the side-stream kernels
-(diagnostic; GPU box): python tools/interference.py
+(diagnostic; GPU box): python tools/interference.py [fb|wn]
+(wn: the WN18RR config-3 model, PNA aggregator, RotatE D = 500)
 
 Times the bench's RotatE launch (HIP events on its stream) in five settings:
   store       alone, plain stores (RotatE.score_into)
@@ -22,9 +23,26 @@ import bench  # noqa: E402
 from rnnlogic_amd import _native  # noqa: E402
 
 dev = torch.device("cuda:0")
+WN = len(sys.argv) > 1 and sys.argv[1] == "wn"
 with contextlib.redirect_stdout(sys.stderr):
-    graph, test_set, model, rows = bench.build_workload("RotatE")
+    if WN:
+        import numpy as np
+        from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset
+        from rnnlogic_amd.predictors import PredictorPlus
+        path = bench.datasets.materialize("wn18rr", with_rotate=True)
+        torch.manual_seed(1)
+        graph = KnowledgeGraph(path)
+        TrainDataset(graph, 32)
+        ValidDataset(graph, 32)
+        test_set = TestDataset(graph, 32)
+        model = PredictorPlus(graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="RotatE",
+                              aggregator="pna", embedding_path=bench.datasets.rotate_path("wn18rr"))
+        model.set_rules(bench.datasets.rule_file("wn18rr"))
+        rows = np.asarray([x for b in test_set.batches for x in b], dtype=np.int64)
+    else:
+        graph, test_set, model, rows = bench.build_workload("RotatE")
 model = model.to(dev).eval()
+AGG = _native.AGG_PNA if WN else _native.AGG_SUM
 h = torch.from_numpy(rows[:, 0]).to(dev)
 r = torch.from_numpy(rows[:, 1]).to(dev)
 nq, E = h.numel(), graph.entity_size
@@ -43,7 +61,7 @@ def ev():
 def ground(stream, wg):
     ncs = torch.empty(nq, dtype=torch.int32, device=dev)
     ws = model._workspace(dev, nq, model.capacity_scale)
-    _native.call("rnnl_predictorplus_ground", g, nr.ptr, _native.AGG_SUM, h.data_ptr(), r.data_ptr(), None, nq,
+    _native.call("rnnl_predictorplus_ground", g, nr.ptr, AGG, h.data_ptr(), r.data_ptr(), None, nq,
                  ncs.data_ptr(), ws.data_ptr(), ws.numel(), model.capacity_scale, wg, stream.cuda_stream)
     return ws, ncs
 
@@ -57,10 +75,11 @@ def score(stream, ws, ncs, params, wg):
 res = {}
 with torch.no_grad():
     params, keep = model._params(dev, model.node_weights(dev))
-    for mode in ("store", "atomic", "+ground", "+score", "+score_late", "+both", "forward"):
+    for mode in ("store", "atomic", "+ground", "+score", "+score_late", "+both", "forward", "forward_1piece"):
         rot, sid = [], []
         for k in range(REPS + 1):
-            if mode == "forward":
+            if mode.startswith("forward"):
+                model.rotate_yield = mode == "forward"
                 evs = {}
                 model.invalidate_cache()
                 model.forward_rows(h, r, None, events=evs)
