@@ -256,10 +256,13 @@ __device__ __forceinline__ void pna_walk(const KParams &p, int beg, int cnt, uin
 }
 
 // One feature block (16 features of each of the wave's 64 candidates) into
-// the four tiles' add_model accumulators: staged, then per tile and scaler
-// one 16-wide K step (three fp16 part products).
+// the four tiles' add_model accumulators: staged, then per tile one split of
+// the features into fp16 parts and per scaler one 16-wide K step (three part
+// products).  The scalers are per candidate, so they factor out of the
+// Linear: Ds accumulates W_s . x, and the tile's output is D0 + s D1 + D2 / s
+// (pna_combine) — one split per tile instead of one per (tile, scaler).
 __device__ __forceinline__ void pna_block(const PnaLds &w, int b, const float (&v)[16], float *stage,
-                                          const float2 *sc, f32x4 (&D)[4]) {
+                                          f32x4 (&D)[3][4]) {
   const int lane = threadIdx.x & 63, k = lane >> 4, i16 = lane & 15;
   float4 *st = reinterpret_cast<float4 *>(stage);
 #pragma unroll
@@ -268,21 +271,85 @@ __device__ __forceinline__ void pna_block(const PnaLds &w, int b, const float (&
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const float4 x = st[(t * 16 + i16) * 4 + k];  // candidate 16 t + i16, features 16 b + 4k .. + 3
-    const float2 c = sc[t * 16 + i16];
+    f16x4 bh, bl;
+    split4(x, bh, bl);
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3) {
-      const float m = s3 == 1 ? c.x : c.y;
-      const float4 u = s3 == 0 ? x : make_float4(x.x * m, x.y * m, x.z * m, x.w * m);
-      f16x4 bh, bl;
-      split4(u, bh, bl);
       const f16x4 ah = __builtin_bit_cast(f16x4, w.aa[b][s3][0][lane]);
       const f16x4 al = __builtin_bit_cast(f16x4, w.aa[b][s3][1][lane]);
-      D[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, D[t], 0, 0, 0);
-      D[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, D[t], 0, 0, 0);
-      D[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, D[t], 0, 0, 0);
+      D[s3][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, D[s3][t], 0, 0, 0);
+      D[s3][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, D[s3][t], 0, 0, 0);
+      D[s3][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, D[s3][t], 0, 0, 0);
     }
   }
   wave_lds_sync();  // the next block rewrites the stage
+}
+
+// Long bucket lists (> PNA_BIG entries): one half of the walk (as pna_walk)
+// by the whole wave — lane i takes entries i, i + 64, ... — and a butterfly
+// over the lanes: the fp64 sums of exact count x record products are exact
+// in any order and min / max are order-free, so the features are the
+// per-lane walk's bit for bit.  slot[0 .. 15] = the sums at the column's
+// scale, slot[16 .. 31] = min (HALF 0) / max (HALF 1).  Returns the count
+// total (HALF 0: with the degree and fingerprint terms).
+constexpr int PNA_BIG = 16;
+constexpr int PNA_BIG_SLOTS = 16;
+template <int HALF>
+__device__ __forceinline__ uint64_t pna_coop(const KParams &p, int beg, int cnt, float *slot, long long &deg,
+                                             uint64_t &fp, bool want_fp) {
+  const int lane = threadIdx.x & 63;
+  double a[16];
+  float mm[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    a[d] = 0;
+    mm[d] = HALF == 0 ? __builtin_huge_valf() : -__builtin_huge_valf();
+  }
+  uint64_t csum = 0;
+  deg = 0;
+  fp = 0;
+#pragma unroll 1
+  for (int e = beg + lane; e < beg + cnt; e += 64) {
+    const int2 be = p.bent[e];
+    const double cd = (double)(uint32_t)be.y;
+    if constexpr (HALF == 0) {
+      const long long c = (uint32_t)be.y;
+      csum += (uint64_t)c;
+      deg += c * p.rl.node_nrules[be.x];
+      if (want_fp) fp += (uint64_t)c * p.rl.node_fp[be.x];
+    }
+    const int *rec = reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna)) + HALF * 16;
+    const float *fr = reinterpret_cast<const float *>(rec + 32);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] = fma(cd, (double)rec[d], a[d]);
+      mm[d] = HALF == 0 ? fminf(mm[d], fr[d]) : fmaxf(mm[d], fr[d]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      a[d] += __shfl_xor(a[d], off, 64);
+      const float o = __shfl_xor(mm[d], off, 64);
+      mm[d] = HALF == 0 ? fminf(mm[d], o) : fmaxf(mm[d], o);
+    }
+    if constexpr (HALF == 0) {
+      csum += __shfl_xor(csum, off, 64);
+      deg += __shfl_xor(deg, off, 64);
+      fp += __shfl_xor(fp, off, 64);
+    }
+  }
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  const double inv = ldexp(1.0, -(int)trailer[HALF == 0 ? 1 : 4]);
+  float v = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    if (lane == d) v = (float)(a[d] * inv);
+    if (lane == 16 + d) v = mm[d];
+  }
+  if (lane < 32) slot[lane] = v;
+  return csum;
 }
 
 __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const float *__restrict__ W) {
@@ -290,7 +357,8 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
   __shared__ __attribute__((aligned(16))) float s_relb[BS / 64][128];
   __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][64 * 16];  // a feature block of 64 candidates
   __shared__ float2 s_sc[BS / 64][64];                                      // their scalers (s, 1 / s)
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, k = lane >> 4;
+  __shared__ float s_big[BS / 64][PNA_BIG_SLOTS][64];                       // long lists' features (pna_coop)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, k = lane >> 4, i16 = lane & 15;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
   check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna));
   load_pna_weights(s_w, W);
@@ -327,49 +395,108 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
     }
     uint64_t csum = 0, fp = 0;
     long long deg = 0;
+    // the first PNA_BIG_SLOTS long lists: both halves walked by the whole wave
+    int slot = -1;
+    {
+      uint64_t big = __ballot(live && cr.z > PNA_BIG);
+#pragma unroll 1
+      for (int nb = 0; big && nb < PNA_BIG_SLOTS; ++nb) {
+        const int owner = __builtin_ctzll(big);
+        big &= big - 1;
+        const int beg = __builtin_amdgcn_readlane(cr.y, owner), cnt = __builtin_amdgcn_readlane(cr.z, owner);
+        long long bdeg;
+        uint64_t bfp, dummy_fp;
+        long long dummy_deg;
+        const uint64_t bsum = pna_coop<0>(p, beg, cnt, s_big[wv][nb], bdeg, bfp, p.digest != nullptr);
+        pna_coop<1>(p, beg, cnt, s_big[wv][nb] + 32, dummy_deg, dummy_fp, false);
+        if (lane == owner && !(bsum >> 23)) {  // past the exact fp64 range: the lane's own walk (exact_sums)
+          slot = nb;
+          csum = bsum;
+          deg = bdeg;
+          fp = bfp;
+        }
+      }
+      wave_lds_sync();
+    }
+    const int wbeg = cr.y, wcnt = slot >= 0 ? 0 : cr.z;  // the lane's own walk (none for a staged list)
     float sum[16], mm[16], mean[16];
     asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop
-    pna_walk<0, true>(p, cr.y, cr.z, csum, deg, fp, p.digest != nullptr, sum, mm);
+    {
+      uint64_t ws = 0, wf = 0;
+      long long wd = 0;
+      pna_walk<0, true>(p, wbeg, wcnt, ws, wd, wf, p.digest != nullptr, sum, mm);
+      if (slot >= 0) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+          sum[d] = s_big[wv][slot][d];
+          mm[d] = s_big[wv][slot][16 + d];
+        }
+      } else {
+        csum = ws;
+        deg = wd;
+        fp = wf;
+      }
+    }
     if (p.digest && live)
       atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q),
                 (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
     if (live && (csum >> 33)) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33
     // degree and scalers (layers.py:92, 103-116): degree = sum of A_fn + 1
     const float degf = (float)(deg + 1);
-    const float dcl = fmaxf(degf, 1e-6f);
+    const float idcl = 1.0f / fmaxf(degf, 1e-6f);  // one reciprocal for the 32 divisions by the degree
     const float sc1 = live ? logf(degf) / fmaxf(p.q_scale[q], 1e-6f) : 1.0f;
     s_sc[wv][lane] = make_float2(sc1, 1.0f / fmaxf(sc1, 1e-6f));
-    f32x4 D[4];
+    f32x4 D[3][4];  // per scaler {1, s, 1 / s}: W_s . features (pna_block)
     {
       const float4 ab = reinterpret_cast<const float4 *>(s_w.addb)[k];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) D[t] = (f32x4){ab.x, ab.y, ab.z, ab.w};
+      for (int t = 0; t < 4; ++t) {
+        D[0][t] = (f32x4){ab.x, ab.y, ab.z, ab.w};
+        D[1][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        D[2][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
-    for (int d = 0; d < 16; ++d) mean[d] = sum[d] / dcl;
-    pna_block(s_w, 0, mean, s_stage[wv], s_sc[wv], D);
+    for (int d = 0; d < 16; ++d) mean[d] = sum[d] * idcl;
+    pna_block(s_w, 0, mean, s_stage[wv], D);
 #pragma unroll
     for (int d = 0; d < 16; ++d) mm[d] = live ? mm[d] : 0.f;  // (an empty walk's min is +inf)
-    pna_block(s_w, 1, mm, s_stage[wv], s_sc[wv], D);
-    pna_walk<1, false>(p, cr.y, cr.z, csum, deg, fp, false, sum, mm);
+    pna_block(s_w, 1, mm, s_stage[wv], D);
+    {
+      uint64_t ws = 0, wf = 0;
+      long long wd = 0;
+      pna_walk<1, false>(p, wbeg, wcnt, ws, wd, wf, false, sum, mm);
+      if (slot >= 0) {
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+          sum[d] = s_big[wv][slot][32 + d];
+          mm[d] = s_big[wv][slot][48 + d];
+        }
+      }
+    }
 #pragma unroll
     for (int d = 0; d < 16; ++d) mm[d] = live ? mm[d] : 0.f;
-    pna_block(s_w, 2, mm, s_stage[wv], s_sc[wv], D);
+    pna_block(s_w, 2, mm, s_stage[wv], D);
 #pragma unroll
-    for (int d = 0; d < 16; ++d) sum[d] = sqrtf(fmaxf(sum[d] / dcl - mean[d] * mean[d], 1e-6f));
-    pna_block(s_w, 3, sum, s_stage[wv], s_sc[wv], D);
+    for (int d = 0; d < 16; ++d) sum[d] = sqrtf(fmaxf(sum[d] * idcl - mean[d] * mean[d], 1e-6f));
+    pna_block(s_w, 3, sum, s_stage[wv], D);
+    wave_lds_sync();  // s_big is rewritten by the next chunk
     // LayerNorm over each candidate's 16 outputs (four k-lanes), ReLU, score_model
     float out = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      float s4 = (D[t][0] + D[t][1]) + (D[t][2] + D[t][3]);
+      const float2 scl = s_sc[wv][t * 16 + i16];  // the scalers of this lane's D column (candidate i16)
+      f32x4 o4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o4[j] = fmaf(scl.y, D[2][t][j], fmaf(scl.x, D[1][t][j], D[0][t][j]));
+      float s4 = (o4[0] + o4[1]) + (o4[2] + o4[3]);
       s4 += __shfl_xor(s4, 16, 64);
       s4 += __shfl_xor(s4, 32, 64);
       const float mu = s4 / 16.0f;
       float z[4], v4 = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        z[j] = D[t][j] - mu;
+        z[j] = o4[j] - mu;
         v4 = fmaf(z[j], z[j], v4);
       }
       v4 += __shfl_xor(v4, 16, 64);
@@ -658,13 +785,15 @@ __device__ __forceinline__ void pair_insert(const KParams &p, unsigned long long
 // relation bias is per wave) and at the end.
 //
 // A candidate with more than BIG_ENTRIES bucket entries is gathered by the
-// whole wave on small launches (COOP; lane i takes entries i, i + 64, ...; a
+// whole wave (COOP builds; lane i takes entries i, i + 64, ...; a
 // butterfly sums the 16 fp64 partials): its lane would otherwise walk the
 // list alone, two dependent loads per entry, while the wave waits — on a
 // one-batch launch the scoring time is the longest such walk.  The fp64 sums
 // of exact count x record products are exact in any order, so the feature is
 // the per-lane walk's bit for bit.  Up to BIG_SLOTS per round, their features
-// staged in LDS.
+// staged in LDS.  A lane-per-candidate walk costs the wave its longest list:
+// on the FB15k-237 split the chunks' longest lists sum to 9.5x the entries /
+// 64 (tools/entry_stats.py); past 24 entries the whole wave takes the list.
 #ifndef RNNL_BIG_ENTRIES
 #define RNNL_BIG_ENTRIES 24
 #endif
@@ -715,9 +844,8 @@ __device__ __forceinline__ void coop_gather(const KParams &p, int beg, int cnt, 
 
 // Score m <= 64 queued candidates of relation r (lane i: queue[i]); the
 // whole wave calls it (score_model on the matrix cores needs every lane).
-// COOP = false (large launches): each lane walks its own list — the
-// cooperative rounds' registers spill at the 64-VGPR cap, which costs the
-// throughput-bound launches more (RotatE step +0.8 ms) than the long walks.
+// COOP = false (the 8-waves/SIMD builds): each lane walks its own list — the
+// cooperative rounds' registers spill at the 64-VGPR cap.
 template <bool DIGEST>
 __device__ __forceinline__ void sum_score_lane(const KParams &p, const SumLds &w, const float *relb, float *stage,
                                                bool live, const int2 it, const int4 cr, const float (&f)[16],
@@ -834,6 +962,12 @@ constexpr int SUM_CK = 8;  // chunks per dequeue on large launches
 #ifndef RNNL_OVERLAP_COOP
 #define RNNL_OVERLAP_COOP true
 #endif
+// One-stream launches (the chip to itself): up to SOLO_FEW_ROWS rows (e.g.
+// the kinship split, 5,343 rows, ~10k chunks for the 8,192 waves of the grid)
+// the 8-waves/SIMD build, whose whole grid is resident; larger ones (the
+// FB15k-237 split: 0.9M chunks) the spill-free 4-waves/SIMD build with the
+// cooperative long-list gather (ground + score alone 12.9 -> 10.4 ms).
+constexpr int SOLO_FEW_ROWS = 8192;
 #ifndef RNNL_SOLO_WPE
 #define RNNL_SOLO_WPE 4
 #endif
@@ -1038,6 +1172,8 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, RNNL_OVERLAP_COOP, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (small)
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
+  else if (nq <= SOLO_FEW_ROWS)  // about one chunk per wave: occupancy (8 waves/SIMD) over spill-free waves
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, RNNL_SOLO_COOP, RNNL_SOLO_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
 }
