@@ -277,13 +277,9 @@ def isolated_ground_ms(model, graph, h, r, dev):
         return e0.elapsed_time(e1)
 
 
-def wn18rr_line(dev, reps=10):
-    """Config 3 of BASELINE.json as a secondary line: PredictorPlus(emb, pna)
-    + RotatE(D=500, gamma=6) over the WN18RR test split (206 batches, 6,268
-    queries, real rnnlogic_rules.txt: 7,386 rules, L <= 5), seeded synthetic
-    train graph and RotatE tables — the same timed step as `value` (rule
-    aggregates recomputed, RotatE + grounding + PNA scoring), plus the
-    grounding/scoring kernels alone and the RotatE kernel's VALU roofline."""
+def wn18rr_model(dev, full=False):
+    """The config-3 model (PredictorPlus(emb, pna) + RotatE D = 500) and the
+    WN18RR test split's rows on `dev`, in run_predictorplus.py's order."""
     path = datasets.materialize("wn18rr", with_rotate=True)
     random.seed(1)
     np.random.seed(1)
@@ -300,6 +296,17 @@ def wn18rr_line(dev, reps=10):
     rows = np.asarray([x for b in test_set.batches for x in b], dtype=np.int64)
     h = torch.from_numpy(np.ascontiguousarray(rows[:, 0])).to(dev)
     r = torch.from_numpy(np.ascontiguousarray(rows[:, 1])).to(dev)
+    return (model, h, r, graph, test_set, rows) if full else (model, h, r)
+
+
+def wn18rr_line(dev, reps=10):
+    """Config 3 of BASELINE.json as a secondary line: PredictorPlus(emb, pna)
+    + RotatE(D=500, gamma=6) over the WN18RR test split (206 batches, 6,268
+    queries, real rnnlogic_rules.txt: 7,386 rules, L <= 5), seeded synthetic
+    train graph and RotatE tables — the same timed step as `value` (rule
+    aggregates recomputed, RotatE + grounding + PNA scoring), plus the
+    grounding/scoring kernels alone and the RotatE kernel's VALU roofline."""
+    model, h, r, graph, test_set, rows = wn18rr_model(dev, full=True)
 
     def step():
         model.invalidate_cache()

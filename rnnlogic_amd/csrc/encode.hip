@@ -11,6 +11,8 @@
 // launch instead of the per-layer/per-step library kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "internal.h"
 
 namespace rnnl {
@@ -19,6 +21,9 @@ constexpr int LH = 16;       // hidden size (the kernels' specialisation)
 constexpr int LMAXL = 3;     // layers supported
 constexpr int LG = 4 * LH;   // gates per layer (i, f, g, o: torch order)
 constexpr int LMAXT = 8;     // tokens per rule (head + body <= 7)
+#ifndef LSTM_BLOCKS_PER_CU
+#define LSTM_BLOCKS_PER_CU 4
+#endif
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
@@ -49,45 +54,49 @@ __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restric
   for (int i = threadIdx.x; i < layers * LG; i += blockDim.x) S.b[i / LG][i % LG] = b_ih[i] + b_hh[i];
   __syncthreads();
   const int j = threadIdx.x & (LH - 1);
-  const int rule = (blockIdx.x * blockDim.x + threadIdx.x) / LH;
-  const bool valid = rule < n_rules;  // whole 16-lane groups agree
-  const int32_t *tok = tokens + (int64_t)(valid ? rule : 0) * T;
-  int len = 0;
-  while (len < T && tok[len] != pad) ++len;
-  float seq[LMAXT];  // element j of the current layer's input (then output) at each step
+  // grid-stride over 16-rule groups: the weight image is loaded once per block
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 < (int64_t)n_rules * LH;
+       g0 += (int64_t)gridDim.x * blockDim.x) {
+    const int rule = (int)((g0 + threadIdx.x) / LH);
+    const bool valid = rule < n_rules;  // whole 16-lane groups agree
+    const int32_t *tok = tokens + (int64_t)(valid ? rule : 0) * T;
+    int len = 0;
+    while (len < T && tok[len] != pad) ++len;
+    float seq[LMAXT];  // element j of the current layer's input (then output) at each step
 #pragma unroll
-  for (int t = 0; t < LMAXT; ++t) seq[t] = vocab[(int64_t)tok[t < len ? t : 0] * LH + j];
+    for (int t = 0; t < LMAXT; ++t) seq[t] = vocab[(int64_t)tok[t < len ? t : 0] * LH + j];
 #pragma unroll 1
-  for (int l = 0; l < layers; ++l) {
-    float h = 0.f, c = 0.f;
+    for (int l = 0; l < layers; ++l) {
+      float h = 0.f, c = 0.f;
 #pragma unroll
-    for (int t = 0; t < LMAXT; ++t) {
-      if (t < len) {
-        float a[4];
+      for (int t = 0; t < LMAXT; ++t) {
+        if (t < len) {
+          float a[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = S.b[l][q * LH + j];
+          for (int q = 0; q < 4; ++q) a[q] = S.b[l][q * LH + j];
 #pragma unroll
-        for (int k = 0; k < LH; ++k) {
-          const float xk = __shfl(seq[t], k, LH), hk = __shfl(h, k, LH);
+          for (int k = 0; k < LH; ++k) {
+            const float xk = __shfl(seq[t], k, LH), hk = __shfl(h, k, LH);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            a[q] = fmaf(S.w[l][q * LH + j][k], xk, a[q]);
-            a[q] = fmaf(S.w[l][q * LH + j][LH + k], hk, a[q]);
+            for (int q = 0; q < 4; ++q) {
+              a[q] = fmaf(S.w[l][q * LH + j][k], xk, a[q]);
+              a[q] = fmaf(S.w[l][q * LH + j][LH + k], hk, a[q]);
+            }
           }
+          c = fmaf(sigm(a[1]), c, sigm(a[0]) * tanhf(a[2]));
+          h = sigm(a[3]) * tanhf(c);
+          seq[t] = h;
         }
-        c = fmaf(sigm(a[1]), c, sigm(a[0]) * tanhf(a[2]));
-        h = sigm(a[3]) * tanhf(c);
-        seq[t] = h;
       }
     }
-  }
-  // top layer's output at the last non-pad position (len >= 1: the head token)
-  if (valid) {
-    float v = 0.f;
+    // top layer's output at the last non-pad position (len >= 1: the head token)
+    if (valid) {
+      float v = 0.f;
 #pragma unroll
-    for (int t = 0; t < LMAXT; ++t)
-      if (t == len - 1) v = seq[t];
-    out[(int64_t)rule * ld_out + j] = v;
+      for (int t = 0; t < LMAXT; ++t)
+        if (t == len - 1) v = seq[t];
+      out[(int64_t)rule * ld_out + j] = v;
+    }
   }
 }
 
@@ -106,7 +115,9 @@ int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, c
     return RNNL_ERR_INVALID;
   }
   if (n_rules == 0) return RNNL_OK;
-  hipLaunchKernelGGL(lstm_encode_kernel, dim3((unsigned)(((int64_t)n_rules * LH + 255) / 256)), dim3(256), 0,
+  // at most LSTM_BLOCKS_PER_CU blocks per CU, each looping over rule groups
+  const int64_t blocks = std::min<int64_t>(((int64_t)n_rules * LH + 255) / 256, 256 * LSTM_BLOCKS_PER_CU);
+  hipLaunchKernelGGL(lstm_encode_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      (hipStream_t)stream, vocab, w_ih,
                      w_hh, b_ih, b_hh, tokens, seq_len, pad, n_rules, layers, out, ld_out);
   RNNL_HIP_CHECK(hipGetLastError());

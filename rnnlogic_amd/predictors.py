@@ -743,14 +743,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # pass 256 vs 512 / 768 workgroups 80.6-80.8 vs 81.25 / 81.1-81.7 ms
         self.overlap_ground_wg = 256
         self.overlap_score_wg = 256
-        # pna aggregator: RotatE in two launches, the first over half its grid
-        # (rnnl_rotate_score_pieces; bitwise the same scores).  The PNA scoring
-        # pass needs 168+ VGPRs per wave and finds no room beside RotatE's waves
-        # (6 x 76 per SIMD) until a launch boundary drains them: WN18RR step
-        # 21.0-21.1 -> 20.0-20.2 ms with the boundary at 0.4-0.6 of the grid.
-        # The sum pass (64 VGPRs) fits beside RotatE; there the boundary only
-        # costs its drain (FB15k-237 81.2 -> 81.5 ms).
+        # pna aggregator: RotatE in two launches (rnnl_rotate_score_pieces;
+        # bitwise the same scores).  The PNA scoring pass needs ~230 registers
+        # per wave and finds no room beside RotatE's waves (6 x 80 per SIMD)
+        # until a launch boundary drains them: WN18RR step 20.5 -> 18.4-18.6 ms
+        # (round 4, tools/yield_ab.py: first launch over 0.35 / 0.5 / 0.65 /
+        # 0.8 of the grid 18.5-18.9 / 18.55 / 18.48 / 18.44 ms).  The sum pass
+        # (96 VGPRs) fits beside RotatE; there the boundary only costs its drain.
         self.rotate_yield = True
+        self.rotate_share = 0.8  # the first launch's share of RotatE's grid
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -943,19 +944,14 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             if events is not None else (lambda k: None)
         rec("start")
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
-        overlap = self.entity_feature == "RotatE" and self.overlap and nq >= 2
-        if overlap:  # zero the rows on a side stream beside the rule encoder
-            _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(),
-                         torch.cuda.current_stream(device).cuda_stream)
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        if self.entity_feature == "RotatE" and self.overlap and nq >= 2:
+            mask = self._forward_overlap(device, g, nr, all_h, all_r, etr, score, n_cand, digest, events)
+            return (score, mask, n_cand) if return_ncand else (score, mask)
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
         none_mode = params.feature == _native.FEATURE_NONE
-        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        if overlap:
-            mask = self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events)
-            del keep
-            return (score, mask, n_cand) if return_ncand else (score, mask)
         while True:
             mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
             scale = self.capacity_scale
@@ -998,46 +994,64 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self._ws_chunks[key] = ws
         return ws
 
-    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events):
-        """RotatE entity feature: one host call (rnnl_predictorplus_forward_rotate)
-        runs the one-stream path's kernels on three streams.  The grounding and
-        then the scoring pass run on a side stream beside RotatE on the current
-        stream (the grounding does not read the base score; it is latency-bound
-        where RotatE is VALU-bound), and are enqueued before RotatE so that
-        their persistent workgroups are resident before RotatE's blocks fill
-        the chip.  The score rows were zeroed on a second side stream
-        (rnnl_forward_rotate_zero, before the rule encoder), and RotatE and the
-        scoring pass both add into them atomically: two addends on an exact
+    def _forward_overlap(self, device, g, nr, all_h, all_r, etr, score, n_cand, digest, events):
+        """RotatE entity feature: the one-stream path's kernels on
+        three streams, in two host calls.  rnnl_forward_rotate_begin launches
+        the grounding on side stream A first — it reads only the rows, and its
+        persistent workgroups must be resident before RotatE's blocks fill the
+        chip — and zeroes the score rows and fills the (all-True) mask on side
+        stream Z; the rule encoder and node aggregates run on the current
+        stream beside them, and rnnl_predictorplus_forward_rotate (zeroed 2)
+        runs RotatE behind them once the rows are zero and the scoring pass
+        on A after the encoder.  RotatE and the scoring
+        pass both add into the zeroed rows atomically: two addends on an exact
         zero round to fl(rotate + out) in either order, so the rows are the
-        one-stream path's bit for bit.  Returns the (all-True) mask, filled
-        on the current stream behind RotatE."""
+        one-stream path's bit for bit.  Returns the mask."""
         main = torch.cuda.current_stream(device)
         nq = all_h.numel()
-        pieces = 2 if self.rotate_yield and params.aggregator == _native.AGG_PNA else 1
-        rot = self.RotatE.native_args(nq, pieces, 0.5 if pieces > 1 else 0.0)
+        agg = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
         mask = torch.empty((nq, self.num_entities), dtype=torch.bool, device=device)
+        scale = self.capacity_scale
+        ws = self._overlap_workspace(device, nq, scale)
+        if getattr(self, "overlap_begin", True):
+            side = ctypes.c_void_p()
+            _native.call("rnnl_forward_rotate_begin", g, nr.ptr, agg, all_h.data_ptr(), all_r.data_ptr(),
+                         etr.data_ptr() if etr is not None else None, nq, self.num_entities, score.data_ptr(),
+                         mask.data_ptr(), n_cand.data_ptr(), ws.data_ptr(), ws.numel(), scale, self.overlap_ground_wg,
+                         main.cuda_stream, ctypes.byref(side))
+            zeroed, mask_arg = 2, None
+        else:
+            _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(), main.cuda_stream)
+            zeroed, mask_arg = 1, mask.data_ptr()
+        # the rule encoder + node aggregates on the current stream, beside the
+        # grounding and the zero fill; on side stream B (side.value) RotatE's
+        # blocks starve the encoder's until RotatE ends (DESIGN §3.7)
+        node_w = self.node_weights(device)
+        params, keep = self._params(device, node_w)
+        pieces = 2 if self.rotate_yield and agg == _native.AGG_PNA else 1
+        rot = self.RotatE.native_args(nq, pieces, self.rotate_share if pieces > 1 else 0.0)
         ev = None
-        if events is not None:  # timing: before the launches, after RotatE, after the side stream
+        if events is not None:  # timing: before RotatE, after RotatE, after the side streams
             evs = [events.setdefault(k, torch.cuda.Event(enable_timing=True)) for k in ("base", "ground", "end")]
             for e in evs:  # torch creates an event's handle on its first record
                 e.record(main)
             ev = (ctypes.c_void_p * 3)(*[e.cuda_event for e in evs])
-        zeroed = 1
         while True:
-            scale = self.capacity_scale
-            ws = self._overlap_workspace(device, nq, scale)
             rc = _native.lib().rnnl_predictorplus_forward_rotate(
                 g, nr.ptr, ctypes.byref(params), ctypes.byref(rot), all_h.data_ptr(), all_r.data_ptr(),
-                etr.data_ptr() if etr is not None else None, nq, score.data_ptr(), mask.data_ptr(), n_cand.data_ptr(),
+                etr.data_ptr() if etr is not None else None, nq, score.data_ptr(), mask_arg, n_cand.data_ptr(),
                 digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
                 self.overlap_ground_wg, self.overlap_score_wg, zeroed, ev, main.cuda_stream, None,
                 self._flags.ctypes.data_as(ctypes.c_void_p))
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
-                zeroed = 0  # the retried launch starts from zeroed rows again
+                # the retried launch grounds again and starts from zeroed rows
+                zeroed, scale = 0, self.capacity_scale
+                ws = self._overlap_workspace(device, nq, scale)
                 logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
                 continue
             _native.check(rc)
+            del keep
             return mask
 
     # ------------------------------------------------------------------ autograd (training) path
