@@ -370,12 +370,8 @@ int rnnl_rotate_score_pieces(const float *eemb, const void *entity_table, const 
  * call again with zeroed 0 and a doubled capacity_scale).  zeroed: 0 = the
  * call zeroes the rows first; 1 = rnnl_forward_rotate_zero(score, ...) was
  * issued earlier on this thread (e.g. before the rule encoder, so the fill
- * runs beside it); 2 = rnnl_forward_rotate_begin was called with the same
- * rows, score, n_cand, workspace and capacity_scale (the grounding is
- * launched; mask NULL here, begin filled it), and the caller's rule encoder
- * and node aggregates were enqueued on the side stream it returned.  The
- * side streams and events are the library's own (per host thread and
- * device).
+ * runs beside it).  The side streams and events are the library's own (per
+ * host thread and device).
  * events (nullable, 3 hipEvent_t, each nullable): recorded on `stream` before
  * the launches, after RotatE and the mask, and after the side stream's work
  * (timing).  Same scores as the one-stream path, bit for bit. */
@@ -399,20 +395,6 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
                                       int32_t zeroed, void *const *events, void *stream, int64_t *totals,
                                       uint32_t *flags);
 int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream);
-/* First half of the RotatE-feature forward with the rule encoder off
- * RotatE's path: after `stream`'s work so far, the grounding
- * (rnnl_predictorplus_ground, ground_workgroups) on side stream A, the score
- * rows zeroed and mask (nullable, n_queries x n_entities bytes) filled with
- * 1 on side stream Z, and *side_stream = side stream B, ordered after
- * `stream`'s work so far.  Enqueue the rule encoder and
- * rnnl_node_weights / rnnl_pack_weights on `stream` (or on B), then call
- * rnnl_predictorplus_forward_rotate with zeroed 2: RotatE runs on `stream`
- * once the rows are zero, the scoring pass on A once the encoder is done. */
-int rnnl_forward_rotate_begin(rnnl_graph g, rnnl_rules r, int32_t aggregator, const int64_t *all_h,
-                              const int64_t *all_r, const int64_t *edges_to_remove, int32_t n_queries,
-                              int32_t n_entities, float *score, uint8_t *mask, int32_t *n_cand, void *workspace,
-                              size_t workspace_bytes, int32_t capacity_scale, int32_t ground_workgroups, void *stream,
-                              void **side_stream);
 
 /* Backward of the RotatE score (training; embedding.py:45-70 under autograd):
  * for grad = dL/dscore (n_queries x E, row-major), hr = h o r per query

@@ -51,8 +51,6 @@ SIGNATURES = [
      [_P, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t, _I32, _I32, _I32, _I32, _P, _P, _P,
       _P]),
     ("rnnl_forward_rotate_zero", ctypes.c_int, [_P, ctypes.c_size_t, _P]),
-    ("rnnl_forward_rotate_begin", ctypes.c_int,
-     [_P, _P, _I32, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, ctypes.c_size_t, _I32, _I32, _P, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_forward_header_bytes", ctypes.c_int, [_P]),

@@ -1254,8 +1254,8 @@ static int status_from_header(const unsigned int *st, int64_t *totals);
 // (rnnl_predictorplus_forward_rotate).  Created on first use, kept.
 struct HostSide {
   unsigned int *pinned = nullptr;
-  hipStream_t a = nullptr, b = nullptr, z = nullptr;
-  hipEvent_t in = nullptr, zero = nullptr, side = nullptr, enc = nullptr, zend = nullptr;
+  hipStream_t a = nullptr, b = nullptr;
+  hipEvent_t in = nullptr, zero = nullptr, side = nullptr;
 };
 
 static HostSide *host_side() {
@@ -1349,12 +1349,9 @@ static HostSide *overlap_side(const char *who) {
   if (!h->a) {
     if (hipStreamCreateWithFlags(&h->a, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->b, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->z, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->zend, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->zero, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->side, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->enc, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->side, hipEventDisableTiming) != hipSuccess) {
       set_error(std::string(who) + ": side stream / event creation failed");
       h->a = nullptr;
       return nullptr;
@@ -1381,52 +1378,13 @@ int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream) {
   return RNNL_OK;
 }
 
-// The first half of a RotatE-feature forward: the grounding on
-// side stream A (it reads only the rows, so it starts with the step, beside
-// the rule encoder, and its workgroups are resident before RotatE's blocks
-// fill the chip), the score rows zeroed and the mask filled on side stream Z
-// (off RotatE's stream).  The caller then enqueues the rule encoder and node
-// aggregates — on `stream`, or on side stream B (*side_stream; ordered after
-// `stream`'s work so far) — and calls rnnl_predictorplus_forward_rotate with
-// zeroed = 2, which scores on A after both and runs RotatE on `stream` once
-// the rows are zero.  (The encoder on B, off RotatE's stream, measured worse:
-// RotatE's blocks starve its 8k blocks, and the scoring pass behind it, until
-// RotatE ends.)
-int rnnl_forward_rotate_begin(rnnl_graph g, rnnl_rules r, int32_t aggregator, const int64_t *all_h,
-                              const int64_t *all_r, const int64_t *etr, int32_t nq, int32_t n_entities,
-                              float *score, uint8_t *mask, int32_t *n_cand, void *ws, size_t ws_bytes, int32_t scale,
-                              int32_t ground_wg, void *stream, void **side_stream) {
-  if (!score || !n_cand || !ws || !side_stream || nq < 1 || n_entities < 1) {
-    set_error("rnnl_forward_rotate_begin: bad arguments");
-    return RNNL_ERR_INVALID;
-  }
-  HostSide *h = overlap_side("rnnl_forward_rotate_begin");
-  if (!h) return RNNL_ERR_HIP;
-  hipStream_t main = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipEventRecord(h->in, main));
-  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->in, 0));
-  if (int rc = rnnl_predictorplus_ground(g, r, aggregator, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
-                                         ground_wg, h->a))
-    return rc;
-  const size_t n = (size_t)nq * (size_t)n_entities;
-  RNNL_HIP_CHECK(hipStreamWaitEvent(h->z, h->in, 0));
-  RNNL_HIP_CHECK(hipMemsetAsync(score, 0, sizeof(float) * n, h->z));
-  RNNL_HIP_CHECK(hipEventRecord(h->zero, h->z));
-  if (mask) RNNL_HIP_CHECK(hipMemsetAsync(mask, 1, n, h->z));
-  RNNL_HIP_CHECK(hipEventRecord(h->zend, h->z));
-  RNNL_HIP_CHECK(hipStreamWaitEvent(h->b, h->in, 0));
-  *side_stream = (void *)h->b;
-  return RNNL_OK;
-}
-
 int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp,
                                       const rnnl_rotate_args *rot, const int64_t *all_h, const int64_t *all_r,
                                       const int64_t *etr, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
                                       uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t ground_wg,
                                       int32_t score_wg, int32_t zeroed, void *const *events, void *stream,
                                       int64_t *totals, uint32_t *flags) {
-  if (bad_params(pp, score) || !rot || !n_cand || !ws || nq < 0 || pp->feature != RNNL_FEATURE_ADD || zeroed < 0 ||
-      zeroed > 2) {
+  if (bad_params(pp, score) || !rot || !n_cand || !ws || nq < 0 || pp->feature != RNNL_FEATURE_ADD) {
     set_error("rnnl_predictorplus_forward_rotate: bad arguments");
     return RNNL_ERR_INVALID;
   }
@@ -1440,26 +1398,15 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
   auto mark = [&](int k) -> hipError_t {
     return events && events[k] ? hipEventRecord((hipEvent_t)events[k], main) : hipSuccess;
   };
-  const bool begun = zeroed == 2;  // rnnl_forward_rotate_begin: grounding on A, zero fill + encoder on B
   if (!zeroed)
     if (int rc = rnnl_forward_rotate_zero(score, (size_t)nq * (size_t)E, main)) return rc;
+  RNNL_HIP_CHECK(hipEventRecord(h->in, main));
   RNNL_HIP_CHECK(mark(0));
-  if (begun) {
-    // the caller's rule encoder / node aggregates, enqueued on `stream` (or on
-    // side stream B) since rnnl_forward_rotate_begin
-    RNNL_HIP_CHECK(hipEventRecord(h->enc, main));
-    RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->enc, 0));
-    RNNL_HIP_CHECK(hipEventRecord(h->in, h->b));
-    RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->in, 0));
-    RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->zero, 0));  // the scoring pass adds into the zeroed rows
-  } else {
-    RNNL_HIP_CHECK(hipEventRecord(h->in, main));
-    RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->in, 0));
-    if (int rc = rnnl_predictorplus_ground(g, r, pp->aggregator, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
-                                           ground_wg, h->a))
-      return rc;
-    RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->zero, 0));
-  }
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->in, 0));
+  if (int rc = rnnl_predictorplus_ground(g, r, pp->aggregator, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
+                                         ground_wg, h->a))
+    return rc;
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->zero, 0));
   if (int rc = rnnl_predictorplus_score(g, r, pp, all_h, all_r, nq, score, nullptr, n_cand, digest, ws, ws_bytes,
                                         scale, score_wg, 2, h->a))
     return rc;
@@ -1472,7 +1419,6 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
   RNNL_HIP_CHECK(mark(1));
   RNNL_HIP_CHECK(hipEventRecord(h->side, h->a));
   RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->side, 0));
-  if (begun) RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->zend, 0));  // the mask fill (B's work: A waited for it)
   RNNL_HIP_CHECK(mark(2));
   return rnnl_forward_status_flags(ws, main, totals, flags);
 }

@@ -944,14 +944,19 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             if events is not None else (lambda k: None)
         rec("start")
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
-        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        if self.entity_feature == "RotatE" and self.overlap and nq >= 2:
-            mask = self._forward_overlap(device, g, nr, all_h, all_r, etr, score, n_cand, digest, events)
-            return (score, mask, n_cand) if return_ncand else (score, mask)
+        overlap = self.entity_feature == "RotatE" and self.overlap and nq >= 2
+        if overlap:  # zero the rows on a side stream beside the rule encoder
+            _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(),
+                         torch.cuda.current_stream(device).cuda_stream)
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
         none_mode = params.feature == _native.FEATURE_NONE
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        if overlap:
+            mask = self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events)
+            del keep
+            return (score, mask, n_cand) if return_ncand else (score, mask)
         while True:
             mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
             scale = self.capacity_scale
@@ -994,64 +999,46 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             self._ws_chunks[key] = ws
         return ws
 
-    def _forward_overlap(self, device, g, nr, all_h, all_r, etr, score, n_cand, digest, events):
-        """RotatE entity feature: the one-stream path's kernels on
-        three streams, in two host calls.  rnnl_forward_rotate_begin launches
-        the grounding on side stream A first — it reads only the rows, and its
-        persistent workgroups must be resident before RotatE's blocks fill the
-        chip — and zeroes the score rows and fills the (all-True) mask on side
-        stream Z; the rule encoder and node aggregates run on the current
-        stream beside them, and rnnl_predictorplus_forward_rotate (zeroed 2)
-        runs RotatE behind them once the rows are zero and the scoring pass
-        on A after the encoder.  RotatE and the scoring
-        pass both add into the zeroed rows atomically: two addends on an exact
+    def _forward_overlap(self, device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events):
+        """RotatE entity feature: one host call (rnnl_predictorplus_forward_rotate)
+        runs the one-stream path's kernels on three streams.  The grounding and
+        then the scoring pass run on a side stream beside RotatE on the current
+        stream (the grounding does not read the base score; it is latency-bound
+        where RotatE is VALU-bound), and are enqueued before RotatE so that
+        their persistent workgroups are resident before RotatE's blocks fill
+        the chip.  The score rows were zeroed on a second side stream
+        (rnnl_forward_rotate_zero, before the rule encoder), and RotatE and the
+        scoring pass both add into them atomically: two addends on an exact
         zero round to fl(rotate + out) in either order, so the rows are the
-        one-stream path's bit for bit.  Returns the mask."""
+        one-stream path's bit for bit.  Returns the (all-True) mask, filled
+        on the current stream behind RotatE."""
         main = torch.cuda.current_stream(device)
         nq = all_h.numel()
-        agg = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
-        mask = torch.empty((nq, self.num_entities), dtype=torch.bool, device=device)
-        scale = self.capacity_scale
-        ws = self._overlap_workspace(device, nq, scale)
-        if getattr(self, "overlap_begin", True):
-            side = ctypes.c_void_p()
-            _native.call("rnnl_forward_rotate_begin", g, nr.ptr, agg, all_h.data_ptr(), all_r.data_ptr(),
-                         etr.data_ptr() if etr is not None else None, nq, self.num_entities, score.data_ptr(),
-                         mask.data_ptr(), n_cand.data_ptr(), ws.data_ptr(), ws.numel(), scale, self.overlap_ground_wg,
-                         main.cuda_stream, ctypes.byref(side))
-            zeroed, mask_arg = 2, None
-        else:
-            _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(), main.cuda_stream)
-            zeroed, mask_arg = 1, mask.data_ptr()
-        # the rule encoder + node aggregates on the current stream, beside the
-        # grounding and the zero fill; on side stream B (side.value) RotatE's
-        # blocks starve the encoder's until RotatE ends (DESIGN §3.7)
-        node_w = self.node_weights(device)
-        params, keep = self._params(device, node_w)
-        pieces = 2 if self.rotate_yield and agg == _native.AGG_PNA else 1
+        pieces = 2 if self.rotate_yield and params.aggregator == _native.AGG_PNA else 1
         rot = self.RotatE.native_args(nq, pieces, self.rotate_share if pieces > 1 else 0.0)
+        mask = torch.empty((nq, self.num_entities), dtype=torch.bool, device=device)
         ev = None
-        if events is not None:  # timing: before RotatE, after RotatE, after the side streams
+        if events is not None:  # timing: before the launches, after RotatE, after the side stream
             evs = [events.setdefault(k, torch.cuda.Event(enable_timing=True)) for k in ("base", "ground", "end")]
             for e in evs:  # torch creates an event's handle on its first record
                 e.record(main)
             ev = (ctypes.c_void_p * 3)(*[e.cuda_event for e in evs])
+        zeroed = 1
         while True:
+            scale = self.capacity_scale
+            ws = self._overlap_workspace(device, nq, scale)
             rc = _native.lib().rnnl_predictorplus_forward_rotate(
                 g, nr.ptr, ctypes.byref(params), ctypes.byref(rot), all_h.data_ptr(), all_r.data_ptr(),
-                etr.data_ptr() if etr is not None else None, nq, score.data_ptr(), mask_arg, n_cand.data_ptr(),
+                etr.data_ptr() if etr is not None else None, nq, score.data_ptr(), mask.data_ptr(), n_cand.data_ptr(),
                 digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
                 self.overlap_ground_wg, self.overlap_score_wg, zeroed, ev, main.cuda_stream, None,
                 self._flags.ctypes.data_as(ctypes.c_void_p))
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
                 self.capacity_scale *= 2
-                # the retried launch grounds again and starts from zeroed rows
-                zeroed, scale = 0, self.capacity_scale
-                ws = self._overlap_workspace(device, nq, scale)
+                zeroed = 0  # the retried launch starts from zeroed rows again
                 logging.info("PredictorPlus: workspace overflow, capacity_scale -> %d", self.capacity_scale)
                 continue
             _native.check(rc)
-            del keep
             return mask
 
     # ------------------------------------------------------------------ autograd (training) path
