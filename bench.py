@@ -550,7 +550,11 @@ def main():
     if os.environ.get("RNNL_BENCH_ONE_DEVICE") == "1":
         local = 0
     backend = os.environ.get("RNNL_BENCH_BACKEND", "nccl")
-    if world > 1:
+    # a process group whenever torch.distributed.run launched this process
+    # (also at --nproc-per-node 1: RCCL then runs its one-rank communicator
+    # through the same barriers / all-reduce / all-gather as at N > 1)
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if distributed:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -559,7 +563,7 @@ def main():
     dev = torch.device("cuda", local)
     if rank == 0:
         datasets.materialize("FB15k-237", with_rotate=(args.feature == "RotatE"))
-    if world > 1:
+    if distributed:
         dist.barrier()
 
     with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
@@ -580,24 +584,24 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     rows_per_rank = [nq]
     shards = None
-    if world > 1:
+    if distributed:
         cnt = torch.tensor([nq], dtype=torch.int64, device=dev)
         parts = [torch.empty_like(cnt) for _ in range(world)]
         dist.all_gather(parts, cnt)
@@ -780,7 +784,7 @@ def main():
         extra["em_iteration"] = em_iteration_line(dev)
 
     if rank != 0:
-        if world > 1:
+        if distributed:
             dist.barrier()
             dist.destroy_process_group()
         return
@@ -862,7 +866,8 @@ def main():
                                   "RotatE(D=1000,gamma=9)" if args.feature == "RotatE" else "bias",
                                   model.num_rules, " and RotatE tables" if args.feature == "RotatE" else ""),
                    "batch_size": 32, "parallelism": "dp%d (test batches sharded, KG replicated)" % world,
-                   "rows_per_rank": rows_per_rank, "batches_per_rank": len(shard), "shards": shards},
+                   "rows_per_rank": rows_per_rank, "batches_per_rank": len(shard), "shards": shards,
+                   "process_group": backend if distributed else None},
         "roofline": dominant,
         "kernels_ms": {"rule_encoder+node_weights": round(nodes_ms, 3), "base_score": round(base_ms, 3),
                        "tail_after_base": round(tail_ms, 3), "ground+score_isolated": round(ground_ms, 3)},
@@ -878,7 +883,7 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             out["reference_pytorch"] = reference_pytorch_baseline(model, graph, test_set, dev, args.feature)
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 
