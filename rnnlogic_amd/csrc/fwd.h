@@ -14,13 +14,13 @@
 namespace rnnl {
 
 constexpr int BS = 256;        // threads per workgroup (scoring kernels)
-#ifndef RNNL_GBS
-#define RNNL_GBS 256
-#endif
-#ifndef RNNL_GWG_PER_CU
-#define RNNL_GWG_PER_CU 3
-#endif
-constexpr int GBS = RNNL_GBS;  // threads per grounding workgroup (WIDE_ROWS launches: 1024)
+// Grounding workgroups: 512 lanes, two per CU (LDS-bound) with the chip to
+// itself — 256 lanes at three per CU measured 12 % slower on the FB15k-237
+// split (ground + score 10.2 vs 9.0 ms), 128 at five 40 % — and 256 lanes,
+// one per CU, beside RotatE (a 512-lane workgroup would hold two of RotatE's
+// six waves per SIMD); launches of <= WIDE_ROWS rows use 1,024 lanes.
+constexpr int GBS = 256;       // threads per grounding workgroup beside another kernel (capped grid)
+constexpr int SOLO_GBS = 512;  // threads per grounding workgroup with the chip to itself
 constexpr int HBITS = 12;
 constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count)
 constexpr int OCC_CAP = 1024;     // phase-A occupied-slot list (fuller levels scan all HCAP slots)
@@ -30,7 +30,7 @@ constexpr int MAXE_BITS = 19;
 constexpr int MAXWIN = (1 << MAXE_BITS) >> WBITS;  // windows per graph (|E| <= 2^MAXE_BITS)
 constexpr int HB = WIN;                // phase-B candidate hash slots
 constexpr int HB_LOAD = HB * 3 / 4;    // max contributions per hash pass
-constexpr int WG_PER_CU = RNNL_GWG_PER_CU;  // grounding workgroups per CU (LDS-bound)
+constexpr int WG_PER_CU = 2;           // grounding workgroups per CU at SOLO_GBS lanes (LDS-bound)
 constexpr int NUM_CU = 256;
 constexpr int SCORE_WG_PER_CU = 8;     // scoring workgroups per CU (full grid)
 constexpr int EMPTY = -1;

@@ -1011,16 +1011,22 @@ void launch_ground(const KParams &p, int agg, hipStream_t st, int grid) {
   const unsigned g = (unsigned)(grid > 0 ? std::min(grid, p.nslots) : p.nslots);
   // few rows (a reference batch per call): one 1024-lane workgroup per query,
   // so the batch's heaviest query — the launch's critical path — expands
-  // four times the frontier items and edges per pass
+  // four times the frontier items and edges per pass; beside another kernel
+  // (a capped grid) 256-lane workgroups; else 512 lanes (GBS / SOLO_GBS, fwd.h)
   const bool wide = p.nq <= WIDE_ROWS;
+  const bool beside = grid > 0;
   if (agg == RNNL_AGG_SUM && wide)
     hipLaunchKernelGGL((ground_kernel<RNNL_AGG_SUM, 1024>), dim3(g), dim3(1024), 0, st, p);
-  else if (agg == RNNL_AGG_SUM)
+  else if (agg == RNNL_AGG_SUM && beside)
     hipLaunchKernelGGL((ground_kernel<RNNL_AGG_SUM, GBS>), dim3(g), dim3(GBS), 0, st, p);
+  else if (agg == RNNL_AGG_SUM)
+    hipLaunchKernelGGL((ground_kernel<RNNL_AGG_SUM, SOLO_GBS>), dim3(g), dim3(SOLO_GBS), 0, st, p);
   else if (wide)
     hipLaunchKernelGGL((ground_kernel<RNNL_AGG_PNA, 1024>), dim3(g), dim3(1024), 0, st, p);
-  else
+  else if (beside)
     hipLaunchKernelGGL((ground_kernel<RNNL_AGG_PNA, GBS>), dim3(g), dim3(GBS), 0, st, p);
+  else
+    hipLaunchKernelGGL((ground_kernel<RNNL_AGG_PNA, SOLO_GBS>), dim3(g), dim3(SOLO_GBS), 0, st, p);
 }
 
 void set_score_params(KParams &p, const rnnl_predictor_params *pp, float *score, uint8_t *mask,
