@@ -1,7 +1,9 @@
 """Where a PredictorPlus training step (bench.py's train_step line: FB15k-237,
 B = 32, edge removal, RotatE feature, Adam) spends its time (diagnostic; GPU
 box): torch.profiler over 10 steps, top ops by device and by host time.
-Usage: python tools/train_profile.py"""
+`emb`: the final PredictorPlus stage of run_rnnlogic.py instead
+(PredictorPlus(graph, hidden_dim=16): emb / bias / sum, rnnlogic_rules.txt).
+Usage: python tools/train_profile.py [emb]"""
 import contextlib
 import os
 import sys
@@ -17,6 +19,12 @@ from rnnlogic_amd.trainer import TrainerPredictor  # noqa: E402
 dev = torch.device("cuda:0")
 with contextlib.redirect_stdout(sys.stderr):
     graph, test_set, model, rows = bench.build_workload("RotatE")
+    if len(sys.argv) > 1 and sys.argv[1] == "emb":
+        from rnnlogic_amd.predictors import PredictorPlus
+        train_set = model.train_set
+        model = PredictorPlus(graph, hidden_dim=16)
+        model.set_rules(bench.datasets.rule_file("FB15k-237"))
+        model.train_set = train_set
 model = model.to(dev)
 solver = TrainerPredictor(model, model.train_set, None, test_set, None, gpus=[0])
 solver.optimizer = torch.optim.Adam(model.parameters(), lr=5e-3)
