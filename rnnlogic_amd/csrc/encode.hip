@@ -36,9 +36,32 @@ struct LstmLds {
   float b[LMAXL][LG];
 };
 
-// 16 lanes per rule, lane j owns hidden unit j: its 4 gate rows, c_j, h_j and
-// its element of every step's layer output.  The step input and the previous
-// hidden state are exchanged with 16-wide shuffles.
+// Element K of a 16-lane row (a rule's group) broadcast to the row: one DPP
+// row_newbcast operand, no LDS traffic (ds_bpermute was 32 LDS ops per step).
+template <int K>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + K, 0xF, 0xF,
+                                                               false));
+}
+
+// The gate pre-activations of one step, k ascending (the order of the
+// shuffle form it replaces): a[q] += w[q][k] x_k + w[q][16 + k] h_k.
+template <int K>
+__device__ __forceinline__ void gate_terms(const float (&w)[4][2 * LH], float x, float h, float (&a)[4]) {
+  const float xk = row_bcast<K>(x), hk = row_bcast<K>(h);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[q] = fmaf(w[q][K], xk, a[q]);
+    a[q] = fmaf(w[q][LH + K], hk, a[q]);
+  }
+  if constexpr (K + 1 < LH) gate_terms<K + 1>(w, x, h, a);
+}
+
+// 16 lanes per rule, lane j owns hidden unit j: its 4 gate rows (in registers
+// for the layer's steps: the LDS image is read once per layer and rule
+// group, not once per step), c_j, h_j and its element of every step's layer
+// output.  The step input and the previous hidden state are broadcast within
+// the rule's 16-lane DPP row.
 __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restrict__ vocab, const float *__restrict__ w_ih,
                                                           const float *__restrict__ w_hh,
                                                           const float *__restrict__ b_ih,
@@ -67,22 +90,19 @@ __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restric
     for (int t = 0; t < LMAXT; ++t) seq[t] = vocab[(int64_t)tok[t < len ? t : 0] * LH + j];
 #pragma unroll 1
     for (int l = 0; l < layers; ++l) {
+      float w[4][2 * LH], bias[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bias[q] = S.b[l][q * LH + j];
+#pragma unroll
+        for (int k = 0; k < 2 * LH; ++k) w[q][k] = S.w[l][q * LH + j][k];
+      }
       float h = 0.f, c = 0.f;
 #pragma unroll
       for (int t = 0; t < LMAXT; ++t) {
-        if (t < len) {
-          float a[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) a[q] = S.b[l][q * LH + j];
-#pragma unroll
-          for (int k = 0; k < LH; ++k) {
-            const float xk = __shfl(seq[t], k, LH), hk = __shfl(h, k, LH);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              a[q] = fmaf(S.w[l][q * LH + j][k], xk, a[q]);
-              a[q] = fmaf(S.w[l][q * LH + j][LH + k], hk, a[q]);
-            }
-          }
+        if (t < len) {  // uniform over the rule's row (DPP reads of inactive lanes would return 0)
+          float a[4] = {bias[0], bias[1], bias[2], bias[3]};
+          gate_terms<0>(w, seq[t], h, a);
           c = fmaf(sigm(a[1]), c, sigm(a[0]) * tanhf(a[2]));
           h = sigm(a[3]) * tanhf(c);
           seq[t] = h;
