@@ -1,6 +1,7 @@
 #!/bin/bash
-# A/B of one environment switch over the bench lines (GPU box, repo root):
-#   VAR=RNNL_LPT VALS="0 1" LINES="bias wn rotate" bash tools/env_ab.sh
+# A/B of one environment variable over the bench lines (GPU box, repo root),
+# e.g. library builds from tools/build_variants.sh:
+#   VAR=RNNL_LIB VALS="rnnlogic_amd/_build/variants/a.so rnnlogic_amd/_build/variants/b.so" LINES="bias wn rotate" bash tools/env_ab.sh
 # optional GPU tests first (TESTS=1).  Two runs per value, interleaved.
 set -o pipefail
 o=gpurun_out/${TAG:-envab}; mkdir -p $o
