@@ -365,7 +365,8 @@ int rnnl_rotate_score_pieces(const float *eemb, const void *entity_table, const 
  * host call: rnnl_predictorplus_ground and rnnl_predictorplus_score
  * (deferred 2) on a side stream beside rnnl_rotate_score_pieces
  * (accumulate 2) on `stream`, into score rows zeroed on a second side
- * stream; mask (nullable, n_queries x E bytes) is filled with 1; then one
+ * stream; mask (nullable, n_queries x E bytes) is filled with 1 (on the
+ * second side stream, beside RotatE); then one
  * header read-back, the result as rnnl_forward_status_flags (RNNL_ERR_OVERFLOW:
  * call again with zeroed 0 and a doubled capacity_scale).  zeroed: 0 = the
  * call zeroes the rows first; 1 = rnnl_forward_rotate_zero(score, ...) was

@@ -1261,7 +1261,7 @@ static int status_from_header(const unsigned int *st, int64_t *totals);
 struct HostSide {
   unsigned int *pinned = nullptr;
   hipStream_t a = nullptr, b = nullptr;
-  hipEvent_t in = nullptr, zero = nullptr, side = nullptr;
+  hipEvent_t in = nullptr, zero = nullptr, side = nullptr, mask = nullptr;
 };
 
 static HostSide *host_side() {
@@ -1340,10 +1340,11 @@ int rnnl_forward_status_flags(void *ws, void *stream, int64_t *totals, uint32_t 
 
 // PredictorPlus forward with the RotatE entity feature in one host call: the
 // stream choreography of the overlap without a Python step per
-// launch.  Side stream B zeroes the score rows; side stream A grounds, then
-// (after the zero fill) scores with atomic adds; the caller's stream runs
-// RotatE with atomic adds after the zero fill, fills the all-True mask and
-// waits for A; then the header is read back (the only wait).  Ground is
+// launch.  Side stream B zeroes the score rows, then fills the all-True
+// mask beside RotatE; side stream A grounds, then (after the zero fill)
+// scores with atomic adds; the caller's stream runs RotatE with atomic adds
+// after the zero fill and waits for A and the mask; then the header is read
+// back (the only wait).  Ground is
 // enqueued before RotatE so its persistent workgroups are resident first.
 // The side streams / events of the overlap, created on first use.
 static HostSide *overlap_side(const char *who) {
@@ -1357,7 +1358,8 @@ static HostSide *overlap_side(const char *who) {
         hipStreamCreateWithFlags(&h->b, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->zero, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->side, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->side, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->mask, hipEventDisableTiming) != hipSuccess) {
       set_error(std::string(who) + ": side stream / event creation failed");
       h->a = nullptr;
       return nullptr;
@@ -1417,14 +1419,18 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
                                         scale, score_wg, 2, h->a))
     return rc;
   RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->zero, 0));
+  if (mask) {  // the all-True mask on side stream B beside RotatE (not behind it on `stream`)
+    RNNL_HIP_CHECK(hipMemsetAsync(mask, 1, (size_t)nq * (size_t)E, h->b));
+    RNNL_HIP_CHECK(hipEventRecord(h->mask, h->b));
+  }
   if (int rc = rnnl_rotate_score_pieces(rot->eemb, rot->etab, rot->rtab, rot->dim, rot->gamma, all_h, all_r, nq, E,
                                         score, 2, rot->mode, rot->workspace, rot->workspace_bytes, rot->pieces,
                                         rot->first_share, main))
     return rc;
-  if (mask) RNNL_HIP_CHECK(hipMemsetAsync(mask, 1, (size_t)nq * (size_t)E, main));
   RNNL_HIP_CHECK(mark(1));
   RNNL_HIP_CHECK(hipEventRecord(h->side, h->a));
   RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->side, 0));
+  if (mask) RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->mask, 0));
   RNNL_HIP_CHECK(mark(2));
   return rnnl_forward_status_flags(ws, main, totals, flags);
 }
