@@ -53,7 +53,8 @@ import torch  # noqa: E402
 
 TOL = 1e-4
 WINDOWS = (0.0, 1e-6, 2e-6, 5e-6, 1e-5, 2e-5, 5e-5, 1e-4)
-NCLOSE, NRAND = 12, 4
+# NCLOSE: --nclose (passed to the spawned workers through the environment)
+NCLOSE, NRAND = int(os.environ.get("RNNL_GOLDEN_NCLOSE", "12")), 4
 NPROBE = NCLOSE + NRAND
 _STATE = {}
 
@@ -207,7 +208,12 @@ def main():
     ap.add_argument("--rotate-rows", action="store_true", help="row-wise RotatE from the reference's methods")
     ap.add_argument("--cache", default="", help="directory of per-batch results (resumable long runs)")
     ap.add_argument("--out", default="", help="output path (default tests/golden/eval_<case>.npz)")
+    ap.add_argument("--nclose", type=int, default=NCLOSE,
+                    help="closest flagged competitors kept as probes (more: more rows accounted exactly)")
     a = ap.parse_args()
+    if a.nclose != NCLOSE:  # the module constant of this process and of the workers it spawns
+        os.environ["RNNL_GOLDEN_NCLOSE"] = str(a.nclose)
+        globals().update(NCLOSE=a.nclose, NPROBE=a.nclose + NRAND)
     if a.cache:
         os.makedirs(a.cache, exist_ok=True)
     graph, test_set, model = _build(a.case)
