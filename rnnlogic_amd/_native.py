@@ -5,13 +5,12 @@ in-tree (rnnlogic_amd/_build/librnnlogic_hip.so, see build()); if it is
 missing, every GPU entry point raises — there is no silent fallback.
 """
 import ctypes
+import functools
 import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "librnnlogic_hip.so")
-# diagnostic A/B builds (tools/build_variants.sh) may be selected with RNNL_LIB
-LIB_PATH = os.environ.get("RNNL_LIB") or LIB_PATH
 
 RNNL_OK, RNNL_ERR_INVALID, RNNL_ERR_HIP, RNNL_ERR_OVERFLOW, RNNL_ERR_NOMEM, RNNL_ERR_INTERNAL, RNNL_ERR_RANGE = \
     0, 1, 2, 3, 4, 5, 6
@@ -140,7 +139,7 @@ def lib():
                                "(or __graft_entry__.build())" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
-            # (a diagnostic build selected with RNNL_LIB may lack newer entry
+            # (an older A/B build loaded by tools/ab_run.py may lack newer entry
             # points: those raise when called; tests/test_host.py checks that
             # the shipped library exports every symbol of the header)
             f = getattr(L, name, None)
@@ -160,3 +159,42 @@ def check(rc):
 
 def call(name, *args):
     return check(getattr(lib(), name)(*args))
+
+
+def _run_on(index, fn, args, kw):
+    import torch
+    if index is None or index == torch.cuda.current_device():
+        return fn(*args, **kw)
+    with torch.cuda.device(index):
+        return fn(*args, **kw)
+
+
+def on_input_device(fn):
+    """Run a method with the current device set to the device of its first
+    tensor argument.  torch's default stream is the null stream (handle 0),
+    which HIP resolves against the *current* device, and the library's side
+    streams belong to the current device too: a caller whose tensors live on
+    cuda:k but whose current device is another (the reference trainer picks
+    cuda:k from `gpus` without set_device) would otherwise launch there."""
+    import torch
+
+    @functools.wraps(fn)
+    def wrapped(*args, **kw):
+        index = None
+        for a in args:
+            if isinstance(a, torch.Tensor):
+                index = a.device.index if a.is_cuda else None
+                break
+        return _run_on(index, fn, args, kw)
+    return wrapped
+
+
+def on_self_device(fn):
+    """on_input_device for methods of objects with a `device` attribute
+    (TrainerPredictor, the device batch builders)."""
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kw):
+        dev = getattr(self, "device", None)
+        index = dev.index if dev is not None and dev.type == "cuda" else None
+        return _run_on(index, fn, (self,) + args, kw)
+    return wrapped

@@ -1264,6 +1264,33 @@ struct HostSide {
   hipEvent_t in = nullptr, zero = nullptr, side = nullptr, mask = nullptr;
 };
 
+// Makes `dev` the current device for the guard's scope (restored after).
+// The host-side resources, the side streams and a null `stream` argument all
+// belong to the current device, which need not be the device of the tensors
+// (a caller on cuda:k that never called set_device).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    int cur = 0;
+    if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// The device of a stream argument: a null stream is the current device's.
+static int stream_device(void *stream) {
+  int dev = 0;
+  if (stream) {
+    if (hipStreamGetDevice((hipStream_t)stream, &dev) == hipSuccess) return dev;
+    return -1;
+  }
+  return hipGetDevice(&dev) == hipSuccess ? dev : -1;
+}
+
+// The current device's resources (callers hold a DeviceGuard for the device
+// of their data / stream).
 static HostSide *host_side() {
   thread_local std::map<int, HostSide> all;
   int dev = 0;
@@ -1278,6 +1305,7 @@ static HostSide *host_side() {
 
 // The launch header's status words into st (one read-back on `stream`).
 static int read_header(void *ws, void *stream, unsigned int (&st)[STATUS_WORDS]) {
+  DeviceGuard guard(stream_device(stream));
   HostSide *h = host_side();
   if (!h) {
     set_error("rnnl_forward_status: no pinned header buffer");
@@ -1377,6 +1405,7 @@ int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream) {
     set_error("rnnl_forward_rotate_zero: bad arguments");
     return RNNL_ERR_INVALID;
   }
+  DeviceGuard guard(stream_device(stream));
   HostSide *h = overlap_side("rnnl_forward_rotate_zero");
   if (!h) return RNNL_ERR_HIP;
   RNNL_HIP_CHECK(hipEventRecord(h->in, (hipStream_t)stream));
@@ -1386,21 +1415,14 @@ int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream) {
   return RNNL_OK;
 }
 
-int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp,
-                                      const rnnl_rotate_args *rot, const int64_t *all_h, const int64_t *all_r,
-                                      const int64_t *etr, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
-                                      uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t ground_wg,
-                                      int32_t score_wg, int32_t zeroed, void *const *events, void *stream,
-                                      int64_t *totals, uint32_t *flags) {
-  if (bad_params(pp, score) || !rot || !n_cand || !ws || nq < 0 || pp->feature != RNNL_FEATURE_ADD) {
-    set_error("rnnl_predictorplus_forward_rotate: bad arguments");
-    return RNNL_ERR_INVALID;
-  }
-  if (nq == 0) return RNNL_OK;
-  HostSide *h = overlap_side("rnnl_predictorplus_forward_rotate");
-  if (!h) return RNNL_ERR_HIP;
-  hipStream_t main = (hipStream_t)stream;
-  const int32_t E = rot->n_entities;
+// The launches of rnnl_predictorplus_forward_rotate (everything but the
+// header read-back).  On an error the caller joins the side streams.
+static int forward_rotate_enqueue(HostSide *h, rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp,
+                                  const rnnl_rotate_args *rot, const int64_t *all_h, const int64_t *all_r,
+                                  const int64_t *etr, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
+                                  uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t ground_wg,
+                                  int32_t score_wg, int32_t zeroed, void *const *events, hipStream_t main,
+                                  int32_t E) {
   // events[0..2] (nullable, timing): before the launches, after RotatE and the
   // mask, after the side stream's work (PredictorPlus.forward_rows `events`)
   auto mark = [&](int k) -> hipError_t {
@@ -1411,6 +1433,11 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
   RNNL_HIP_CHECK(hipEventRecord(h->in, main));
   RNNL_HIP_CHECK(mark(0));
   RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->in, 0));
+  // B fills `mask`, which the caller allocated after the zero fill was
+  // enqueued: B must also be ordered after everything the caller's stream
+  // has queued up to now (the allocator may have recycled a block that
+  // kernels queued there still read)
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->b, h->in, 0));
   if (int rc = rnnl_predictorplus_ground(g, r, pp->aggregator, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
                                          ground_wg, h->a))
     return rc;
@@ -1432,6 +1459,40 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
   RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->side, 0));
   if (mask) RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->mask, 0));
   RNNL_HIP_CHECK(mark(2));
+  return RNNL_OK;
+}
+
+int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp,
+                                      const rnnl_rotate_args *rot, const int64_t *all_h, const int64_t *all_r,
+                                      const int64_t *etr, int32_t nq, float *score, uint8_t *mask, int32_t *n_cand,
+                                      uint64_t *digest, void *ws, size_t ws_bytes, int32_t scale, int32_t ground_wg,
+                                      int32_t score_wg, int32_t zeroed, void *const *events, void *stream,
+                                      int64_t *totals, uint32_t *flags) {
+  if (bad_params(pp, score) || !rot || !n_cand || !ws || nq < 0 || pp->feature != RNNL_FEATURE_ADD) {
+    set_error("rnnl_predictorplus_forward_rotate: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (nq == 0) return RNNL_OK;
+  // the graph's device: the side streams, the host resources and a null
+  // `stream` must all be that device's (the caller's current device may differ)
+  DeviceGuard guard(g->device);
+  HostSide *h = overlap_side("rnnl_predictorplus_forward_rotate");
+  if (!h) return RNNL_ERR_HIP;
+  hipStream_t main = (hipStream_t)stream;
+  const int32_t E = rot->n_entities;
+  const int rc = forward_rotate_enqueue(h, g, r, pp, rot, all_h, all_r, etr, nq, score, mask, n_cand, digest, ws,
+                                        ws_bytes, scale, ground_wg, score_wg, zeroed, events, main, E);
+  if (rc) {
+    // a failed enqueue may leave work on side streams A / B that writes the
+    // caller's buffers (score, mask, n_cand, ws): join both into `stream`
+    // before returning, so that the caller's allocator (which orders frees on
+    // `stream`) cannot hand those buffers out while they are still written
+    if (hipEventRecord(h->side, h->a) == hipSuccess) (void)hipStreamWaitEvent(main, h->side, 0);
+    if (hipEventRecord(h->mask, h->b) == hipSuccess) (void)hipStreamWaitEvent(main, h->mask, 0);
+    (void)hipStreamSynchronize(h->a);
+    (void)hipStreamSynchronize(h->b);
+    return rc;
+  }
   return rnnl_forward_status_flags(ws, main, totals, flags);
 }
 

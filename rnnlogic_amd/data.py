@@ -282,6 +282,9 @@ class _RowTable(object):
     def rows(self, batches, indices):
         tab, lens, off = self.get(batches)
         idx = np.asarray(list(indices), dtype=np.int64)
+        idx = np.where(idx < 0, idx + len(lens), idx)  # Python indexing; `off` has one more entry
+        if idx.size and (idx.min() < 0 or idx.max() >= len(lens)):
+            raise IndexError("batch index out of range")
         n = lens[idx]
         # positions of the selected batches' rows, in the order of `indices`
         sel = np.repeat(off[idx] - (np.cumsum(n) - n), n) + np.arange(int(n.sum()), dtype=np.int64)
@@ -322,9 +325,16 @@ class DeviceTrainBatches(object):
     def __len__(self):
         return len(self.train_set)
 
+    @_native.on_self_device
     def __getitem__(self, idx):
         E = self.train_set.graph.entity_size
         tab, lens, off = self.table.get(self.train_set.batches)
+        n = len(lens)
+        idx = int(idx)
+        if idx < 0:  # Python indexing, as train_set[idx]; `off` has n + 1 entries
+            idx += n
+        if not 0 <= idx < n:
+            raise IndexError("DeviceTrainBatches index out of range")
         B = int(lens[idx])
         out = torch.empty((4, B), dtype=torch.int64, device=self.device)  # h, r, t, edges_to_remove
         target = torch.empty((B, E), dtype=torch.float32, device=self.device)
@@ -335,7 +345,7 @@ class DeviceTrainBatches(object):
                      out[3].data_ptr(), target.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
         return out[0], out[1], out[2], target, out[3]
 
-
+    @_native.on_self_device
     def rows(self, idx):
         """(all_h, all_r, all_t, edges_to_remove) of many batches at once
         (their concatenation, in `idx` order), without the dense targets."""
@@ -363,6 +373,7 @@ class DeviceEvalBatches(object):
     def __len__(self):
         return len(self.eval_set)
 
+    @_native.on_self_device
     def rows(self, indices):
         E = self.eval_set.graph.entity_size
         all_h, all_r, all_t = self.table.rows(self.eval_set.batches, indices)

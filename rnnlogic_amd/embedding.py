@@ -129,6 +129,7 @@ class RotatE(torch.nn.Module):
             self._args = a = (key, args)
         return a[1]
 
+    @_native.on_input_device
     def score_into(self, all_h, all_r, out, accumulate=False, pieces=1, first_share=0.0):
         """out (B, |E|) (+)= gamma - dist(h o r, e) for every entity (HIP);
         accumulate 2: atomic adds (rnnl_rotate_score).  pieces > 1: the same
@@ -162,6 +163,7 @@ class RotatE(torch.nn.Module):
         diff = torch.stack([re_hr.unsqueeze(1) - re_t.unsqueeze(0), im_hr.unsqueeze(1) - im_t.unsqueeze(0)], dim=0)
         return self.gamma - diff.norm(dim=0).sum(dim=-1)
 
+    @_native.on_input_device
     def forward_grad(self, all_h, all_r):
         """Differentiable (B, |E|) scores for training: the HIP scorer forward
         and rnnl_rotate_backward (_RotatEScore); h o r by torch ops, as in
@@ -178,6 +180,7 @@ class RotatE(torch.nn.Module):
         im_hr = re_h * im_r + im_h * re_r
         return _RotatEScore.apply(self.eemb, re_hr, im_hr, self, all_h, all_r)
 
+    @_native.on_input_device
     def forward(self, all_h, all_r):
         """(B, |E|) = gamma - sum_d |h o r - e| (embedding.py:64-70): the HIP
         kernel; with autograd active (training) the same kernel plus its HIP

@@ -154,6 +154,7 @@ class _HipGrounding(object):
         self._ws_uses[ws.data_ptr()] = self._ws_uses.get(ws.data_ptr(), 0) + 1
         return self._ws_uses[ws.data_ptr()]
 
+    @_native.on_input_device
     def ground(self, all_h, all_r, edges_to_remove=None, totals=None):
         """Grounding of every rule of every row into the workspace (HIP
         rnnl_ground).  Returns (ws, scale, n_cand (n,) int32); `totals` as in
@@ -171,6 +172,7 @@ class _HipGrounding(object):
         ws, scale = self._launch(device, nq, run, totals)
         return ws, scale, n_cand
 
+    @_native.on_input_device
     def ground_coo(self, all_h, all_r, edges_to_remove=None):
         """The grounding of every rule of every row as the COO of the
         reference's stacked rule_count matrix (HIP: rnnl_ground + export).
@@ -222,6 +224,7 @@ class _RuleGrounder(_HipGrounding):
         self._flags = np.zeros(1, dtype=np.uint32)
         self.capacity_scale = 1
 
+    @_native.on_input_device
     def counts(self, h, edges_to_remove):
         """(B, |E|) int64 path counts of the rule from each h."""
         device = h.device
@@ -354,12 +357,14 @@ class Predictor(_HipGrounding, torch.nn.Module):
             self._roots[key] = (list(roots)[:self.num_relations], max(int(mh.value), 1))
         return self._roots[key]
 
+    @_native.on_input_device
     def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False):
         """Forward for any rows (one or many reference batches, mixed
         relations): (score (n, |E|) f32, mask (n, |E|) bool[, n_cand])."""
         score, mask, n_cand, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
+    @_native.on_input_device
     def prefetch(self, all_h, all_r, edges_to_remove=None):
         """Ground these rows now, on a side stream, for a forward that will be
         called with the same tensor objects (the training loop's lookahead:
@@ -546,6 +551,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
     def mask_all_true(self):
         return self.entity_feature == "bias"
 
+    @_native.on_input_device
     def forward(self, all_h, all_r, edges_to_remove):
         """predictors.py:53-80: one single-relation batch -> (score, mask).
         With autograd (training) the same HIP forward runs inside
@@ -561,6 +567,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
             score = torch.where(mask.any(), score, torch.full_like(score, float("inf")))
         return score, mask
 
+    @_native.on_input_device
     def forward_autograd(self, all_h, all_r, edges_to_remove):
         """Differentiable forward (training): the HIP grounding's COO, then
         score = scatter of sum(count x node weight) with node weight = the sum
@@ -586,6 +593,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         return score.masked_fill(~mask, float("-inf")), mask
 
     @torch.no_grad()
+    @_native.on_input_device
     def compute_H(self, all_h, all_r, all_t, edges_to_remove):
         """Per-rule H scores (predictors.py:82-119): per row, pos = w x count at
         the true tail, neg = w x (sum of counts over candidates) / #candidates;
@@ -638,6 +646,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         return out
 
     @torch.no_grad()
+    @_native.on_input_device
     def compute_H_rows(self, all_h, all_r, all_t, edges_to_remove, chunk=8192):
         """Σ over rows of compute_H's per-row softmax (predictors.py:82-119),
         for rows of any relations in a few launches: the per-row terms are
@@ -876,8 +885,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if self.entity_feature == "bias":  # the scoring kernels add bias[t] without reading the filled row
             keep.append(self.bias.detach().float().contiguous())
             p.base_row = keep[-1].data_ptr()
-        # packed once per weight version, not per launch (a diagnostic RNNL_LIB
-        # build without rnnl_pack_weights packs per launch)
+        # packed once per weight version, not per launch (an older A/B build
+        # without rnnl_pack_weights packs per launch)
         if self.hidden_dim == 16 and getattr(_native.lib(), "rnnl_pack_weights", None) is not None:
             n = ctypes.c_size_t()
             _native.call("rnnl_pack_weights_floats", ctypes.byref(n))
@@ -904,6 +913,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         """Drop cached per-node rule aggregates (recomputed on the next forward)."""
         self._node_cache = {}
 
+    @_native.on_input_device
     def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False, digest=None, events=None,
                      dedupe=False):
         """Forward for any rows (one or many reference batches, mixed relations).
@@ -1042,6 +1052,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             return mask
 
     # ------------------------------------------------------------------ autograd (training) path
+    @_native.on_input_device
     def forward_autograd(self, all_h, all_r, edges_to_remove, query_r=None):
         """Differentiable forward (training): the HIP grounding's COO, then the
         reference's aggregation / MLP / entity feature as torch ops on it, so
@@ -1062,6 +1073,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
         return self._score_coo(all_h, all_r, row, ent, ce, node, count, rels=query_r)
 
+    @_native.on_input_device
     def forward_coo(self, all_h, all_r, edges_to_remove=None):
         """Rows of any relations through the HIP grounding COO and the torch
         aggregation / MLP (any hidden_dim): (score, mask, n_cand), the
@@ -1171,6 +1183,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             ridx = torch.cat([ridx, ridx.new_zeros(rows - n)])
         return self.encode_rules(tok.index_select(0, ridx))[:n]
 
+    @_native.on_input_device
     def forward(self, all_h, all_r, edges_to_remove):
         """predictors.py:210-271: one single-relation batch -> (score, mask).
 

@@ -148,6 +148,7 @@ class TrainerPredictor(object):
             dev = self._dev_batches = DeviceTrainBatches(self.train_set, self.device)
         return dev
 
+    @_native.on_self_device
     def train(self, batch_per_epoch, smoothing, print_every):
         """trainer.py:48-105."""
         if comm.get_rank() == 0:
@@ -221,6 +222,7 @@ class TrainerPredictor(object):
             yield b
             pull()  # after the step: its inputs are queued, and the ring slot it frees is the oldest
 
+    @_native.on_self_device
     def train_step(self, model, batch, smoothing, sync=True):
         """One optimizer step on one batch (trainer.py:72-98); returns
         (loss, mask size) or (None, None) when the batch has no candidate.
@@ -266,6 +268,7 @@ class TrainerPredictor(object):
 
     # ------------------------------------------------------------------ H scores
     @torch.no_grad()
+    @_native.on_self_device
     def compute_H(self, print_every):
         """trainer.py:107-143 (the model must provide compute_H, e.g. Predictor)."""
         if comm.get_rank() == 0:
@@ -381,6 +384,7 @@ class TrainerPredictor(object):
         return out
 
     @torch.no_grad()
+    @_native.on_self_device
     def evaluate(self, split, expectation=True):
         """trainer.py:145-248 -> MRR."""
         if comm.get_rank() == 0:

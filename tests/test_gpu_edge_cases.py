@@ -148,3 +148,28 @@ def test_mixed_relation_batch_fails_like_the_reference(umls):
                 model(t(mixed[:, 0]), t(mixed[:, 1]), None)
             model(t(one[:, 0]), t(one[:, 1]), None)  # the flag does not stick
         plus.forward_rows(t(mixed[:, 0]), t(mixed[:, 1]), None)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_forward_on_second_device_with_current_device_elsewhere(umls):
+    """a model and rows on cuda:1 while the current device is
+    cuda:0 (the reference trainer picks cuda:k without set_device).  The
+    overlap's side streams, the header read-back and torch's null stream must
+    all be cuda:1's: the scores equal the same forward run on cuda:0."""
+    path, graph, _ = umls
+    outs = []
+    for k in (0, 1):
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", k)
+        torch.manual_seed(0)
+        model = PredictorPlus(graph, type="lstm", entity_feature="RotatE", aggregator="sum",
+                              embedding_path=datasets.rotate_path("umls", 200))
+        model.set_rules(datasets.rule_file("umls"))
+        model = model.to(dev).eval()
+        h = torch.arange(0, 64, device=dev) % graph.entity_size
+        r = torch.full_like(h, 3)
+        with torch.no_grad():
+            score, mask = model.forward_rows(h, r, None)
+        assert torch.cuda.current_device() == 0
+        outs.append((score.cpu(), mask.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

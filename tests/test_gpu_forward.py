@@ -110,12 +110,14 @@ def test_path_count_digests(case, dev):
         np.testing.assert_array_equal(dig.cpu().numpy().view(np.uint64), want_d)
 
 
-@pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "wn_emb_pna_bias"])
+@pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "wn_emb_pna_bias", "kinship_lstm_sum_none"])
 def test_full_test_split_digests(case, dev):
     """Size-independent property at full size: every test query of the
-    synthetic FB15k-237 graph (40,932, rules L <= 3, sum) and of WN18RR
-    (6,268, rules L <= 5, PNA: its two phase-B sweeps) grounds to exactly the
-    oracle's path counts (digest + candidate count), 8,192 rows per launch."""
+    synthetic FB15k-237 graph (40,932, rules L <= 3, sum), of WN18RR
+    (6,268, rules L <= 5, PNA: its two phase-B sweeps) and of kinship (5,343,
+    config 2's exact model: mined L <= 3 rules, no entity feature) grounds to
+    exactly the oracle's path counts (digest + candidate count), 8,192 rows
+    per launch."""
     fx = Fixture(case)
     model = build_model(fx, dev)
     g, orc = oracle_for(fx)

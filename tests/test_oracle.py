@@ -157,3 +157,55 @@ def test_rule_search_restatement_vs_reference_pool(data):
     from rnnlogic_amd import datasets
     g = ref.Graph(datasets.materialize(data))
     assert ref.rule_search_pool(g, 2) == golden_rules("rules_%s_L2" % data)
+
+
+def test_oracle_full_split_ranks_kinship_none(fixtures):
+    """Config 2's exact model (kinship lstm/sum, no entity feature) over ALL
+    178 test batches: the restatement's per-query filtered rank bounds equal
+    the reference's (tests/golden/eval_kinship_lstm_sum_none.npz, written by
+    the reference through tools/make_golden_eval.py) up to the flagged
+    competitors within 2e-5 of the target (the two sides sum in different
+    orders), and the metric code reproduces the fixture's metrics from its
+    own rows exactly."""
+    import os
+    from conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "eval_kinship_lstm_sum_none.npz"))
+    fx = fixtures("kinship_lstm_sum_none")
+    g = graph_for(fx)
+    rules = ref.Rules(fx.rule_path(), g.relation_size)
+    want = z["rows"]
+    ptr = z["batch_ptr"]
+    assert int(z["batches"]) == 178 and len(want) == 5343
+    w = list(z["windows"]).index(2e-5)
+    moved = 0
+    for k in range(int(z["batches"])):
+        b = want[ptr[k]:ptr[k + 1], :3]
+        flag = ref.test_flags(g, b)
+        score, mask = ref.predictorplus_forward(fx.sd, fx.cfg["model"], g, rules, b[:, 0], b[:, 1], None, None)
+        lh = np.asarray(ref.query_ranks(score, mask, flag, b[:, 2]), np.int64).reshape(-1, 2)
+        d = np.abs(lh - want[ptr[k]:ptr[k + 1], 3:5]).max(1)
+        allow = z["near_w"][ptr[k]:ptr[k + 1], w]
+        assert (d <= allow).all(), (k, np.nonzero(d > allow)[0])
+        moved += int((d > 0).sum())
+    m = ref.rank_metrics([tuple(int(x) for x in row[:5]) for row in want], len(want))
+    for key in ("MRR", "Hit1", "Hit3", "Hit10", "MR"):
+        assert abs(m[key] - float(z["metric/" + key])) <= 1e-12, key
+    print("kinship lstm/sum/none full split: %d rows, %d moved within their 2e-5 windows" % (len(want), moved))
+
+
+def test_headline_eval_fixture_is_verified_against_unpatched_reference():
+    """tests/golden/eval_fb_lstm_sum_rotate.npz (the headline model's full
+    split) was written with the reference's RotatE evaluated row by row
+    (tools/make_golden_eval.py --rotate-rows); `--verify` re-ran the whole
+    unpatched reference on two batches of two relations and found every
+    stored record of those rows bitwise equal.  The fixture lists them."""
+    import os
+    from conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "eval_fb_lstm_sum_rotate.npz"))
+    rows = z["rotate_verified_rows"]
+    assert len(rows) >= 64 and len(set(rows.tolist())) == len(rows)
+    rels = set(z["rows"][rows, 1].tolist())
+    assert len(rels) >= 2, rels
+    for b in z["rotate_verified_batches"]:
+        lo, hi = int(z["batch_ptr"][b]), int(z["batch_ptr"][b + 1])
+        assert set(range(lo, hi)) <= set(rows.tolist())

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Builds compile-flag variants of one kernel source (ground.hip or rotate.hip)
-# into rnnlogic_amd/_build/variants/<name>.so, for A/B runs selected at run
-# time with RNNL_LIB (e.g. VAR=RNNL_LIB VALS="rnnlogic_amd/_build/variants/a.so ..."
-# bash tools/env_ab.sh, or tools/bench_rotate.py).
+# into rnnlogic_amd/_build/variants/<name>.so, for A/B runs through
+# tools/ab_run.py (e.g. VAR=LIB VALS="rnnlogic_amd/_build/variants/a.so ..."
+# bash tools/env_ab.sh).
 # Usage: tools/build_variants.sh <source>.hip name "flags" [name "flags" ...]
 set -e
 src=$1

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of one environment variable over the bench lines (GPU box, repo root),
-# e.g. library builds from tools/build_variants.sh:
-#   VAR=RNNL_LIB VALS="rnnlogic_amd/_build/variants/a.so rnnlogic_amd/_build/variants/b.so" LINES="bias wn rotate" bash tools/env_ab.sh
+# or, with VAR=LIB, of library builds from tools/build_variants.sh (loaded
+# through tools/ab_run.py):
+#   VAR=LIB VALS="rnnlogic_amd/_build/variants/a.so rnnlogic_amd/_build/variants/b.so" LINES="bias wn rotate" bash tools/env_ab.sh
 # optional GPU tests first (TESTS=1).  Two runs per value, interleaved.
 set -o pipefail
 o=gpurun_out/${TAG:-envab}; mkdir -p $o
@@ -14,11 +15,12 @@ for rep in 1 2; do
 for v in ${VALS:-0 1}; do
   for l in ${LINES:-bias wn rotate}; do
     f=$o/${l}_$(basename "$v" .so)_$rep.log
+    if [ "$VAR" = LIB ]; then run="timeout -k 10 300 python -u tools/ab_run.py $v"; else run="env $VAR=$v timeout -k 10 300 python -u"; fi
     case $l in
-      bias) env $VAR=$v timeout -k 10 300 python -u bench.py --feature bias --no-cpu-baseline --profile-only > $f 2> $f.err ;;
-      rotate) env $VAR=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --profile-only > $f 2> $f.err ;;
-      wn) env $VAR=$v timeout -k 10 300 python -u tools/wn_profile.py > $f 2> $f.err ;;
-      kin) env $VAR=$v timeout -k 10 300 python -u tools/kin_profile.py > $f 2> $f.err ;;
+      bias) $run bench.py --feature bias --no-cpu-baseline --profile-only > $f 2> $f.err ;;
+      rotate) $run bench.py --no-cpu-baseline --profile-only > $f 2> $f.err ;;
+      wn) $run tools/wn_profile.py > $f 2> $f.err ;;
+      kin) $run tools/kin_profile.py > $f 2> $f.err ;;
     esac || { tail -20 $f.err; exit 1; }
     python - "$f" "$l" "$VAR=$v" <<'PY'
 import ast, json, sys

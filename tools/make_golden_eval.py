@@ -32,11 +32,17 @@ entity, diff()'s norm of the (re, im) pair taken over a trailing size-2 axis
 instead of a leading one (10x faster; the same torch norm of the same two
 values), the sum over dims, and gamma minus that.  Before use, this is checked
 to equal the unpatched forward bitwise on the first CHECK_ROWS rows.
+`--verify` re-runs the whole unpatched reference model (rules part and
+RotatE.forward as shipped) on test batch 0 and on the first batch of another
+relation (64 rows at B = 32), requires every stored record of those rows —
+(L, H), s_t, the windows' counts, the probe entities and their scores — to be
+bitwise what the unpatched reference gives, and records the verified batches
+and rows in the fixture (`rotate_verified_batches`, `rotate_verified_rows`).
 
 Output: tests/golden/eval_<case>.npz.  Long runs: FB15k-237 full test split
 (40,932 rows) takes ~25 min on 8 cores; rows are split over worker processes.
 
-Usage: python tools/make_golden_eval.py <case> [--batches N] [--workers W]
+Usage: python tools/make_golden_eval.py <case> [--batches N] [--workers W] [--rotate-rows] [--verify]
 """
 import argparse
 import os
@@ -78,7 +84,7 @@ def _build(name):
     return graph, test_set, model
 
 
-CHECK_ROWS = 3
+CHECK_ROWS = 32  # one full reference batch (3 before round 5; --verify covers 64 rows)
 
 
 def _rotate_rows(rot):
@@ -199,6 +205,42 @@ def metrics(rows, expectation=True):
     return dict(Hit1=hit1 / n, Hit3=hit3 / n, Hit10=hit10 / n, MR=mr / n, MRR=mrr / n)
 
 
+def verify(case, path):
+    """--verify: the unpatched reference on two batches of two relations
+    against the stored rows (see the module docstring); adds the verified
+    batch / row lists to the fixture at `path`."""
+    graph, test_set, model = _build(case)
+    z = dict(np.load(path))
+    ptr = z["batch_ptr"]
+    r0 = int(test_set[0][1][0])
+    other = next(i for i in range(1, len(test_set)) if int(test_set[i][1][0]) != r0)
+    done = []
+    for i in (0, other):
+        t0 = time.time()
+        _, got = _ranks_of_batch_with(graph, test_set, model, i)
+        lo, hi = int(ptr[i]), int(ptr[i + 1])
+        assert len(got) == hi - lo
+        for k, row in enumerate(got):
+            j = lo + k
+            assert tuple(row[:6]) == tuple(int(x) for x in z["rows"][j]), (i, k, row[:6], z["rows"][j])
+            assert np.float32(row[6]).tobytes() == np.float32(z["s_t"][j]).tobytes(), (i, k)
+            assert np.array_equal(row[7], z["near_w"][j]), (i, k)
+            assert np.array_equal(row[8].astype(np.int32), z["probe_ent"][j]), (i, k)
+            assert np.array_equal(row[9].view(np.uint32), np.asarray(z["probe_score"][j], np.float32).view(np.uint32)), (i, k)
+        done.append((i, lo, hi))
+        print("batch %d (relation %d, rows %d..%d): unpatched reference == stored rows bitwise (%.0f s)" % (
+            i, int(test_set[i][1][0]), lo, hi, time.time() - t0), flush=True)
+    z["rotate_verified_batches"] = np.asarray([d[0] for d in done], np.int64)
+    z["rotate_verified_rows"] = np.concatenate([np.arange(d[1], d[2]) for d in done]).astype(np.int64)
+    np.savez_compressed(path, **z)
+    print("%s: %d rows verified against the unpatched reference -> %s" % (case, len(z["rotate_verified_rows"]), path))
+
+
+def _ranks_of_batch_with(graph, test_set, model, i):
+    _STATE.update(g=graph, t=test_set, m=model)
+    return _ranks_of_batch(i)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("case")
@@ -210,7 +252,12 @@ def main():
     ap.add_argument("--out", default="", help="output path (default tests/golden/eval_<case>.npz)")
     ap.add_argument("--nclose", type=int, default=NCLOSE,
                     help="closest flagged competitors kept as probes (more: more rows accounted exactly)")
+    ap.add_argument("--verify", action="store_true",
+                    help="check an existing fixture's rows against the unpatched reference on two batches")
     a = ap.parse_args()
+    if a.verify:
+        verify(a.case, a.out or os.path.join(MG.OUT, "eval_%s.npz" % a.case))
+        return
     if a.nclose != NCLOSE:  # the module constant of this process and of the workers it spawns
         os.environ["RNNL_GOLDEN_NCLOSE"] = str(a.nclose)
         globals().update(NCLOSE=a.nclose, NPROBE=a.nclose + NRAND)
