@@ -255,19 +255,26 @@ def csrc_fingerprint():
 
 
 def isolated_ground_ms(model, graph, h, r, dev):
-    """Device time of the grounding + scoring kernels alone: one untimed
-    one-stream rnnl_predictorplus_forward over all rows into a scratch score."""
+    """Device time of the rule part of a bias-feature forward alone: one
+    untimed one-stream launch over all rows — the bias-row fill of the score
+    rows (rnnl_fill_rows: SURVEY §8(d)'s 4 B |E| score write) then
+    rnnl_predictorplus_forward (grounding + scoring) — so that the time, the
+    algorithmic bytes and the counter traffic (fill_rows_kernel included)
+    describe the same kernels."""
     import ctypes
     from rnnlogic_amd import _native
     nq = h.numel()
     with torch.no_grad():
-        scratch = torch.zeros((nq, graph.entity_size), dtype=torch.float32, device=dev)
+        scratch = torch.empty((nq, graph.entity_size), dtype=torch.float32, device=dev)
         ncs = torch.empty(nq, dtype=torch.int32, device=dev)
         params, keep = model._params(dev, model.node_weights(dev))
         ws = model._workspace(dev, nq, model.capacity_scale)
+        bias = torch.randn(graph.entity_size, device=dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st = torch.cuda.current_stream(dev).cuda_stream
+        torch.cuda.synchronize(dev)
         e0.record()
+        _native.call("rnnl_fill_rows", bias.data_ptr(), nq, graph.entity_size, scratch.data_ptr(), st)
         _native.call("rnnl_predictorplus_forward", model.graph.device_graph(dev), model.native_rules(dev).ptr,
                      ctypes.byref(params), h.data_ptr(), r.data_ptr(), None, nq, scratch.data_ptr(), None,
                      ncs.data_ptr(), None, ws.data_ptr(), ws.numel(), model.capacity_scale, st)
@@ -668,7 +675,7 @@ def main():
         ground_ms, ground_how = isolated_ground_ms(model, graph, h, r, dev), \
             "one untimed one-stream launch over all rows (isolated from RotatE)"
     elif args.feature != "RotatE":
-        ground_ms, ground_how = tail_ms, "timed steps (one stream)"
+        ground_ms, ground_how = base_ms + tail_ms, "timed steps (one stream: bias-row fill + ground + score)"
     else:
         ground_ms, ground_how = None, None
 
@@ -800,14 +807,18 @@ def main():
     rotate_bytes = 8.0 * D * E * ((nq + 15) // 16) + 8.0 * D * nq + 4.0 * nq * E
     if ground_ms is None:  # --profile-only with the RotatE overlap: no isolated grounding time
         ground_ms = float("nan")
-    gt = [gtraffic.get(k) for k in ("ground_kernel", "memo_sum_kernel", "score_sum_chunk_kernel",
+    # like for like: the counted kernels are the ones the time covers (the
+    # bias-row fill that writes SURVEY §8(d)'s 4 B |E| score rows included)
+    gt = [gtraffic.get(k) for k in ("fill_rows_kernel", "ground_kernel", "memo_sum_kernel", "score_sum_chunk_kernel",
                                     "score_pna_chunk_kernel", "pack_weights_kernel", "chunk_sum_kernel",
                                     "chunk_fill_kernel")]
     gt = sum(x for x in gt if x) or None
     ground = {"bound": "hbm", "achieved": round(ground_bytes / (ground_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(ground_bytes / (ground_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
               "traffic": gt, "traffic_source": "profiles/traffic_bias.json: " + traffic_note.get("bias", "n/a"),
-              "kernel": "ground_kernel + scoring (chunk list + memo_sum_kernel + score_sum_chunk_kernel)",
+              "kernel": "fill_rows (bias rows) + ground_kernel + scoring (chunk list + memo_sum_kernel + "
+                        "score_sum_chunk_kernel)",
+              "traffic_over_alg": round(gt / ground_bytes, 3) if gt else None,
               "ms": round(ground_ms, 3),
               "measured": ground_how,
               "alg_bytes": int(ground_bytes), "work": {"F": int(F), "T": int(T), "P": int(P), "C": C}}
@@ -836,13 +847,19 @@ def main():
                         "an add per term; the sqrt inside the reduction keeps it off the matrix cores); "
                         "157.3 TF/s is the fp32 peak shared by VALU and MFMA; entity-table bytes %.3g per launch"
                         % rotate_bytes}
-        # the SURVEY's algorithmic bytes for RotatE: X = 8 D |E| + 8 D B per
-        # reference batch (table + h∘r) plus the score write
+        # RotatE's HBM fraction from the counters (the bytes the launch moved,
+        # profiles/traffic_rotate.json) over its time; SURVEY §8(d)'s
+        # X = 8 D |E| + 8 D B per reference batch charges one entity-table
+        # read per 32-row batch (1,514 reads) — a formula, kept beside it
         x_bytes = len(test_set) * 8.0 * D * E + 8.0 * D * nq + 4.0 * nq * E
-        roof["hbm_view"] = {"bound": "hbm", "achieved": round(x_bytes / (base_ms * 1e-3) / 1e9, 1),
+        tr = traffic.get("rotate_%s_kernel" % mode)
+        roof["hbm_view"] = {"bound": "hbm", "achieved": round(tr / (base_ms * 1e-3) / 1e9, 1) if tr else None,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(x_bytes / (base_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                            "alg_bytes": x_bytes}
+                            "frac": round(tr / (base_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None,
+                            "bytes": tr, "bytes_source": "PMC counters (traffic_source)" if tr else "n/a",
+                            "survey_formula_bytes": x_bytes,
+                            "note": "survey_formula_bytes charges one entity-table read per reference batch; the "
+                                    "kernel reads each XCD's table slab once per launch (HBM fraction = counters)"}
         dominant = roof if not (ground_ms > base_ms) else ground
     else:
         dominant = ground

@@ -104,6 +104,12 @@ int rnnl_rules_head_roots(rnnl_rules r, int32_t *head_root, int32_t *max_head_no
  * FuncToNodeSum / FuncToNode (reference src/layers.py:53-126). */
 int rnnl_node_weights(rnnl_rules r, const float *rule_emb, int32_t ld, int32_t aggregator, const float *add_w,
                       void *node_w, void *stream);
+/* rnnl_node_weights for the trie of one head relation only (the records of
+ * every other node are left unset; the table's fixed-point shift then covers
+ * that head's nodes): a launch whose rows are all of relation `head` (a
+ * training batch) reads no other record. */
+int rnnl_node_weights_head(rnnl_rules r, int32_t head, const float *rule_emb, int32_t ld, int32_t aggregator,
+                           const float *add_w, void *node_w, void *stream);
 int rnnl_node_weights_size(rnnl_rules r, int32_t aggregator, size_t *bytes);
 
 /* Rule encoder (reference src/predictors.py:201-208, type 'lstm'): for each
@@ -479,6 +485,58 @@ int rnnl_nll_forward(const float *logits, const float *target, const int64_t *al
 int rnnl_nll_backward(const float *logits, const float *target, const int64_t *all_t, int32_t B, int32_t E,
                       float smoothing, const void *aux, const float *loss, const float *grad_out, float *grad,
                       void *stream);
+
+/* ------------------------------------------------ training backward (K2^T) --
+ * The gradient of PredictorPlus's rule part for the SUM aggregator: replaces
+ * torch autograd over the reference's forward (src/predictors.py:238-271,
+ * src/layers.py:9-77: rule_to_entity = relu(LayerNorm(Linear(sum of count x
+ * rule embedding))), cat with relation_emb, score_model MLP(32, [128, 1]),
+ * scatter into the score rows) as called by TrainerPredictor.train
+ * (src/trainer.py:84-93).  After rnnl_predictorplus_forward over the same
+ * rows (its workspace, capacity_scale and n_cand hold the grounding COO and
+ * the scoring chunk list; p is that forward's parameter block, node_w from
+ * rnnl_node_weights over `emb`; n_cand_total: that forward's candidate total,
+ * rnnl_forward_status_totals), given grad_score = dL/d score (n_queries x E),
+ * writes dL/d parameter for every parameter of the rule part:
+ *   emb: (n_rules x emb_ld) rows of the rule-embedding table the node weights
+ *        were built from (rules outside the launch's rows get 0);
+ *   add_w (16 x 16), add_b, ln_w, ln_b (16), s0_w (128 x 32), s0_b (128),
+ *   s1_w (128), s1_b (1), rel_emb (R x 16).
+ * The entity feature's gradient (bias: column sums of grad_score; RotatE:
+ * rnnl_rotate_backward) is the caller's.  head >= 0: every row is of that
+ * relation (a training batch; only its trie is touched), -1: any rows.
+ * scratch: rnnl_predictorplus_backward_size bytes.  Deterministic except for
+ * the fp64 atomic sums of the per-node and relation_emb gradients (order-
+ * dependent in the last fp64 bits only). */
+typedef struct {
+  float *emb;
+  int32_t emb_ld;
+  float *add_w, *add_b, *ln_w, *ln_b, *s0_w, *s0_b, *s1_w, *s1_b, *rel_emb;
+} rnnl_sum_grads;
+int rnnl_predictorplus_backward_size(rnnl_rules r, int32_t n_relations, size_t *bytes);
+int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p, const float *emb,
+                                int32_t emb_ld, const int64_t *all_r, int32_t n_queries, const float *grad_score,
+                                const int32_t *n_cand, int64_t n_cand_total, void *workspace, size_t workspace_bytes,
+                                int32_t capacity_scale, int32_t head, void *scratch, size_t scratch_bytes,
+                                const rnnl_sum_grads *grads, void *stream);
+
+/* ------------------------------------------------ 64-bit path counts --
+ * Rows whose path counts (or PNA degree) reach 2^32 fail the forward with
+ * RNNL_ERR_RANGE (the grounding kernel sums u32) and n_cand = -2; the
+ * reference counts in int64 (src/data.py:139-171).  rnnl_ground_wide grounds
+ * rows[0 .. n_rows) again with exact u64 counts, rule-end trie node by node
+ * (slow: O(|E|) per hop, for those rows only), appending (row, entity, node,
+ * count) entries in no particular order; *cursor receives the entry total
+ * (compare with cap; rerun with a larger buffer when it exceeds it).
+ * scratch: rnnl_ground_wide_scratch_bytes(n_rows).
+ * rnnl_forward_error_bits: the failed launch's error bits (synchronises):
+ * 8 count width, 16 node-table range, 32 feature-sum range. */
+int rnnl_ground_wide_scratch_bytes(rnnl_graph g, int32_t n_rows, size_t *bytes);
+int rnnl_ground_wide(rnnl_graph g, rnnl_rules r, const int64_t *all_h, const int64_t *all_r,
+                     const int64_t *edges_to_remove, const int32_t *rows, int32_t n_rows, void *scratch,
+                     size_t scratch_bytes, int32_t *out_row, int32_t *out_entity, int32_t *out_node,
+                     uint64_t *out_count, int64_t cap, uint64_t *cursor, void *stream);
+int rnnl_forward_error_bits(void *workspace, void *stream, uint32_t *bits);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,7 @@ AGG_SUM, AGG_PNA = 0, 1
 FEATURE_ADD, FEATURE_NONE = 0, 1
 ROTATE_DIRECT, ROTATE_MFMA = 0, 1
 FLAG_MIXED = 1
+ERR_COUNT_WIDTH, ERR_NODE_RANGE, ERR_ACC_RANGE = 8, 16, 32
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -38,6 +39,7 @@ SIGNATURES = [
     ("rnnl_rules_head_roots", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P]),
     ("rnnl_node_weights_size", ctypes.c_int, [_P, _I32, _P]),
+    ("rnnl_node_weights_head", ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P]),
     ("rnnl_lstm_encode", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _I32, _P]),
     ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     ("rnnl_predictorplus_forward", ctypes.c_int,
@@ -96,6 +98,13 @@ SIGNATURES = [
     ("rnnl_nll_aux_bytes", ctypes.c_int, [_I32, _P]),
     ("rnnl_nll_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _F32, _P, _P, _P, _P]),
     ("rnnl_nll_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _F32, _P, _P, _P, _P, _P]),
+    ("rnnl_ground_wide_scratch_bytes", ctypes.c_int, [_P, _I32, _P]),
+    ("rnnl_ground_wide", ctypes.c_int,
+     [_P, _P, _P, _P, _P, _P, _I32, _P, ctypes.c_size_t, _P, _P, _P, _P, _I64, _P, _P]),
+    ("rnnl_forward_error_bits", ctypes.c_int, [_P, _P, _P]),
+    ("rnnl_predictorplus_backward_size", ctypes.c_int, [_P, _I32, _P]),
+    ("rnnl_predictorplus_backward", ctypes.c_int,
+     [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I64, _P, ctypes.c_size_t, _I32, _I32, _P, ctypes.c_size_t, _P, _P]),
 ]
 
 
@@ -104,6 +113,12 @@ class PredictorParams(ctypes.Structure):
     _fields_ = [("aggregator", _I32), ("feature", _I32), ("node_w", _P), ("add_w", _P), ("add_b", _P),
                 ("ln_w", _P), ("ln_b", _P), ("s0_w", _P), ("s0_b", _P), ("s1_w", _P), ("s1_b", _P),
                 ("rel_emb", _P), ("base_row", _P), ("packed", _P)]
+
+
+class SumGrads(ctypes.Structure):
+    """rnnl_sum_grads (include/rnnlogic_hip.h)."""
+    _fields_ = [("emb", _P), ("emb_ld", _I32), ("add_w", _P), ("add_b", _P), ("ln_w", _P), ("ln_b", _P),
+                ("s0_w", _P), ("s0_b", _P), ("s1_w", _P), ("s1_b", _P), ("rel_emb", _P)]
 
 
 class RotateArgs(ctypes.Structure):

@@ -259,6 +259,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   rs->d.n_heads = R;
   rs->node_of_rule = std::move(node_of_rule);
   rs->head_root = head_root;
+  rs->head_nodes = head_nodes;
   rs->d.max_leaves = max_leaves;
   rs->d.max_head_nodes = max_head_nodes;
   std::vector<int32_t> node_info(4 * node_rel.size());

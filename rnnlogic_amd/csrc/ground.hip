@@ -788,14 +788,15 @@ void launch_chunk_list(const KParams &p, hipStream_t st) {
 // sum, y[o] = sum_i add_w[o][i] x[i] (fp32, i ascending; x from the node's 16
 // lanes by width-16 shuffles): the Linear commutes with the candidate's sum of
 // count x record, so the scoring pass adds only its bias.
-__global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const float *__restrict__ emb, int ld,
-                                                          int agg, const float *__restrict__ add_w,
+// Nodes [lo, lo + cnt) (all of them, or one head relation's trie).
+__global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, int lo, int cnt, const float *__restrict__ emb,
+                                                          int ld, int agg, const float *__restrict__ add_w,
                                                           unsigned char *__restrict__ out) {
-  const int64_t total = (int64_t)rl.n_nodes * 16;
+  const int64_t total = (int64_t)cnt * 16;
   unsigned int m = 0, m2 = 0;
   for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
        gid += (int64_t)gridDim.x * blockDim.x) {
-    const int n = (int)(gid >> 4), d = (int)(gid & 15);
+    const int n = lo + (int)(gid >> 4), d = (int)(gid & 15);
     float s1 = 0.f, s2 = 0.f, mn = __builtin_huge_valf(), mx = -__builtin_huge_valf();
     for (int k = rl.node_rule_ptr[n]; k < rl.node_rule_ptr[n + 1]; ++k) {
       const float x = emb[(int64_t)rl.node_rules[k] * ld + d];
@@ -851,7 +852,7 @@ __global__ __launch_bounds__(256) void node_weights_kernel(RulesDev rl, const fl
 // own table-wide shift (as the SUM table: every value fits 2^30, so count x
 // record is exact in int64); shifts in trailer[1] / trailer[4], trailer[2]
 // flags a table that cannot be represented (or held a NaN min / max).
-__global__ void pna_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
+__global__ void pna_fix_kernel(int n_nodes, int lo, int cnt, unsigned char *__restrict__ out) {
   unsigned int *trailer = reinterpret_cast<unsigned int *>(out + (int64_t)n_nodes * kStridePna);
   const unsigned int b1 = trailer[0], b2 = trailer[3];
   int e1 = 0, e2 = 0;
@@ -866,9 +867,9 @@ __global__ void pna_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
     trailer[2] = bad ? 1u : 0u;
   }
   const float sc1 = ldexpf(1.f, sh1), sc2 = ldexpf(1.f, sh2);
-  const int64_t n = (int64_t)n_nodes * 32;
+  const int64_t n = (int64_t)cnt * 32;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t node = i >> 5;
+    const int64_t node = lo + (i >> 5);
     const int w = (int)(i & 31);
     float *rec = reinterpret_cast<float *>(out + node * kStridePna);
     const float f = rec[w];
@@ -914,17 +915,17 @@ __global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent
 // count x fix is exact (deterministic in any entry order) with ~2^-30
 // relative resolution.  Trailer: u32 max|x| bits, i32 shift (fix_shift), bad flag, u32 max|sum x| bits
 // before the Linear fold (range-checked as well).
-__global__ void node_fix_kernel(int n_nodes, unsigned char *__restrict__ out) {
+__global__ void node_fix_kernel(int n_nodes, int lo, int cnt, unsigned char *__restrict__ out) {
   unsigned int *trailer = reinterpret_cast<unsigned int *>(out + (int64_t)n_nodes * kStrideSum);
   bool bad;
   // trailer[3]: max |sum x| bits before the folded Linear — an aggregate of
   // 2^30 or more fails the launch as it did before the fold
   const int shift = fix_shift(trailer, bad, trailer[3]);
   const float sc = ldexpf(1.f, shift);
-  const int64_t n = (int64_t)n_nodes * 16;
+  const int64_t n = (int64_t)cnt * 16;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float *f = reinterpret_cast<float *>(out) + i;
-    reinterpret_cast<int *>(out)[i] = bad ? 0 : (int)rintf(*f * sc);
+    float *f = reinterpret_cast<float *>(out) + (int64_t)lo * 16 + i;
+    *reinterpret_cast<int *>(f) = bad ? 0 : (int)rintf(*f * sc);
   }
 }
 
@@ -1073,29 +1074,49 @@ using namespace rnnl;
 
 extern "C" {
 
-int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, const float *add_w, void *node_w,
-                      void *stream) {
+static int node_weights_range(const char *who, rnnl_rules r, int lo, int cnt, const float *emb, int32_t ld,
+                              int32_t agg, const float *add_w, void *node_w, void *stream) {
   if (!r || !emb || !node_w || (agg != RNNL_AGG_SUM && agg != RNNL_AGG_PNA) || ld < 16 ||
       (agg == RNNL_AGG_SUM && !add_w)) {
-    set_error("rnnl_node_weights: bad arguments");
+    set_error(std::string(who) + ": bad arguments");
     return RNNL_ERR_INVALID;
   }
-  const int64_t n = (int64_t)r->d.n_nodes * 16;
+  const int64_t n = (int64_t)cnt * 16;
   unsigned char *out = static_cast<unsigned char *>(node_w);
   RNNL_HIP_CHECK(hipMemsetAsync(out + (int64_t)r->d.n_nodes * (agg == RNNL_AGG_SUM ? kStrideSum : kStridePna), 0, 32,
                                 (hipStream_t)stream));
   if (n == 0) return RNNL_OK;
   const int bs = 256;
   hipLaunchKernelGGL(node_weights_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 2048)), dim3(bs), 0,
-                     (hipStream_t)stream, r->d, emb, ld, agg, add_w, out);
+                     (hipStream_t)stream, r->d, lo, cnt, emb, ld, agg, add_w, out);
   if (agg == RNNL_AGG_PNA)
     hipLaunchKernelGGL(pna_fix_kernel, dim3((unsigned)std::min<int64_t>((2 * n + bs - 1) / bs, 4096)), dim3(bs), 0,
-                       (hipStream_t)stream, r->d.n_nodes, out);
+                       (hipStream_t)stream, r->d.n_nodes, lo, cnt, out);
   if (agg == RNNL_AGG_SUM)
     hipLaunchKernelGGL(node_fix_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 4096)), dim3(bs), 0,
-                       (hipStream_t)stream, r->d.n_nodes, out);
+                       (hipStream_t)stream, r->d.n_nodes, lo, cnt, out);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
+}
+
+int rnnl_node_weights(rnnl_rules r, const float *emb, int32_t ld, int32_t agg, const float *add_w, void *node_w,
+                      void *stream) {
+  if (!r) {
+    set_error("rnnl_node_weights: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  return node_weights_range("rnnl_node_weights", r, 0, r->d.n_nodes, emb, ld, agg, add_w, node_w, stream);
+}
+
+int rnnl_node_weights_head(rnnl_rules r, int32_t head, const float *emb, int32_t ld, int32_t agg,
+                           const float *add_w, void *node_w, void *stream) {
+  if (!r || head < 0 || head >= (int)r->head_root.size()) {
+    set_error("rnnl_node_weights_head: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  const int lo = r->head_root[head];
+  return node_weights_range("rnnl_node_weights_head", r, lo < 0 ? 0 : lo, lo < 0 ? 0 : r->head_nodes[head], emb, ld,
+                            agg, add_w, node_w, stream);
 }
 
 int rnnl_node_weights_size(rnnl_rules r, int32_t agg, size_t *bytes) {

@@ -88,6 +88,7 @@ struct rnnl_rules_s {
   void *mem[16] = {};
   std::vector<int32_t> node_of_rule;  // host: trie node where each rule's body ends
   std::vector<int32_t> head_root;     // host copy of d.head_root (R)
+  std::vector<int32_t> head_nodes;    // host copy of d.head_nodes (R)
 };
 
 #define RNNL_HIP_CHECK(expr)                                                              \

@@ -36,7 +36,14 @@ class _RotatEScore(torch.autograd.Function):
         eemb, hr_re, hr_im = ctx.saved_tensors
         E, D = ctx.module.num_entities, ctx.module.emb_dim
         nq = hr_re.size(0)
-        planes = eemb.detach().view(E, 2, D).permute(2, 1, 0).contiguous()  # [D][2][E]
+        if ctx.module.mode == _native.ROTATE_DIRECT:
+            # the forward's entity planes [D][2][Ep] (rnnl_rotate_entity_table,
+            # cached for this weight version): no transposed copy of the table
+            planes = ctx.module._device_tables()[0]
+            ld = planes.numel() // (2 * D)
+        else:
+            planes = eemb.detach().view(E, 2, D).permute(2, 1, 0).contiguous()  # [D][2][E]
+            ld = E
         hr = torch.cat([hr_re, hr_im], dim=1).detach().float().contiguous()
         grad = grad.detach().float().contiguous()
         d_hr = torch.zeros((nq, 2 * D), dtype=torch.float32, device=eemb.device)
@@ -44,7 +51,7 @@ class _RotatEScore(torch.autograd.Function):
         # trained remb still needs d(h o r))
         need_tail = ctx.needs_input_grad[0]
         d_tail = torch.empty((D, 2, E), dtype=torch.float32, device=eemb.device) if need_tail else None
-        _native.call("rnnl_rotate_backward", planes.data_ptr(), E, hr.data_ptr(), grad.data_ptr(), nq, E, D,
+        _native.call("rnnl_rotate_backward", planes.data_ptr(), ld, hr.data_ptr(), grad.data_ptr(), nq, E, D,
                      d_hr.data_ptr(), d_tail.data_ptr() if need_tail else None,
                      torch.cuda.current_stream(eemb.device).cuda_stream)
         d_eemb = d_tail.permute(2, 1, 0).reshape(E, 2 * D) if need_tail else None

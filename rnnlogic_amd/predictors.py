@@ -128,11 +128,13 @@ class _HipGrounding(object):
         (predictors.py:54-55, 211-212), from the last launch's flags."""
         assert not (int(self._flags[0]) & _native.FLAG_MIXED), "a batch must hold one relation (predictors.py:54-55)"
 
-    def _launch(self, device, nq, run, totals=None):
+    def _launch(self, device, nq, run, totals=None, tolerate_range=False):
         """run(ws, scale) launches onto the workspace; retried with a doubled
         capacity_scale while the launch reports overflow.  Returns (ws, scale).
         `totals` (int64[2] numpy array): filled with the grounding's candidate
-        and bucket-entry totals by the same read-back as the status."""
+        and bucket-entry totals by the same read-back as the status.
+        tolerate_range: return on RNNL_ERR_RANGE as well (the caller reads
+        the rows' n_cand: -2 marks a row whose path counts reached 2^32)."""
         stream = torch.cuda.current_stream(device).cuda_stream
         while True:
             scale = self.capacity_scale
@@ -144,7 +146,8 @@ class _HipGrounding(object):
                 logging.info("%s: workspace overflow, capacity_scale -> %d", type(self).__name__,
                              self.capacity_scale)
                 continue
-            _native.check(rc)
+            if not (tolerate_range and rc == _native.RNNL_ERR_RANGE):
+                _native.check(rc)
             self._ws_touch(ws)
             return ws, scale
 
@@ -155,10 +158,10 @@ class _HipGrounding(object):
         return self._ws_uses[ws.data_ptr()]
 
     @_native.on_input_device
-    def ground(self, all_h, all_r, edges_to_remove=None, totals=None):
+    def ground(self, all_h, all_r, edges_to_remove=None, totals=None, tolerate_range=False):
         """Grounding of every rule of every row into the workspace (HIP
-        rnnl_ground).  Returns (ws, scale, n_cand (n,) int32); `totals` as in
-        _launch."""
+        rnnl_ground).  Returns (ws, scale, n_cand (n,) int32); `totals` and
+        `tolerate_range` as in _launch."""
         device, all_h, all_r, etr = self._rows(all_h, all_r, edges_to_remove)
         nq = all_h.numel()
         g, nr = self.graph.device_graph(device), self.native_rules(device)
@@ -169,11 +172,69 @@ class _HipGrounding(object):
             _native.call("rnnl_ground", g, nr.ptr, all_h.data_ptr(), all_r.data_ptr(),
                          etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(),
                          ws.numel(), scale, stream)
-        ws, scale = self._launch(device, nq, run, totals)
+        ws, scale = self._launch(device, nq, run, totals, tolerate_range)
         return ws, scale, n_cand
 
     @_native.on_input_device
     def ground_coo(self, all_h, all_r, edges_to_remove=None):
+        """The grounding COO (see _ground_coo) with exact int64 counts for
+        every row: rows whose path counts reach 2^32 (the grounding kernel's
+        u32 sums; RNNL_ERR_RANGE) are grounded again by rnnl_ground_wide, as
+        the reference counts in int64 (src/data.py:139-171)."""
+        try:
+            return self._ground_coo(all_h, all_r, edges_to_remove)
+        except _native.NativeError as e:
+            if e.code != _native.RNNL_ERR_RANGE:
+                raise
+        return self._ground_coo_wide(all_h, all_r, edges_to_remove)
+
+    def _ground_coo_wide(self, all_h, all_r, edges_to_remove):
+        device, h, r, etr = self._rows(all_h, all_r, edges_to_remove)
+        nq, E = h.numel(), self.graph.entity_size
+        _, _, n_cand = self.ground(h, r, etr, tolerate_range=True)
+        bad = torch.nonzero(n_cand == -2).squeeze(1)
+        good = torch.nonzero(n_cand != -2).squeeze(1)
+        keys, nodes, counts = [], [], []
+        if good.numel():
+            row, ent, ce, node, count = self._ground_coo(h[good], r[good], etr[good] if etr is not None else None)
+            keys.append(good[row][ce] * E + ent[ce])
+            nodes.append(node)
+            counts.append(count)
+        if bad.numel():
+            g, nr = self.graph.device_graph(device), self.native_rules(device)
+            stream = torch.cuda.current_stream(device).cuda_stream
+            rows32 = bad.to(torch.int32).contiguous()
+            sb = ctypes.c_size_t()
+            _native.call("rnnl_ground_wide_scratch_bytes", g, rows32.numel(), ctypes.byref(sb))
+            scratch = torch.empty(sb.value, dtype=torch.uint8, device=device)
+            cursor = torch.zeros(1, dtype=torch.int64, device=device)
+            cap = 1 << 16
+            while True:
+                o_row = torch.empty(cap, dtype=torch.int32, device=device)
+                o_ent = torch.empty(cap, dtype=torch.int32, device=device)
+                o_node = torch.empty(cap, dtype=torch.int32, device=device)
+                o_cnt = torch.empty(cap, dtype=torch.int64, device=device)
+                _native.call("rnnl_ground_wide", g, nr.ptr, h.data_ptr(), r.data_ptr(),
+                             etr.data_ptr() if etr is not None else None, rows32.data_ptr(), rows32.numel(),
+                             scratch.data_ptr(), scratch.numel(), o_row.data_ptr(), o_ent.data_ptr(),
+                             o_node.data_ptr(), o_cnt.data_ptr(), cap, cursor.data_ptr(), stream)
+                n = int(cursor.item())
+                if n <= cap:
+                    break
+                cap = n
+            keys.append(o_row[:n].to(torch.int64) * E + o_ent[:n].to(torch.int64))
+            nodes.append(o_node[:n].to(torch.int64))
+            counts.append(o_cnt[:n])  # u64 counts < 2^63 (more paths than int64 would hold: as the reference)
+        key = torch.cat(keys) if keys else torch.zeros(0, dtype=torch.int64, device=device)
+        node = torch.cat(nodes) if nodes else torch.zeros(0, dtype=torch.int64, device=device)
+        count = torch.cat(counts) if counts else torch.zeros(0, dtype=torch.int64, device=device)
+        # the reference's order: candidates row-major by entity (nonzero), entries by node
+        order = torch.argsort(key * max(self.native_rules(device).n_nodes, 1) + node)
+        key, node, count = key[order], node[order], count[order]
+        cand, ce = torch.unique_consecutive(key, return_inverse=True)
+        return cand // E, cand % E, ce, node, count
+
+    def _ground_coo(self, all_h, all_r, edges_to_remove=None):
         """The grounding of every rule of every row as the COO of the
         reference's stacked rule_count matrix (HIP: rnnl_ground + export).
 
@@ -206,6 +267,171 @@ class _HipGrounding(object):
         cand_of_entry = torch.repeat_interleave(torch.arange(C, device=device), nent, output_size=P)
         # path counts are u32 in the kernel (< 2^32, carry-checked): reinterpret the int32 bits
         return row, ent, cand_of_entry, node[:P].to(torch.int64), count[:P].to(torch.int64) & 0xFFFFFFFF
+
+    @_native.on_input_device
+    def prefetch(self, all_h, all_r, edges_to_remove=None):
+        """Ground these rows now, on a side stream, for a forward that will be
+        called with the same tensor objects (the training loop's lookahead:
+        the grounding does not depend on the weights, so batch k + 1's runs
+        while batch k scores, steps back and updates).  Up to prefetch_depth
+        groundings are queued, each in its own workspace of a ring; a forward
+        whose rows are not the queue's head drops the queue."""
+        if self.prefetch_depth <= 0 or not self._prefetch_enabled():
+            return
+        device, h, r, etr = self._rows(all_h, all_r, edges_to_remove)
+        nq = h.numel()
+        if nq == 0:
+            return
+        key = self._device_index(device)
+        pf = self._pf.get(key)
+        if pf is None:
+            pf = self._pf[key] = {"stream": torch.cuda.Stream(device), "ring": {}, "next": 0,
+                                  "queue": collections.deque()}
+        if len(pf["queue"]) >= self.prefetch_depth:
+            return
+        g, nr = self.graph.device_graph(device), self.native_rules(device)
+        scale = self.capacity_scale
+        need = ctypes.c_size_t()
+        _native.call("rnnl_forward_workspace_size", g, nr.ptr, nq, scale, ctypes.byref(need))
+        # ring of depth + 1 workspaces: the forward in flight keeps one until its backward
+        slot = pf["next"] % (self.prefetch_depth + 1)
+        pf["next"] += 1
+        ws = pf["ring"].get(slot)
+        if ws is None or ws.numel() < need.value:
+            ws = pf["ring"][slot] = torch.empty(need.value, dtype=torch.uint8, device=device)
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        side, main = pf["stream"], torch.cuda.current_stream(device)
+        # inputs, and the slot's previous user (its backward is on the current stream already)
+        side.wait_stream(main)
+        self._prefetch_ground(g, nr, h, r, etr, nq, n_cand, ws, scale, side.cuda_stream)
+        # the grounding's status / totals and the one-relation flag, copied to the
+        # host behind it: the forward reads them without waiting for the current stream
+        # (pinned buffer and event of the ring slot: the slot's previous entry was
+        # consumed, or dropped behind the same side stream, before it comes round)
+        hdr, ev = self._host_slot(pf, "pf", slot, self.prefetch_depth + 1)
+        hb = self._header_bytes()
+        with torch.cuda.stream(side):
+            hdr[:hb].copy_(ws[:hb], non_blocking=True)  # status, totals and the one-relation flag
+            hdr[hb:hb + 8].copy_(r[:1].view(torch.uint8), non_blocking=True)  # the first row's relation
+        ev.record(side)
+        # the side stream's use of these blocks outlives a dropped queue entry or a
+        # grown ring slot: the caching allocator must not hand them out before it ends
+        for t in (ws, n_cand, h, r) + ((etr,) if etr is not None else ()):
+            t.record_stream(side)
+        self._ws_touch(ws)
+        pf["queue"].append((all_h, all_r, edges_to_remove, ws, scale, n_cand, ev, (h, r, etr), hdr))
+
+    def _host_slot(self, pf, name, k, n):
+        """(pinned header buffer, event) number k % n of a ring kept in pf:
+        reused instead of a pinned allocation and an event creation per step."""
+        ring = pf.get(name)
+        if ring is None or len(ring) != n:
+            hb = self._header_bytes() + 8  # + the first row's relation (int64)
+            ring = pf[name] = [(torch.empty(hb, dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
+                               for _ in range(n)]
+        return ring[k % n]
+
+    def _header_bytes(self):
+        if getattr(self, "_hdr_bytes", None) is None:
+            n = ctypes.c_size_t()
+            _native.call("rnnl_forward_header_bytes", ctypes.byref(n))
+            self._hdr_bytes = n.value
+        return self._hdr_bytes
+
+    def check_deferred(self, keep=0):
+        """Raise the scoring pass's own error (an integer range flag) of the
+        lookahead forwards, whose status is read late so the host does not
+        wait for the scoring: every pending status but the newest `keep`
+        (the training step checks the forward before last, which has long
+        finished; train() checks them all at its end).  The training steps of
+        those forwards have then already run their backward and optimizer
+        step on the flagged scores: the error names the forward, and a run
+        resumed from a checkpoint written after it should not trust it."""
+        q = getattr(self, "_deferred_status", None)
+        while q and len(q) > keep:
+            dh, ev, n = q.popleft()
+            ev.synchronize()
+            rc = _native.lib().rnnl_forward_status_host(dh.data_ptr(), None)
+            if rc != _native.RNNL_OK:
+                q.clear()
+                raise _native.NativeError(rc, "%s (scoring pass of lookahead forward #%d, read late: that step's "
+                                              "backward and optimizer update have already been applied)" % (
+                                                  _native.lib().rnnl_last_error().decode(errors="replace"), n))
+
+    def _prefetched(self, device, all_h, all_r, edges_to_remove, peek=False):
+        """The queued grounding of exactly these row tensors, or None.  Entries
+        grounded at another capacity_scale (a retry raised it since) and those
+        queued before the match (batches that ran without their lookahead) are
+        dropped; entries after it are later batches and stay queued.
+        peek: leave the match queued."""
+        pf = self._pf.get(self._device_index(device))
+        if not pf or not pf["queue"]:
+            return None
+        q = pf["queue"]
+        stale = [e for e in q if e[4] != self.capacity_scale]
+        if stale:
+            self._drop_lookahead(pf, [e for e in q if e[4] == self.capacity_scale], len(stale))
+            q = pf["queue"]
+        for i, e in enumerate(q):
+            if e[0] is all_h and e[1] is all_r and e[2] is edges_to_remove:
+                if i:
+                    self._drop_lookahead(pf, list(q)[i:], i)
+                    q = pf["queue"]
+                if peek:
+                    return q[0]
+                self.prefetch_hits = getattr(self, "prefetch_hits", 0) + 1
+                return q.popleft()
+        return None  # these rows were not grounded ahead; the queued ones are later batches
+
+    def _drop_lookahead(self, pf, keep, n):
+        # the side stream's work on dropped entries still ends before their
+        # ring slots come round again (record_stream, the slots' order)
+        self.prefetch_dropped += n
+        logging.debug(type(self).__name__ + ": %d lookahead groundings dropped (%d so far)", n, self.prefetch_dropped)
+        pf["queue"] = collections.deque(keep)
+
+    def _defer_status(self, device, ws):
+        """After a scoring pass on a prefetched grounding: its header copied
+        behind it into a pinned ring slot, checked two forwards later
+        (check_deferred) instead of waiting for the pass now."""
+        hb = self._header_bytes()
+        main = torch.cuda.current_stream(device)
+        self._lookahead_forwards = getattr(self, "_lookahead_forwards", 0) + 1
+        dh, dev_ev = self._host_slot(self._pf[self._device_index(device)], "dev", self._lookahead_forwards, 4)
+        dh[:hb].copy_(ws[:hb], non_blocking=True)
+        dev_ev.record(main)
+        if getattr(self, "_deferred_status", None) is None:
+            self._deferred_status = collections.deque()
+        self._deferred_status.append((dh, dev_ev, self._lookahead_forwards))
+
+    @staticmethod
+    def _prefetch_relation(hdr, hb):
+        """The first row's relation recorded by prefetch (host read of the
+        pinned slot; its event has been waited on)."""
+        return int(hdr[hb:hb + 8].view(torch.int64)[0])
+
+    def _reference_nonfinite(self, device, all_r, ridx, rule_vals, row, ce, node, C):
+        """Where the reference's dense sums over a relation's rules meet 0 x
+        (a non-finite value): it multiplies every rule's path counts, zeros
+        included, by the rule's value (Predictor: score += x * w,
+        predictors.py:63-64; FuncToNodeSum: (message * weight).sum(1),
+        layers.py:70), so a candidate gets NaN in dim d when a rule it is NOT
+        reached by has a non-finite value there.  rule_vals: (len(ridx), D).
+        Returns (per candidate (C, D), per row (nq, D)) bool: the candidate's
+        entry / a non-candidate entity of the row is NaN in the reference."""
+        nr = self.native_rules(device)
+        bad = (~torch.isfinite(rule_vals.detach())).to(torch.int64)
+        D = bad.size(1)
+        heads = torch.tensor([h for h, _ in self.rules], dtype=torch.int64, device=device)
+        rel_bad = torch.zeros((self.graph.relation_size, D), dtype=torch.int64, device=device).index_add(
+            0, heads[ridx], bad)
+        node_bad = torch.zeros((max(nr.n_nodes, 1), D), dtype=torch.int64, device=device).index_add(
+            0, nr.node_of_rule[ridx], bad)
+        key = torch.unique(ce * max(nr.n_nodes, 1) + node)  # distinct (candidate, node) pairs
+        reached = torch.zeros((C, D), dtype=torch.int64, device=device).index_add(
+            0, key // max(nr.n_nodes, 1), node_bad[key % max(nr.n_nodes, 1)])
+        r64 = all_r.to(device, torch.int64)
+        return rel_bad[r64[row]] > reached, rel_bad[r64] > 0
 
     def _needs_grad(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
@@ -361,115 +587,33 @@ class Predictor(_HipGrounding, torch.nn.Module):
     def forward_rows(self, all_h, all_r, edges_to_remove=None, return_ncand=False):
         """Forward for any rows (one or many reference batches, mixed
         relations): (score (n, |E|) f32, mask (n, |E|) bool[, n_cand])."""
-        score, mask, n_cand, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
+        try:
+            score, mask, n_cand, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove)
+        except _native.NativeError as e:
+            if e.code != _native.RNNL_ERR_RANGE:
+                raise
+            score, mask, n_cand = self._forward_range_fallback(all_h, all_r, edges_to_remove)
         return (score, mask, n_cand) if return_ncand else (score, mask)
 
-    @_native.on_input_device
-    def prefetch(self, all_h, all_r, edges_to_remove=None):
-        """Ground these rows now, on a side stream, for a forward that will be
-        called with the same tensor objects (the training loop's lookahead:
-        the grounding does not depend on the weights, so batch k + 1's runs
-        while batch k scores, steps back and updates).  Up to prefetch_depth
-        groundings are queued, each in its own workspace of a ring; a forward
-        whose rows are not the queue's head drops the queue."""
-        if self.prefetch_depth <= 0:
-            return
-        device, h, r, etr = self._rows(all_h, all_r, edges_to_remove)
-        nq = h.numel()
-        if nq == 0:
-            return
-        key = self._device_index(device)
-        pf = self._pf.get(key)
-        if pf is None:
-            pf = self._pf[key] = {"stream": torch.cuda.Stream(device), "ring": {}, "next": 0,
-                                  "queue": collections.deque()}
-        if len(pf["queue"]) >= self.prefetch_depth:
-            return
-        g, nr = self.graph.device_graph(device), self.native_rules(device)
-        scale = self.capacity_scale
-        need = ctypes.c_size_t()
-        _native.call("rnnl_forward_workspace_size", g, nr.ptr, nq, scale, ctypes.byref(need))
-        # ring of depth + 1 workspaces: the forward in flight keeps one until its backward
-        slot = pf["next"] % (self.prefetch_depth + 1)
-        pf["next"] += 1
-        ws = pf["ring"].get(slot)
-        if ws is None or ws.numel() < need.value:
-            ws = pf["ring"][slot] = torch.empty(need.value, dtype=torch.uint8, device=device)
-        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
-        side, main = pf["stream"], torch.cuda.current_stream(device)
-        # inputs, and the slot's previous user (its backward is on the current stream already)
-        side.wait_stream(main)
+    def _forward_range_fallback(self, all_h, all_r, edges_to_remove):
+        """Past the fixed-point kernels' integer ranges (a path count reaching
+        2^32, non-finite or huge rule weights): the reference's arithmetic on
+        the grounding COO with int64 counts (forward_autograd's torch ops)."""
+        logging.info("Predictor: %s; rows recomputed on the grounding COO (int64 counts, torch ops)",
+                     _native.lib().rnnl_last_error().decode(errors="replace"))
+        with torch.no_grad():
+            score, mask = self.forward_autograd(all_h, all_r, edges_to_remove, nonfinite=True)
+            row = self.ground_coo(all_h, all_r, edges_to_remove)[0]
+            n_cand = torch.bincount(row, minlength=all_h.numel()).to(torch.int32)
+        return score, mask, n_cand
+
+    def _prefetch_enabled(self):
+        return True
+
+    def _prefetch_ground(self, g, nr, h, r, etr, nq, n_cand, ws, scale, stream):
         _native.call("rnnl_predictor_ground", g, nr.ptr, h.data_ptr(), r.data_ptr(),
                      etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(), ws.numel(),
-                     scale, side.cuda_stream)
-        # the grounding's status / totals and the one-relation flag, copied to the
-        # host behind it: the forward reads them without waiting for the current stream
-        # (pinned buffer and event of the ring slot: the slot's previous entry was
-        # consumed, or dropped behind the same side stream, before it comes round)
-        hdr, ev = self._host_slot(pf, "pf", slot, self.prefetch_depth + 1)
-        with torch.cuda.stream(side):
-            hdr.copy_(ws[:hdr.numel()], non_blocking=True)  # status, totals and the one-relation flag
-        ev.record(side)
-        # the side stream's use of these blocks outlives a dropped queue entry or a
-        # grown ring slot: the caching allocator must not hand them out before it ends
-        for t in (ws, n_cand, h, r) + ((etr,) if etr is not None else ()):
-            t.record_stream(side)
-        self._ws_touch(ws)
-        pf["queue"].append((all_h, all_r, edges_to_remove, ws, scale, n_cand, ev, (h, r, etr), hdr))
-
-    def _host_slot(self, pf, name, k, n):
-        """(pinned header buffer, event) number k % n of a ring kept in pf:
-        reused instead of a pinned allocation and an event creation per step."""
-        ring = pf.get(name)
-        if ring is None or len(ring) != n:
-            hb = self._header_bytes()
-            ring = pf[name] = [(torch.empty(hb, dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
-                               for _ in range(n)]
-        return ring[k % n]
-
-    def _header_bytes(self):
-        if getattr(self, "_hdr_bytes", None) is None:
-            n = ctypes.c_size_t()
-            _native.call("rnnl_forward_header_bytes", ctypes.byref(n))
-            self._hdr_bytes = n.value
-        return self._hdr_bytes
-
-    def check_deferred(self, keep=0):
-        """Raise the scoring pass's own error (an integer range flag) of the
-        lookahead forwards, whose status is read late so the host does not
-        wait for the scoring: every pending status but the newest `keep`
-        (the training step checks the forward before last, which has long
-        finished; train() checks them all at its end).  The training steps of
-        those forwards have then already run their backward and optimizer
-        step on the flagged scores: the error names the forward, and a run
-        resumed from a checkpoint written after it should not trust it."""
-        q = getattr(self, "_deferred_status", None)
-        while q and len(q) > keep:
-            dh, ev, n = q.popleft()
-            ev.synchronize()
-            rc = _native.lib().rnnl_forward_status_host(dh.data_ptr(), None)
-            if rc != _native.RNNL_OK:
-                q.clear()
-                raise _native.NativeError(rc, "%s (scoring pass of lookahead forward #%d, read late: that step's "
-                                              "backward and optimizer update have already been applied)" % (
-                                                  _native.lib().rnnl_last_error().decode(errors="replace"), n))
-
-    def _prefetched(self, device, all_h, all_r, edges_to_remove):
-        """The queued grounding of exactly these row tensors, or None (a
-        mismatch drops the lookahead queue)."""
-        pf = self._pf.get(self._device_index(device))
-        if not pf or not pf["queue"]:
-            return None
-        e = pf["queue"][0]
-        if e[0] is all_h and e[1] is all_r and e[2] is edges_to_remove and e[4] == self.capacity_scale:
-            return pf["queue"].popleft()
-        # other row tensors than the queue's head (e.g. a wrapper copied the
-        # inputs): the lookahead is lost — counted, so a profile can show it
-        self.prefetch_dropped += len(pf["queue"])
-        logging.debug("Predictor: lookahead queue dropped (%d groundings; %d so far)", len(pf["queue"]),
-                      self.prefetch_dropped)
-        pf["queue"].clear()
-        return None
+                     scale, stream)
 
     def _forward_launch(self, all_h, all_r, edges_to_remove, single_relation=False):
         """rnnl_predictor_forward over the rows -> (score, mask, n_cand, ws,
@@ -514,7 +658,6 @@ class Predictor(_HipGrounding, torch.nn.Module):
         if pre is not None:  # grounded ahead (prefetch): the scoring half only
             _, _, _, ws, scale, n_cand_pf, ev, _, hdr = pre
             ev.synchronize()  # that grounding and its header copy, not the later side-stream work
-            hb = self._header_bytes()
             rc = _native.lib().rnnl_forward_status_host(hdr.data_ptr(), totals.ctypes.data_as(ctypes.c_void_p))
             _native.call("rnnl_forward_flags_host", hdr.data_ptr(), self._flags.ctypes.data_as(ctypes.c_void_p))
             if single_relation:
@@ -528,13 +671,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
                              n_cand_pf.data_ptr(), ws.data_ptr(), ws.numel(), scale, stream)
                 # the scoring pass's range flag: copied behind it, read two forwards
                 # later (a ring of 4 pinned buffers / events: at most 2 are pending)
-                self._lookahead_forwards = getattr(self, "_lookahead_forwards", 0) + 1
-                dh, dev_ev = self._host_slot(self._pf[self._device_index(device)], "dev", self._lookahead_forwards, 4)
-                dh.copy_(ws[:hb], non_blocking=True)
-                dev_ev.record(main)
-                if getattr(self, "_deferred_status", None) is None:
-                    self._deferred_status = collections.deque()
-                self._deferred_status.append((dh, dev_ev, self._lookahead_forwards))
+                self._defer_status(device, ws)
                 n_cand = n_cand_pf
             else:  # overflow (or another failure): the one-call path, with its retry
                 pre = None
@@ -556,11 +693,19 @@ class Predictor(_HipGrounding, torch.nn.Module):
         """predictors.py:53-80: one single-relation batch -> (score, mask).
         With autograd (training) the same HIP forward runs inside
         _PredictorLinear, whose backward is rnnl_predictor_backward."""
-        if self._needs_grad():
-            bias = self.bias if self.entity_feature == "bias" else None
-            score, mask = _PredictorLinear.apply(self.rule_weights, bias, self, all_h, all_r, edges_to_remove)
-        else:
-            score, mask, _, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
+        try:
+            if self._needs_grad():
+                bias = self.bias if self.entity_feature == "bias" else None
+                score, mask = _PredictorLinear.apply(self.rule_weights, bias, self, all_h, all_r, edges_to_remove)
+            else:
+                score, mask, _, _, _, _ = self._forward_launch(all_h, all_r, edges_to_remove, single_relation=True)
+        except _native.NativeError as e:
+            if e.code != _native.RNNL_ERR_RANGE:
+                raise
+            # past the kernels' integer ranges: torch ops on the int64 grounding COO
+            logging.info("Predictor: %s; batch recomputed on the grounding COO",
+                         _native.lib().rnnl_last_error().decode(errors="replace"))
+            score, mask = self.forward_autograd(all_h, all_r, edges_to_remove, nonfinite=True)
         if self.entity_feature != "bias":
             # early return `mask - float('-inf')` (predictors.py:68-72): +inf where the
             # batch has no candidate at all (mask all False), without a host read
@@ -568,11 +713,12 @@ class Predictor(_HipGrounding, torch.nn.Module):
         return score, mask
 
     @_native.on_input_device
-    def forward_autograd(self, all_h, all_r, edges_to_remove):
+    def forward_autograd(self, all_h, all_r, edges_to_remove, nonfinite=False):
         """Differentiable forward (training): the HIP grounding's COO, then
         score = scatter of sum(count x node weight) with node weight = the sum
         of its rules' rule_weights — torch autograd yields the reference's
-        gradients (predictors.py:53-80)."""
+        gradients (predictors.py:53-80).  nonfinite: reproduce the reference's
+        0 x (non-finite weight) NaNs (the range fallback)."""
         device = all_h.device
         nq, E = all_h.numel(), self.num_entities
         row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
@@ -586,7 +732,15 @@ class Predictor(_HipGrounding, torch.nn.Module):
         w = self.rule_weights
         node_w = torch.zeros(nr.n_nodes, device=device, dtype=w.dtype).index_add(0, nr.node_of_rule, w)
         val = torch.zeros(C, device=device, dtype=w.dtype).index_add(0, ce, count.to(w.dtype) * node_w.index_select(0, node))
-        score = torch.zeros(nq * E, device=device, dtype=w.dtype).scatter(0, row * E + ent, val).view(nq, E)
+        score = torch.zeros(nq * E, device=device, dtype=w.dtype)
+        if nonfinite:
+            rels = torch.unique(all_r).tolist()
+            ridx = torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
+            cand_nan, row_nan = self._reference_nonfinite(device, all_r, ridx, w.detach()[ridx].unsqueeze(1), row, ce,
+                                                          node, C)
+            val = torch.where(cand_nan[:, 0], torch.full_like(val, float("nan")), val)
+            score = torch.where(row_nan[:, 0].repeat_interleave(E), torch.full_like(score, float("nan")), score)
+        score = score.scatter(0, row * E + ent, val).view(nq, E)
         if self.entity_feature == "bias":
             return score + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
         mask = torch.zeros(nq * E, dtype=torch.bool, device=device).index_fill(0, row * E + ent, True).view(nq, E)
@@ -606,22 +760,46 @@ class Predictor(_HipGrounding, torch.nn.Module):
         if len(rules) == 0:
             return None, None
         nq = all_h.numel()
-        ws, scale, n_cand = self.ground(all_h, all_r, edges_to_remove)
         nr = self.native_rules(device)
         roots, ld = self.head_roots(device)
-        all_r = all_r.to(device, torch.int64).contiguous()
-        all_t = all_t.to(device, torch.int64).contiguous()
-        pos = torch.zeros((nq, ld), dtype=torch.int64, device=device)
-        tot = torch.zeros((nq, ld), dtype=torch.int64, device=device)
-        _native.call("rnnl_predictor_rule_stats", ws.data_ptr(), nq, scale, n_cand.data_ptr(), nr.ptr,
-                     all_r.data_ptr(), all_t.data_ptr(), ld, pos.data_ptr(), tot.data_ptr(),
-                     torch.cuda.current_stream(device).cuda_stream)
+        pos, tot, n_cand = self._rule_stats(all_h, all_r, all_t, edges_to_remove, ld)
         rule_index = torch.tensor([i for i, _ in rules], dtype=torch.long, device=device)
         k = nr.node_of_rule[rule_index] - roots[query_r]
         w = self.rule_weights.detach()[rule_index]
         pos_score = pos[:, k].to(w.dtype) * w
         neg_score = tot[:, k].to(w.dtype) * w / torch.clamp(n_cand.to(w.dtype), min=1).unsqueeze(1)
         return torch.softmax(pos_score - neg_score, dim=-1).sum(0), rule_index
+
+    def _rule_stats(self, all_h, all_r, all_t, edges_to_remove, ld):
+        """Per row and trie node of the row's head (local index < ld): the
+        path count to the true tail (pos) and the total over the candidates
+        (tot), int64, and the rows' candidate counts — rnnl_predictor_rule_stats
+        on the grounding, or, for rows whose counts reach 2^32 (the grounding
+        kernel's u32 sums), the same sums on the int64 grounding COO
+        (rnnl_ground_wide; the reference counts in int64, data.py:139-171)."""
+        device = all_h.device
+        nq = all_h.numel()
+        r64 = all_r.to(device, torch.int64).contiguous()
+        t64 = all_t.to(device, torch.int64).contiguous()
+        nr = self.native_rules(device)
+        pos = torch.zeros((nq, ld), dtype=torch.int64, device=device)
+        tot = torch.zeros((nq, ld), dtype=torch.int64, device=device)
+        try:
+            ws, scale, n_cand = self.ground(all_h, all_r, edges_to_remove)
+        except _native.NativeError as e:
+            if e.code != _native.RNNL_ERR_RANGE:
+                raise
+            row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
+            roots = torch.tensor(self.head_roots(device)[0], dtype=torch.int64, device=device)
+            rr = row[ce]
+            flat = rr * ld + (node - roots[r64[rr]])
+            tot.view(-1).index_add_(0, flat, count)
+            pos.view(-1).index_add_(0, flat, count * (ent[ce] == t64[rr]).to(torch.int64))
+            return pos, tot, torch.bincount(row, minlength=nq).to(torch.int32)
+        _native.call("rnnl_predictor_rule_stats", ws.data_ptr(), nq, scale, n_cand.data_ptr(), nr.ptr,
+                     r64.data_ptr(), t64.data_ptr(), ld, pos.data_ptr(), tot.data_ptr(),
+                     torch.cuda.current_stream(device).cuda_stream)
+        return pos, tot, n_cand
 
     def _rule_table(self, device):
         """Per relation its rules padded to the longest list: (R, Rmax) rule ids
@@ -666,15 +844,8 @@ class Predictor(_HipGrounding, torch.nn.Module):
         for s0 in range(0, n, chunk):
             h, r, t = all_h[s0:s0 + chunk], all_r[s0:s0 + chunk], all_t[s0:s0 + chunk]
             e = edges_to_remove[s0:s0 + chunk] if edges_to_remove is not None else None
-            m = h.numel()
-            ws, scale, n_cand = self.ground(h, r, e)
+            pos, tot, n_cand = self._rule_stats(h, r, t, e, ld)
             r = r.to(device, torch.int64).contiguous()
-            t = t.to(device, torch.int64).contiguous()
-            pos = torch.zeros((m, ld), dtype=torch.int64, device=device)
-            tot = torch.zeros((m, ld), dtype=torch.int64, device=device)
-            _native.call("rnnl_predictor_rule_stats", ws.data_ptr(), m, scale, n_cand.data_ptr(), nr.ptr,
-                         r.data_ptr(), t.data_ptr(), ld, pos.data_ptr(), tot.data_ptr(),
-                         torch.cuda.current_stream(device).cuda_stream)
             ridx, k = idx[r], node[r]  # (m, Rmax)
             valid = ridx >= 0
             w = w_all[ridx.clamp(min=0)]
@@ -685,6 +856,148 @@ class Predictor(_HipGrounding, torch.nn.Module):
             sm = torch.where(valid & has, sm, torch.zeros_like(sm))
             H.index_add_(0, ridx.clamp(min=0).reshape(-1), sm.reshape(-1))
         return H
+
+
+class _PlusSumTrain(torch.autograd.Function):
+    """PredictorPlus.forward under autograd for the SUM aggregator (hidden 16):
+    the fused HIP forward (rnnl_predictorplus_forward with the batch's edge
+    removal) and the fused backward K2^T (rnnl_predictorplus_backward,
+    csrc/backward.hip) instead of torch autograd over the grounding COO —
+    reference src/predictors.py:238-271, src/layers.py:9-77 as differentiated
+    in src/trainer.py:84-93.
+
+    Inputs: the rule-embedding table `emb` (num_rules x 16: rule_emb, or the
+    batch relation's LSTM outputs scattered into a zero table), the rule part's
+    weights, and the entity feature: `base` = the bias vector (kind 'bias'),
+    the RotatE rows (kind 'rows', whose gradient is grad_score itself) or None
+    (kind 'none': -inf outside the candidates, mask from the kernel).  A
+    batch without any candidate takes the reference's early return
+    (predictors.py:230-237): the rule part is not in the graph, so its
+    parameters get no gradient (None, which Adam skips)."""
+
+    @staticmethod
+    def forward(ctx, model, raw, all_h, all_r, etr, head, kind, base, emb, add_w, add_b, ln_w, ln_b, s0_w, s0_b,
+                s1_w, s1_b, rel_w):
+        device = all_h.device
+        nq, E = all_h.numel(), model.num_entities
+        g, nr = model.graph.device_graph(device), model.native_rules(device)
+        emb_d = emb.detach().float().contiguous()
+        ws_ = [t.detach().float().contiguous() for t in (add_w, add_b, ln_w, ln_b, s0_w, s0_b, s1_w, s1_b, rel_w)]
+        nbytes = ctypes.c_size_t()
+        _native.call("rnnl_node_weights_size", nr.ptr, _native.AGG_SUM, ctypes.byref(nbytes))
+        node_w = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if head >= 0:  # a one-relation batch reads that head's trie only
+            _native.call("rnnl_node_weights_head", nr.ptr, head, emb_d.data_ptr(), 16, _native.AGG_SUM,
+                         ws_[0].data_ptr(), node_w.data_ptr(), stream)
+        else:
+            _native.call("rnnl_node_weights", nr.ptr, emb_d.data_ptr(), 16, _native.AGG_SUM, ws_[0].data_ptr(),
+                         node_w.data_ptr(), stream)
+        p = _native.PredictorParams()
+        p.aggregator = _native.AGG_SUM
+        p.feature = _native.FEATURE_NONE if kind == "none" else _native.FEATURE_ADD
+        p.node_w = node_w.data_ptr()
+        (p.add_w, p.add_b, p.ln_w, p.ln_b, p.s0_w, p.s0_b, p.s1_w, p.s1_b, p.rel_emb) = [t.data_ptr() for t in ws_]
+        bias = base.detach().float().contiguous() if kind == "bias" else None
+        if bias is not None:
+            p.base_row = bias.data_ptr()
+        mask8 = None
+        totals = np.zeros(2, dtype=np.int64)
+
+        def run(ws, scale):
+            if kind == "bias":
+                _native.call("rnnl_fill_rows", bias.data_ptr(), nq, E, score.data_ptr(), stream)
+            elif kind == "rows":
+                score.copy_(base.detach())
+            else:
+                _native.call("rnnl_fill_value", float("-inf"), score.numel(), score.data_ptr(), stream)
+                mask8.zero_()
+            _native.call("rnnl_predictorplus_forward", g, nr.ptr, ctypes.byref(p), all_h.data_ptr(),
+                         all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
+                         mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(), None, ws.data_ptr(),
+                         ws.numel(), scale, stream)
+        score = torch.empty((nq, E), dtype=torch.float32, device=device)
+        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        if kind == "none":
+            mask8 = torch.empty((nq, E), dtype=torch.uint8, device=device)
+        model.check_deferred(keep=1)
+        pre = model._prefetched(device, *raw) if raw is not None else None
+        if pre is not None:  # grounded ahead (prefetch): the scoring half only
+            _, _, _, ws, scale, n_cand_pf, ev, _, hdr = pre
+            ev.synchronize()  # that grounding and its header copy, not the later side-stream work
+            rc = _native.lib().rnnl_forward_status_host(hdr.data_ptr(), totals.ctypes.data_as(ctypes.c_void_p))
+            if rc == _native.RNNL_OK:
+                if kind == "bias":
+                    _native.call("rnnl_fill_rows", bias.data_ptr(), nq, E, score.data_ptr(), stream)
+                elif kind == "rows":
+                    score.copy_(base.detach())
+                else:
+                    _native.call("rnnl_fill_value", float("-inf"), score.numel(), score.data_ptr(), stream)
+                    mask8.zero_()
+                torch.cuda.current_stream(device).wait_event(ev)
+                _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(p), all_h.data_ptr(),
+                             all_r.data_ptr(), nq, score.data_ptr(), mask8.data_ptr() if mask8 is not None else None,
+                             n_cand_pf.data_ptr(), None, ws.data_ptr(), ws.numel(), scale, 0, 0, stream)
+                model._defer_status(device, ws)  # the scoring pass's range flags, read two forwards later
+                n_cand = n_cand_pf
+            else:  # overflow (or another failure): the one-call path, with its retry
+                pre = None
+        if pre is None:
+            ws, scale = model._launch(device, nq, run, totals)
+        ctx.no_cand = int(totals[0]) == 0
+        ctx.n_total = int(totals[0])
+        if ctx.no_cand and kind == "none":
+            # the reference's early return `mask - float('-inf')` (predictors.py:236-237): +inf, mask False
+            score.fill_(float("inf"))
+        mask = mask8.bool() if mask8 is not None else torch.ones((nq, E), dtype=torch.bool, device=device)
+        ctx.model, ctx.kind, ctx.head = model, kind, head
+        ctx.launch = (ws, scale, n_cand, model._ws_uses.get(ws.data_ptr()), node_w, p, emb_d, ws_, bias)
+        ctx.rows = (all_h, all_r, etr)
+        ctx.mark_non_differentiable(mask)
+        return score, mask
+
+    @staticmethod
+    def backward(ctx, grad_score, grad_mask):
+        model, kind = ctx.model, ctx.kind
+        ws, scale, n_cand, gen, node_w, p, emb_d, ws_, bias = ctx.launch
+        all_h, all_r, etr = ctx.rows
+        device = all_h.device
+        nq, E = all_h.numel(), model.num_entities
+        g_base = None
+        if kind == "bias" and ctx.needs_input_grad[7]:
+            g_base = grad_score.sum(0)
+        elif kind == "rows" and ctx.needs_input_grad[7]:
+            g_base = grad_score
+        if ctx.no_cand or nq == 0:
+            return (None,) * 7 + (g_base,) + (None,) * 10
+        g, nr = model.graph.device_graph(device), model.native_rules(device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if model._ws_uses.get(ws.data_ptr()) != gen:
+            # another launch reused the workspace since the forward: the same
+            # rows grounded and scored again rebuild the COO and chunk list
+            scratch = torch.empty((nq, E), dtype=torch.float32, device=device)
+            _native.call("rnnl_fill_value", 0.0, scratch.numel(), scratch.data_ptr(), stream)
+            p2 = _native.PredictorParams.from_buffer_copy(p)
+            p2.feature, p2.base_row = _native.FEATURE_ADD, None
+
+            def run(ws2, scale2):
+                _native.call("rnnl_predictorplus_forward", g, nr.ptr, ctypes.byref(p2), all_h.data_ptr(),
+                             all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, scratch.data_ptr(),
+                             None, n_cand.data_ptr(), None, ws2.data_ptr(), ws2.numel(), scale2, stream)
+            ws, scale = model._launch(device, nq, run)
+        gs = grad_score.float().contiguous()
+        sb = model._backward_scratch(device)
+        outs = [torch.empty_like(emb_d)] + [torch.empty_like(t) for t in ws_]
+        gr = _native.SumGrads()
+        gr.emb, gr.emb_ld = outs[0].data_ptr(), 16
+        (gr.add_w, gr.add_b, gr.ln_w, gr.ln_b, gr.s0_w, gr.s0_b, gr.s1_w, gr.s1_b, gr.rel_emb) = \
+            [t.data_ptr() for t in outs[1:]]
+        _native.call("rnnl_predictorplus_backward", g, nr.ptr, ctypes.byref(p), emb_d.data_ptr(), 16,
+                     all_r.data_ptr(), nq, gs.data_ptr(), n_cand.data_ptr(), ctx.n_total, ws.data_ptr(), ws.numel(),
+                     scale,
+                     ctx.head, sb.data_ptr(), sb.numel(), ctypes.byref(gr), stream)
+        grads = [o if ctx.needs_input_grad[8 + k] else None for k, o in enumerate(outs)]
+        return (None,) * 7 + (g_base,) + tuple(grads)
 
 
 class PredictorPlus(_HipGrounding, torch.nn.Module):
@@ -761,6 +1074,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # (96 VGPRs) fits beside RotatE; there the boundary only costs its drain.
         self.rotate_yield = True
         self.rotate_share = 0.8  # the first launch's share of RotatE's grid
+        # training forwards of the SUM aggregator: the fused HIP forward and
+        # backward (_PlusSumTrain); False: torch autograd over the grounding COO
+        self.fused_backward = True
+        # training lookahead (TrainerPredictor.train calls prefetch on the next
+        # batches): their grounding runs on a side stream during this step, and
+        # the step reads its status and relation without waiting on the GPU
+        self._pf = {}
+        self.prefetch_depth = 2
+        self.prefetch_dropped = 0
 
     # ------------------------------------------------------------------ rules
     def set_rules(self, input):
@@ -948,6 +1270,22 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             with torch.no_grad():
                 score, mask, n_cand = self.forward_coo(all_h, all_r, etr)
             return (score, mask, n_cand) if return_ncand else (score, mask)
+        try:
+            return self._forward_rows_fused(device, all_h, all_r, etr, nq, return_ncand, digest, events)
+        except _native.NativeError as e:
+            if e.code != _native.RNNL_ERR_RANGE or digest is not None:
+                raise
+        # out of the fused kernels' exact integer ranges (a path count past 2^32,
+        # non-finite or huge rule aggregates, feature sums past int64): the
+        # reference's fp32 arithmetic on the grounding COO with int64 counts,
+        # which propagates infinities and NaNs as the reference does
+        logging.info("PredictorPlus: %s; rows recomputed on the grounding COO (int64 counts, fp32 torch ops)",
+                     _native.lib().rnnl_last_error().decode(errors="replace"))
+        with torch.no_grad():
+            score, mask, n_cand = self.forward_coo(all_h, all_r, etr, nonfinite=True)
+        return (score, mask, n_cand) if return_ncand else (score, mask)
+
+    def _forward_rows_fused(self, device, all_h, all_r, etr, nq, return_ncand, digest, events):
         g = self.graph.device_graph(device)
         nr = self.native_rules(device)
         rec = (lambda k: events.setdefault(k, torch.cuda.Event(enable_timing=True)).record()) \
@@ -1062,6 +1400,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         all_h = all_h.to(torch.int64)
         all_r = all_r.to(torch.int64)
         nq, E = all_h.numel(), self.num_entities
+        if self.fused and self.aggregator == "sum" and self.fused_backward and device.type == "cuda":
+            try:
+                return self._forward_sum_train(all_h, all_r, edges_to_remove, query_r)
+            except _native.NativeError as e:
+                if e.code != _native.RNNL_ERR_RANGE:
+                    raise
+                # past the fused kernels' integer ranges: the autograd COO path below
         row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
         if ent.numel() == 0:
             # predictors.py:230-237 early return
@@ -1074,11 +1419,63 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         return self._score_coo(all_h, all_r, row, ent, ce, node, count, rels=query_r)
 
     @_native.on_input_device
-    def forward_coo(self, all_h, all_r, edges_to_remove=None):
+    def _forward_sum_train(self, all_h, all_r, edges_to_remove, query_r):
+        """forward_autograd for the SUM aggregator through _PlusSumTrain."""
+        raw = (all_h, all_r, edges_to_remove)
+        device = all_h.device
+        etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
+        all_h, all_r = all_h.contiguous(), all_r.contiguous()
+        head = int(query_r) if isinstance(query_r, int) else -1
+        if self.type == "emb":
+            emb = self.rule_emb
+        else:
+            rels = [head] if head >= 0 else torch.unique(all_r).tolist()
+            ridx = self._rule_ids(rels, device)
+            x_f = self._encode_rules_padded(ridx, device)
+            emb = torch.zeros((self.num_rules, self.hidden_dim), dtype=x_f.dtype, device=device).index_copy(
+                0, ridx, x_f)
+        if self.entity_feature == "bias":
+            kind, base = "bias", self.bias
+        elif self.entity_feature == "RotatE":
+            kind, base = "rows", self.RotatE(all_h, all_r)
+        else:
+            kind, base = "none", None
+        rte, sm = self.rule_to_entity, self.score_model
+        # (autograd runs Function.forward with grad mode off: decide here)
+        raw = raw if self._prefetch_enabled() else None
+        return _PlusSumTrain.apply(self, raw, all_h, all_r, etr, head, kind, base, emb, rte.add_model.layers[0].weight,
+                                   rte.add_model.layers[0].bias, rte.layer_norm.weight, rte.layer_norm.bias,
+                                   sm.layers[0].weight, sm.layers[0].bias, sm.layers[1].weight, sm.layers[1].bias,
+                                   self.relation_emb.weight)
+
+    def _prefetch_enabled(self):
+        """The lookahead serves the fused SUM training forward only."""
+        return (self.fused and self.aggregator == "sum" and self.fused_backward and self.training and
+                torch.is_grad_enabled())
+
+    def _prefetch_ground(self, g, nr, h, r, etr, nq, n_cand, ws, scale, stream):
+        _native.call("rnnl_predictorplus_ground", g, nr.ptr, _native.AGG_SUM, h.data_ptr(), r.data_ptr(),
+                     etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(), ws.numel(),
+                     scale, 0, stream)
+
+    def _backward_scratch(self, device):
+        key = ("bwd", self._device_index(device))
+        sb = self._side.get(key)
+        if sb is None:
+            n = ctypes.c_size_t()
+            _native.call("rnnl_predictorplus_backward_size", self.native_rules(device).ptr, self.num_relations,
+                         ctypes.byref(n))
+            sb = self._side[key] = torch.empty(n.value, dtype=torch.uint8, device=device)
+        return sb
+
+    @_native.on_input_device
+    def forward_coo(self, all_h, all_r, edges_to_remove=None, nonfinite=False):
         """Rows of any relations through the HIP grounding COO and the torch
         aggregation / MLP (any hidden_dim): (score, mask, n_cand), the
         forward_rows contract — rows without candidates keep their base score
-        (bias / RotatE) or -inf with the mask False (entity_feature none)."""
+        (bias / RotatE) or -inf with the mask False (entity_feature none).
+        nonfinite: the reference's 0 x (non-finite embedding) NaNs (range
+        fallback, _reference_nonfinite)."""
         device = all_h.device
         all_h = all_h.to(torch.int64)
         all_r = all_r.to(torch.int64)
@@ -1094,10 +1491,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 return self.RotatE(all_h, all_r), torch.ones((nq, E), dtype=torch.bool, device=device), n_cand
             return torch.full((nq, E), float("-inf"), device=device), \
                 torch.zeros((nq, E), dtype=torch.bool, device=device), n_cand
-        score, mask = self._score_coo(all_h, all_r, row, ent, ce, node, count)
+        score, mask = self._score_coo(all_h, all_r, row, ent, ce, node, count, nonfinite=nonfinite)
         return score, mask, n_cand
 
-    def _score_coo(self, all_h, all_r, row, ent, ce, node, count, rels=None):
+    def _score_coo(self, all_h, all_r, row, ent, ce, node, count, rels=None, nonfinite=False):
         """predictors.py:238-271 on the grounding COO (torch ops).  `rels`: the
         rows' relations when the caller knows them (forward's single-relation
         batch), which saves the host sync of torch.unique."""
@@ -1119,6 +1516,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         cnt = count.to(x_f.dtype).unsqueeze(-1)
         node_sum = torch.zeros((nr.n_nodes, H), device=device, dtype=x_f.dtype).index_add(0, nodes, x_f)
         wsum = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sum.index_select(0, node))
+        cand_nan = None
+        if nonfinite:
+            cand_nan = self._reference_nonfinite(device, all_r, ridx, x_f, row, ce, node, C)[0]
+            wsum = torch.where(cand_nan, torch.full_like(wsum, float("nan")), wsum)
         if self.aggregator == "sum":
             out = self.rule_to_entity.finish(wsum)
         else:
@@ -1131,6 +1532,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             node_max = torch.full((nr.n_nodes, H), float("-inf"), device=device, dtype=x_f.dtype).scatter_reduce(
                 0, idx_n, x_f, "amax", include_self=True)
             wsq = torch.zeros((C, H), device=device, dtype=x_f.dtype).index_add(0, ce, cnt * node_sq.index_select(0, node))
+            if cand_nan is not None:
+                wsq = torch.where(cand_nan, torch.full_like(wsq, float("nan")), wsq)
             deg = torch.zeros(C, device=device, dtype=x_f.dtype).index_add(0, ce, cnt.squeeze(-1) * node_n.index_select(0, node)) + 1
             idx_c = ce.unsqueeze(-1).expand(-1, H)
             mn = torch.full((C, H), float("inf"), device=device, dtype=x_f.dtype).scatter_reduce(
@@ -1190,10 +1593,20 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         With autograd active (training) the differentiable path runs
         (forward_autograd); otherwise the fused HIP kernels (forward_rows)."""
         if self._needs_grad():
-            # the reference's single-relation check (predictors.py:211-212) in one host
-            # read, which also gives the relation whose rules the autograd path gathers
-            query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
-            assert n_other == 0
+            pre = self._prefetched(all_h.device, all_h, all_r, edges_to_remove, peek=True) \
+                if self._prefetch_enabled() and all_h.is_cuda else None
+            if pre is not None:
+                # grounded ahead: the one-relation flag and the relation from its
+                # header copy (its event ended long ago: no wait on this step)
+                pre[6].synchronize()
+                _native.call("rnnl_forward_flags_host", pre[8].data_ptr(), self._flags.ctypes.data_as(ctypes.c_void_p))
+                self._check_one_relation()
+                query_r = self._prefetch_relation(pre[8], self._header_bytes())
+            else:
+                # the reference's single-relation check (predictors.py:211-212) in one host
+                # read, which also gives the relation whose rules the autograd path gathers
+                query_r, n_other = torch.stack([all_r[0], (all_r != all_r[0]).sum()]).tolist()
+                assert n_other == 0
             return self.forward_autograd(all_h, all_r, edges_to_remove, query_r=query_r)
         # eval: the grounding kernel flags rows of another relation in the
         # launch header, read back with the status (no extra reduction or sync)

@@ -202,6 +202,9 @@ class TrainerPredictor(object):
         does not depend on the weights: same COO, same results)."""
         inner = getattr(model, "module", model)
         depth = getattr(inner, "prefetch_depth", 0) if self.device.type == "cuda" else 0
+        for pf in getattr(inner, "_pf", {}).values():  # a previous loop's leftovers can never match
+            if pf.get("queue"):
+                inner._drop_lookahead(pf, [], len(pf["queue"]))
         if depth <= 0 or not hasattr(inner, "prefetch"):
             for b in batches:
                 yield self._prepare(b)

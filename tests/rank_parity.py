@@ -57,7 +57,11 @@ def check(want, L, H, hip_t, hip_p, hit, ref_t, ref_p, pe, near_w, windows, batc
     valid_p = pe >= 0
     # the target is a candidate in both or in neither (exact mask parity)
     assert np.array_equal(hit, ~np.isnan(ref_t))
-    err = np.where(valid_p, np.abs(hip_p - ref_p), 0.0).max(1)
+    # equal scores (including the -inf of non-candidates without an entity
+    # feature on both sides) are no error; an inf on one side only is
+    with np.errstate(invalid="ignore"):
+        d = np.where(hip_p == ref_p, 0.0, np.abs(hip_p - ref_p))
+    err = np.where(valid_p, d, 0.0).max(1)
     err = np.maximum(err, np.where(hit, np.abs(hip_t - np.nan_to_num(ref_t)), 0.0))
     eps = np.zeros(n)
     for b in range(len(batch_ptr) - 1):

@@ -4,8 +4,10 @@ The first three optimizer steps of TrainerPredictor.train on the seeded
 model — batch order (DistributedSampler, world 1), batch contents (edge ids to
 remove), loss per step, and every parameter gradient of step 0 — against the
 reference's own values (tests/golden/train_*.npz, tools/make_golden_train.py).
-The grounding runs in HIP (rnnl_ground + COO export); the aggregation, MLP and
-RotatE run as torch autograd on the exported COO.
+The grounding runs in HIP.  The SUM aggregator's rule part runs the fused
+HIP forward and backward (csrc/backward.hip, `fused_backward`), and, as a
+second parametrisation, torch autograd over the exported grounding COO; PNA
+runs the latter; RotatE its HIP forward / backward.
 """
 import numpy as np
 import pytest
@@ -32,8 +34,9 @@ def dev():
     return torch.device("cuda:0")
 
 
+@pytest.mark.parametrize("fused", [True, False], ids=["fused_backward", "autograd_coo"])
 @pytest.mark.parametrize("case", TRAIN_CASES)
-def test_train_steps_match_reference(case, dev):
+def test_train_steps_match_reference(case, fused, dev):
     import os
     from rnnlogic_amd import datasets
     from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset
@@ -51,6 +54,9 @@ def test_train_steps_match_reference(case, dev):
     model = PredictorPlus(graph, num_layers=3, hidden_dim=16,
                           embedding_path=datasets.rotate_path(data, dim) if dim else None, **kw)
     model.set_rules(datasets.rule_file(data))
+    if not fused and kw.get("aggregator", "sum") != "sum":
+        pytest.skip("the PNA aggregator trains through the autograd COO path only")
+    model.fused_backward = fused
     sd = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd/")}
     missing, unexpected = model.load_state_dict(sd, strict=False)
     assert not unexpected and all(k.startswith("RotatE.") for k in missing)
@@ -187,3 +193,136 @@ def test_device_train_batches_match_dataset(data, dev):
             for w, g in zip(want, got):
                 np.testing.assert_array_equal(g.cpu().numpy(), w.numpy())
         ts.make_batches()
+
+
+@pytest.mark.parametrize("data", ["FB15k-237", "umls"])
+@pytest.mark.parametrize("type_,feature", [("emb", "bias"), ("lstm", "RotatE"), ("lstm", "none"), ("emb", "none")])
+def test_fused_sum_backward_matches_autograd(data, type_, feature, dev):
+    """The fused SUM backward (rnnl_predictorplus_backward) against torch
+    autograd over the grounding COO (predictors.py:238-271 restated as torch
+    ops) on the same seeded model and training batches (edge removal): the
+    loss and every parameter gradient, four batches of distinct relations."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph, TrainDataset
+    from rnnlogic_amd.predictors import PredictorPlus
+    torch.manual_seed(5)
+    graph = KnowledgeGraph(datasets.materialize(data))
+    ts = TrainDataset(graph, 32)
+    model = PredictorPlus(graph, type=type_, num_layers=3, hidden_dim=16, entity_feature=feature, aggregator="sum",
+                          embedding_path=datasets.rotate_path(data) if feature == "RotatE" else None)
+    model.set_rules(datasets.rule_file(data))
+    with torch.no_grad():
+        for n, prm in model.named_parameters():
+            if not n.startswith("RotatE."):
+                prm.add_(torch.randn_like(prm) * 0.3)
+    model = model.to(dev).train()
+    seen, picks = set(), []
+    for i in range(len(ts)):
+        r = int(ts[i][1][0])
+        if r not in seen:
+            seen.add(r)
+            picks.append(i)
+        if len(picks) == 4:
+            break
+    for idx in picks:
+        all_h, all_r, all_t, target, etr = [x.to(dev) for x in ts[idx]]
+        res = []
+        for fused in (True, False):
+            model.fused_backward = fused
+            model.zero_grad(set_to_none=True)
+            logits, mask = model(all_h, all_r, etr)
+            tt = target * 0.2 + torch.nn.functional.one_hot(all_t, graph.entity_size) * 0.8
+            lp = (torch.softmax(logits, dim=1) + 1e-8).log()
+            if not bool(mask.any()):
+                res.append((None, None))
+                continue
+            loss = -(lp[mask] * tt[mask]).sum() / torch.clamp(tt[mask].sum(), min=1)
+            loss.backward()
+            res.append((loss.item(), {n: (p.grad.detach().clone() if p.grad is not None else None)
+                                      for n, p in model.named_parameters()}))
+        (l1, g1), (l2, g2) = res
+        if l1 is None or l2 is None:
+            assert l1 is None and l2 is None
+            continue
+        assert abs(l1 - l2) <= 1e-5 * abs(l2), (idx, l1, l2)
+        for n in g2:
+            a, b = g1[n], g2[n]
+            if b is None:
+                assert a is None or float(a.abs().max()) == 0.0, n
+                continue
+            # floor: a sum over candidates of dL/dscore cancels to ~0 (the
+            # softmax gradient of a row sums to ~0; sum |dL/dscore| <= 2), so
+            # fp32 summation-order noise is ~1e-7 absolute there
+            atol = max(2e-4 * float(b.abs().max()), 1e-6)
+            np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-3, atol=atol,
+                                       err_msg="%s %s/%s batch %d grad %s" % (data, type_, feature, idx, n))
+
+
+@pytest.mark.parametrize("overflow", [False, True])
+def test_plus_train_lookahead_matches(overflow, dev):
+    """TrainerPredictor.train with the PredictorPlus lookahead (prefetch: the
+    next batches grounded on a side stream by rnnl_predictorplus_ground, the
+    step scores them with rnnl_predictorplus_score and reads no status on its
+    critical path) against prefetch_depth 0 (the one-call forward and its
+    status read): the logged losses and the trained weights — also when
+    lowered workspace capacities make the prefetched groundings overflow and
+    fall back to the retried path.  Weights to a tight tolerance: the node
+    gradients are fp64 atomic sums (order-dependent in the last fp64 bits)."""
+    import io
+    import logging
+    import random
+
+    from rnnlogic_amd import _native, datasets
+    from rnnlogic_amd.data import KnowledgeGraph, TestDataset, TrainDataset, ValidDataset
+    from rnnlogic_amd.predictors import PredictorPlus
+    from rnnlogic_amd.trainer import TrainerPredictor
+    from rnnlogic_amd.utils import set_seed
+    set_seed(1)
+    graph = KnowledgeGraph(datasets.materialize("FB15k-237"))
+    train_set, valid_set, test_set = TrainDataset(graph, 32), ValidDataset(graph, 32), TestDataset(graph, 32)
+    model = PredictorPlus(graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="bias", aggregator="sum")
+    model.set_rules(datasets.rule_file("FB15k-237"))
+    init = {k: v.clone() for k, v in model.state_dict().items()}
+    rng = (random.getstate(), np.random.get_state(), torch.get_rng_state())
+    r2i = [list(x) for x in train_set.r2instances]
+    runs = []
+    for depth in (0, 2):
+        model.load_state_dict(init)
+        train_set.r2instances = [list(x) for x in r2i]
+        random.setstate(rng[0])
+        np.random.set_state(rng[1])
+        torch.set_rng_state(rng[2])
+        model.prefetch_depth = depth
+        model.capacity_scale = 1
+        optim = torch.optim.Adam(model.parameters(), lr=5e-3, weight_decay=0)
+        solver = TrainerPredictor(model, train_set, valid_set, test_set, optim, gpus=[dev])
+        stream = io.StringIO()
+        h = logging.StreamHandler(stream)
+        root = logging.getLogger()
+        old = root.level
+        root.addHandler(h)
+        root.setLevel(logging.INFO)
+        if overflow:
+            _native.call("rnnl_debug_capacity", 8192, 8192, 1024)  # 1/8 of the defaults
+        try:
+            solver.train(batch_per_epoch=40, smoothing=0.2, print_every=10)
+            torch.cuda.synchronize()
+        finally:
+            _native.call("rnnl_debug_capacity", 0, 0, 0)
+            root.removeHandler(h)
+            root.setLevel(old)
+        losses = [line for line in stream.getvalue().splitlines() if line[:1].isdigit()]
+        runs.append(({k: v.detach().cpu().clone() for k, v in solver.model.state_dict().items()}, losses,
+                     model.capacity_scale, model.prefetch_dropped, getattr(model, "prefetch_hits", 0)))
+        model.prefetch_dropped, model.prefetch_hits = 0, 0
+        model = solver.model
+    (w0, l0, s0, _, _), (w1, l1, s1, dropped, hits) = runs
+    assert len(l0) == 4 and l0 == l1, (l0, l1)
+    # groundings are dropped only when a workspace retry raises capacity_scale
+    # (the queued ones were grounded at the old scale): at most depth per doubling
+    assert dropped <= 2 * int(np.log2(s1)), (dropped, s1)
+    assert hits >= 40 - 1 - dropped, (hits, dropped)
+    if overflow:
+        assert s0 > 1 and s1 > 1, (s0, s1)
+    for k in w0:
+        torch.testing.assert_close(w0[k], w1[k], rtol=1e-5, atol=1e-7, msg=k)
