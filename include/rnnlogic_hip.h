@@ -122,6 +122,34 @@ int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, c
                      int32_t layers, int32_t hidden, const int32_t *tokens, int32_t n_rules, int32_t seq_len,
                      int32_t pad, float *out, int32_t ld_out, void *stream);
 
+/* The rule encoder under autograd (training; predictors.py:201-208 and
+ * torch.nn.LSTM's backward): the rules ridx[0..n) (int64 rows of `tokens`).
+ * Per-layer weights come as arrays of `layers` pointers (w_ih[l]: 64 x 16,
+ * w_hh[l]: 64 x 16, b_ih[l] / b_hh[l]: 64), so torch's parameters are used in
+ * place.  rnnl_lstm_train_sizes gives the float counts of
+ *   act [layers][seq_len][6][n x 16]: i, f, g, o, c_t, h_t of every step,
+ *   da  [layers][n seq_len][64]: dL/d(gate pre-activations), 0 at pad steps,
+ *   xh  [layers][n seq_len][32]: the step input x_t | h_(t-1), 0 at pad steps,
+ *   dvx [n seq_len][16]: dL/d(layer-0 input).
+ * forward: out (n x 16) = the top layer's output at each rule's last token,
+ * act saved.  backward: for d_out = dL/d out, fills da, xh, dvx (the caller
+ * forms dW_l = da_l^T xh_l and db_l = column sums of da_l) and d_vocab
+ * (vocab_rows x 16, written whole) = the per-token sums of dvx rows listed
+ * by tok_id[u] / tok_pos[tok_ptr[u] .. tok_ptr[u + 1]) (positions row
+ * seq_len + t, summed in list order; rows of no listed token are zero). */
+int rnnl_lstm_train_sizes(int32_t layers, int32_t hidden, int32_t seq_len, int32_t n, size_t *act_floats,
+                          size_t *da_floats, size_t *xh_floats, size_t *dvx_floats);
+int rnnl_lstm_train_forward(const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                            const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                            const int32_t *tokens, int32_t seq_len, int32_t pad, const int64_t *ridx, int32_t n,
+                            float *out, float *act, void *stream);
+int rnnl_lstm_train_backward(const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                             const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                             const int32_t *tokens, int32_t seq_len, int32_t pad, const int64_t *ridx, int32_t n,
+                             const float *act, const float *d_out, float *da, float *xh, float *dvx,
+                             const int32_t *tok_id, const int32_t *tok_ptr, const int32_t *tok_pos, int32_t n_tok,
+                             float *d_vocab, int32_t vocab_rows, void *stream);
+
 /* ------------------------------------------------------------- forward --
  * Replaces the body of PredictorPlus.forward (reference
  * src/predictors.py:210-271) for n_queries rows — one reference batch, or
@@ -413,6 +441,24 @@ int rnnl_forward_rotate_zero(float *score, size_t n_floats, void *stream);
  * dL/d(h o r).  torch.norm's convention: zero gradient where |hr - t| = 0. */
 int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const float *grad, int32_t n_queries,
                          int32_t n_entities, int32_t dim, float *d_hr, float *d_tail, void *stream);
+
+/* The RotatE parameter gradients in one call (training; embedding.py:45-70
+ * and the h o r product of :55-61 under autograd): for grad = dL/dscore
+ * (n_queries x E) of score = gamma - dist(eemb[h] o rot(remb[r]), eemb[e]),
+ *   d_eemb (E x 2 dim, eemb's layout; NULL: frozen table) = the tail term of
+ *     rnnl_rotate_backward plus the head rows' chain rule,
+ *   d_remb (n_rel_total x dim; NULL: frozen) = the phase chain rule,
+ * both written whole (no accumulation into the caller's buffers).  planes /
+ * ld: the direct-mode entity planes of eemb (rnnl_rotate_entity_table) or any
+ * dim x 2 x ld copy; rtab: rnnl_rotate_relation_table of remb and gamma.
+ * scratch: rnnl_rotate_param_grads_scratch bytes (with_eemb = d_eemb given).
+ * Head rows and relations that repeat in the batch are summed in row order. */
+int rnnl_rotate_param_grads_scratch(int32_t n_queries, int32_t n_entities, int32_t dim, int32_t with_eemb,
+                                    size_t *bytes);
+int rnnl_rotate_param_grads(const float *eemb, const float *planes, int32_t ld, const float *rtab, float gamma,
+                            const int64_t *all_h, const int64_t *all_r, int32_t n_queries, int32_t n_entities,
+                            int32_t dim, int32_t n_rel_total, const float *grad, void *scratch, size_t scratch_bytes,
+                            float *d_eemb, float *d_remb, void *stream);
 
 /* ------------------------------------------------------ training batches --
  * Device-side TrainDataset rows (reference src/data.py:201-219, the target

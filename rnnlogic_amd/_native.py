@@ -40,6 +40,10 @@ SIGNATURES = [
     ("rnnl_node_weights", ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P]),
     ("rnnl_node_weights_size", ctypes.c_int, [_P, _I32, _P]),
     ("rnnl_node_weights_head", ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P]),
+    ("rnnl_lstm_train_sizes", ctypes.c_int, [_I32, _I32, _I32, _I32] + [ctypes.POINTER(ctypes.c_size_t)] * 4),
+    ("rnnl_lstm_train_forward", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P]),
+    ("rnnl_lstm_train_backward", ctypes.c_int,
+     [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _I32, _P]),
     ("rnnl_lstm_encode", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _I32, _P]),
     ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     ("rnnl_predictorplus_forward", ctypes.c_int,
@@ -93,6 +97,9 @@ SIGNATURES = [
     ("rnnl_rotate_score_pieces", ctypes.c_int,
      [_P, _P, _P, _I32, _F32, _P, _P, _I32, _I32, _P, _I32, _I32, _P, ctypes.c_size_t, _I32, _F32, _P]),
     ("rnnl_rotate_backward", ctypes.c_int, [_P, _I32, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    ("rnnl_rotate_param_grads_scratch", ctypes.c_int, [_I32, _I32, _I32, _I32, ctypes.POINTER(ctypes.c_size_t)]),
+    ("rnnl_rotate_param_grads", ctypes.c_int, [_P, _P, _I32, _P, ctypes.c_float, _P, _P, _I32, _I32, _I32, _I32, _P,
+                                               _P, ctypes.c_size_t, _P, _P, _P]),
     ("rnnl_pack_weights_floats", ctypes.c_int, [_P]),
     ("rnnl_pack_weights", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_nll_aux_bytes", ctypes.c_int, [_I32, _P]),

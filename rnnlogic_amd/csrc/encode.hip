@@ -120,6 +120,197 @@ __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// Training (autograd through the rule encoder): the same recurrence over the
+// rules ridx[0..n) of one batch, saving each step's activations, and the
+// backward through time.  Activation / gradient rows are (row, t) = row T + t.
+//
+//   act  [L][T][6][n 16]: i, f, g, o, c_t, h_t (lane-contiguous per field)
+//   da   [L][n T][64]  : dL/d(gate pre-activations) (zero for pad steps)
+//   xh   [L][n T][32]  : the step's input x_t | h_(t-1) (zero for pad steps)
+//   dvx  [n T][16]     : dL/d(layer-0 input) = the vocab rows' gradient
+// The weight gradients are then dW_l = da_l^T xh_l and db_l = sum of da_l's
+// rows (a batched GEMM over the n T rows, host side), the vocab gradient a
+// per-token sum of dvx rows (vocab_grad_kernel).
+
+struct LstmLayerPtrs {
+  const float *w_ih[LMAXL], *w_hh[LMAXL], *b_ih[LMAXL], *b_hh[LMAXL];
+};
+
+__global__ __launch_bounds__(256) void lstm_train_fwd_kernel(const float *__restrict__ vocab, LstmLayerPtrs P,
+                                                             const int32_t *__restrict__ tokens, int T, int pad,
+                                                             const int64_t *__restrict__ ridx, int n, int layers,
+                                                             float *__restrict__ out, float *__restrict__ act) {
+  __shared__ LstmLds S;
+  for (int i = threadIdx.x; i < layers * LG * 2 * LH; i += blockDim.x) {
+    const int l = i / (LG * 2 * LH), g = (i / (2 * LH)) % LG, k = i % (2 * LH);
+    S.w[l][g][k] = k < LH ? P.w_ih[l][g * LH + k] : P.w_hh[l][g * LH + (k - LH)];
+  }
+  for (int i = threadIdx.x; i < layers * LG; i += blockDim.x) S.b[i / LG][i % LG] = P.b_ih[i / LG][i % LG] + P.b_hh[i / LG][i % LG];
+  __syncthreads();
+  const int j = threadIdx.x & (LH - 1);
+  const int64_t N16 = (int64_t)n * LH;
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 < N16; g0 += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)((g0 + threadIdx.x) / LH);
+    const bool valid = row < n;
+    const int32_t *tok = tokens + (valid ? ridx[row] : ridx[0]) * (int64_t)T;
+    int len = 0;
+    while (len < T && tok[len] != pad) ++len;
+    float seq[LMAXT];
+#pragma unroll
+    for (int t = 0; t < LMAXT; ++t) seq[t] = vocab[(int64_t)tok[t < len ? t : 0] * LH + j];
+#pragma unroll 1
+    for (int l = 0; l < layers; ++l) {
+      float w[4][2 * LH], bias[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bias[q] = S.b[l][q * LH + j];
+#pragma unroll
+        for (int k = 0; k < 2 * LH; ++k) w[q][k] = S.w[l][q * LH + j][k];
+      }
+      float h = 0.f, c = 0.f;
+#pragma unroll
+      for (int t = 0; t < LMAXT; ++t) {
+        if (t < len) {
+          float a[4] = {bias[0], bias[1], bias[2], bias[3]};
+          gate_terms<0>(w, seq[t], h, a);
+          const float gi = sigm(a[0]), gf = sigm(a[1]), gg = tanhf(a[2]), go = sigm(a[3]);
+          c = fmaf(gf, c, gi * gg);
+          h = go * tanhf(c);
+          seq[t] = h;
+          if (valid) {
+            float *o = act + ((int64_t)(l * T + t) * 6) * N16 + (int64_t)row * LH + j;
+            o[0] = gi;
+            o[N16] = gf;
+            o[2 * N16] = gg;
+            o[3 * N16] = go;
+            o[4 * N16] = c;
+            o[5 * N16] = h;
+          }
+        }
+      }
+    }
+    if (valid) {
+      float v = 0.f;
+#pragma unroll
+      for (int t = 0; t < LMAXT; ++t)
+        if (t == len - 1) v = seq[t];
+      out[(int64_t)row * LH + j] = v;
+    }
+  }
+}
+
+// dst[k] = sum over the rule row's 16 lanes jj and the 4 gates q of
+// wt[q][jj] a_q(lane jj): the lane's column of W times the row's gate grads
+template <int JJ>
+__device__ __forceinline__ void col_terms(const float (&wi)[4][LH], const float (&wh)[4][LH], const float (&a)[4],
+                                          float &dx, float &dh) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float aq = row_bcast<JJ>(a[q]);
+    dx = fmaf(wi[q][JJ], aq, dx);
+    dh = fmaf(wh[q][JJ], aq, dh);
+  }
+  if constexpr (JJ + 1 < LH) col_terms<JJ + 1>(wi, wh, a, dx, dh);
+}
+
+__global__ __launch_bounds__(256) void lstm_train_bwd_kernel(const float *__restrict__ vocab, LstmLayerPtrs P,
+                                                             const int32_t *__restrict__ tokens, int T, int pad,
+                                                             const int64_t *__restrict__ ridx, int n, int layers,
+                                                             const float *__restrict__ act,
+                                                             const float *__restrict__ d_out, float *__restrict__ da,
+                                                             float *__restrict__ xh, float *__restrict__ dvx) {
+  // W^T images: s_wt[l][k][gate] (k < 16: w_ih column k, else w_hh column k - 16)
+  __shared__ float s_wt[LMAXL][2 * LH][LG + 1];
+  for (int i = threadIdx.x; i < layers * LG * 2 * LH; i += blockDim.x) {
+    const int l = i / (LG * 2 * LH), g = (i / (2 * LH)) % LG, k = i % (2 * LH);
+    s_wt[l][k][g] = k < LH ? P.w_ih[l][g * LH + k] : P.w_hh[l][g * LH + (k - LH)];
+  }
+  __syncthreads();
+  const int j = threadIdx.x & (LH - 1);
+  const int64_t N16 = (int64_t)n * LH;
+  const int64_t NT = (int64_t)n * T;
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 < N16; g0 += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)((g0 + threadIdx.x) / LH);
+    const bool valid = row < n;  // whole 16-lane rows agree
+    const int32_t *tok = tokens + (valid ? ridx[row] : ridx[0]) * (int64_t)T;
+    int len = 0;
+    while (len < T && tok[len] != pad) ++len;
+    if (!valid) len = 0;
+    float dseq[LMAXT];  // dL/d(this layer's output h_t), element j
+#pragma unroll
+    for (int t = 0; t < LMAXT; ++t) dseq[t] = (valid && t == len - 1) ? d_out[(int64_t)row * LH + j] : 0.f;
+#pragma unroll 1
+    for (int l = layers - 1; l >= 0; --l) {
+      float wi[4][LH], wh[4][LH];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jj = 0; jj < LH; ++jj) {
+          wi[q][jj] = s_wt[l][j][q * LH + jj];
+          wh[q][jj] = s_wt[l][LH + j][q * LH + jj];
+        }
+      const float *A = act + (int64_t)l * T * 6 * N16 + (int64_t)row * LH + j;
+      float dh_next = 0.f, dc_next = 0.f;
+#pragma unroll
+      for (int t = LMAXT - 1; t >= 0; --t) {
+        if (t >= T) continue;
+        float *dar = da + ((int64_t)l * NT + (int64_t)row * T + t) * LG;
+        float *xr = xh + ((int64_t)l * NT + (int64_t)row * T + t) * 2 * LH;
+        if (t < len) {  // uniform over the row
+          const float *at = A + (int64_t)t * 6 * N16;
+          const float gi = at[0], gf = at[N16], gg = at[2 * N16], go = at[3 * N16], c = at[4 * N16];
+          const float cp = t > 0 ? at[4 * N16 - 6 * N16] : 0.f;
+          const float hp = t > 0 ? at[5 * N16 - 6 * N16] : 0.f;
+          const float x = l == 0 ? vocab[(int64_t)tok[t] * LH + j] : act[((int64_t)((l - 1) * T + t) * 6 + 5) * N16 +
+                                                                           (int64_t)row * LH + j];
+          const float dh = dseq[t] + dh_next;
+          const float tc = tanhf(c);
+          const float dc = fmaf(dh * go, 1.f - tc * tc, dc_next);
+          float a[4];
+          a[0] = dc * gg * gi * (1.f - gi);
+          a[1] = dc * cp * gf * (1.f - gf);
+          a[2] = dc * gi * (1.f - gg * gg);
+          a[3] = dh * tc * go * (1.f - go);
+          dc_next = dc * gf;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dar[q * LH + j] = a[q];
+          xr[j] = x;
+          xr[LH + j] = hp;
+          float dx = 0.f, dhp = 0.f;
+          col_terms<0>(wi, wh, a, dx, dhp);
+          dh_next = dhp;
+          dseq[t] = dx;  // this step's gradient to the layer below (or to the vocab row)
+        } else if (valid) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dar[q * LH + j] = 0.f;
+          xr[j] = 0.f;
+          xr[LH + j] = 0.f;
+        }
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < LMAXT; ++t)
+        if (t < T) dvx[((int64_t)row * T + t) * LH + j] = t < len ? dseq[t] : 0.f;
+    }
+  }
+}
+
+// d_vocab[tok_id[u]][k] = sum of dvx rows pos[ptr[u] .. ptr[u + 1]) (in list
+// order: deterministic), one thread per (token, k); the other vocab rows are
+// zeroed by the caller.
+__global__ void vocab_grad_kernel(const float *__restrict__ dvx, const int32_t *__restrict__ tok_id,
+                                  const int32_t *__restrict__ ptr, const int32_t *__restrict__ pos, int n_tok,
+                                  float *__restrict__ d_vocab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_tok * LH) return;
+  const int u = i / LH, k = i % LH;
+  float s = 0.f;
+  for (int p = ptr[u]; p < ptr[u + 1]; ++p) s += dvx[(int64_t)pos[p] * LH + k];
+  d_vocab[(int64_t)tok_id[u] * LH + k] = s;
+}
+
 }  // namespace rnnl
 
 using namespace rnnl;
@@ -140,6 +331,79 @@ int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, c
   hipLaunchKernelGGL(lstm_encode_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      (hipStream_t)stream, vocab, w_ih,
                      w_hh, b_ih, b_hh, tokens, seq_len, pad, n_rules, layers, out, ld_out);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+static bool lstm_train_args(const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                            const float *const *b_ih, const float *const *b_hh, int32_t layers, const int32_t *tokens,
+                            int32_t seq_len, const int64_t *ridx, int32_t n, LstmLayerPtrs &P) {
+  if (!vocab || !w_ih || !w_hh || !b_ih || !b_hh || !tokens || !ridx || n <= 0 || seq_len <= 0 ||
+      seq_len > LMAXT || layers < 1 || layers > LMAXL)
+    return false;
+  for (int l = 0; l < layers; ++l) {
+    if (!w_ih[l] || !w_hh[l] || !b_ih[l] || !b_hh[l]) return false;
+    P.w_ih[l] = w_ih[l];
+    P.w_hh[l] = w_hh[l];
+    P.b_ih[l] = b_ih[l];
+    P.b_hh[l] = b_hh[l];
+  }
+  return true;
+}
+
+static unsigned lstm_blocks(int32_t n) {
+  return (unsigned)std::min<int64_t>(((int64_t)n * LH + 255) / 256, 256 * LSTM_BLOCKS_PER_CU);
+}
+
+int rnnl_lstm_train_sizes(int32_t layers, int32_t hidden, int32_t seq_len, int32_t n, size_t *act_floats,
+                          size_t *da_floats, size_t *xh_floats, size_t *dvx_floats) {
+  if (hidden != LH || layers < 1 || layers > LMAXL || seq_len <= 0 || seq_len > LMAXT || n < 0 || !act_floats ||
+      !da_floats || !xh_floats || !dvx_floats) {
+    set_error("rnnl_lstm_train_sizes: bad arguments (hidden 16, 1 <= layers <= 3, rules of <= 7 tokens)");
+    return RNNL_ERR_INVALID;
+  }
+  *act_floats = (size_t)layers * seq_len * 6 * n * LH;
+  *da_floats = (size_t)layers * n * seq_len * LG;
+  *xh_floats = (size_t)layers * n * seq_len * 2 * LH;
+  *dvx_floats = (size_t)n * seq_len * LH;
+  return RNNL_OK;
+}
+
+int rnnl_lstm_train_forward(const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                            const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                            const int32_t *tokens, int32_t seq_len, int32_t pad, const int64_t *ridx, int32_t n,
+                            float *out, float *act, void *stream) {
+  LstmLayerPtrs P{};
+  if (hidden != LH || !out || !act || !lstm_train_args(vocab, w_ih, w_hh, b_ih, b_hh, layers, tokens, seq_len, ridx, n, P)) {
+    set_error("rnnl_lstm_train_forward: bad arguments (hidden 16, 1 <= layers <= 3, rules of <= 7 tokens, n >= 1)");
+    return RNNL_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(lstm_train_fwd_kernel, dim3(lstm_blocks(n)), dim3(256), 0, (hipStream_t)stream, vocab, P, tokens,
+                     seq_len, pad, ridx, n, layers, out, act);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_lstm_train_backward(const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                             const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                             const int32_t *tokens, int32_t seq_len, int32_t pad, const int64_t *ridx, int32_t n,
+                             const float *act, const float *d_out, float *da, float *xh, float *dvx,
+                             const int32_t *tok_id, const int32_t *tok_ptr, const int32_t *tok_pos, int32_t n_tok,
+                             float *d_vocab, int32_t vocab_rows, void *stream) {
+  LstmLayerPtrs P{};
+  if (hidden != LH || !act || !d_out || !da || !xh || !dvx || !d_vocab || n_tok < 0 || vocab_rows <= 0 ||
+      (n_tok > 0 && (!tok_id || !tok_ptr || !tok_pos)) ||
+      !lstm_train_args(vocab, w_ih, w_hh, b_ih, b_hh, layers, tokens, seq_len, ridx, n, P)) {
+    set_error("rnnl_lstm_train_backward: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(lstm_train_bwd_kernel, dim3(lstm_blocks(n)), dim3(256), 0, st, vocab, P, tokens, seq_len, pad,
+                     ridx, n, layers, act, d_out, da, xh, dvx);
+  RNNL_HIP_CHECK(hipMemsetAsync(d_vocab, 0, (size_t)vocab_rows * LH * sizeof(float), st));
+  if (n_tok > 0)
+    hipLaunchKernelGGL(vocab_grad_kernel, dim3((unsigned)((n_tok * LH + 255) / 256)), dim3(256), 0, st, dvx, tok_id,
+                       tok_ptr, tok_pos, n_tok, d_vocab);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

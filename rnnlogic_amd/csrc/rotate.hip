@@ -639,7 +639,9 @@ __global__ __launch_bounds__(BW_BS) void rotate_backward_kernel(const float *__r
           if (e < E) {
             const float x = hre - a[k], y = him - b[k];
             const float s = fmaf(x, x, y * y);
-            const float w = s > 0.f ? g[(int64_t)q * E + e] / sqrtf(s) : 0.f;
+            // g / |hr - t| as g x rsq(s) (v_rsq_f32, 1 ulp): the correctly
+            // rounded sqrt + divide sequence was ~60 % of the kernel's VALU
+            const float w = s > 0.f ? g[(int64_t)q * E + e] * __builtin_amdgcn_rsqf(s) : 0.f;
             sx = fmaf(w, x, sx);
             sy = fmaf(w, y, sy);
             ta[k] = fmaf(w, x, ta[k]);
@@ -681,6 +683,74 @@ __global__ __launch_bounds__(BW_BS) void rotate_backward_kernel(const float *__r
     }
   }
 }
+
+namespace rnnl {
+
+// hr[q][d | D + d] = re | im of (h o r)_d (rotate_head: the forward's rounding)
+__global__ void hr_rows_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D,
+                               const int64_t *__restrict__ all_h, const int64_t *__restrict__ all_r,
+                               float *__restrict__ hr) {
+  const int q = blockIdx.y, d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float re, im;
+  rotate_head(eemb + all_h[q] * 2 * (int64_t)D, rtab + all_r[q] * (int64_t)D, D, d, re, im);
+  hr[(int64_t)q * 2 * D + d] = re;
+  hr[(int64_t)q * 2 * D + D + d] = im;
+}
+
+// d_eemb[e][part D + d] = d_tail[2 d + part][e]: 32 x 32 tiles through LDS
+// (the transposing copy torch's permute().reshape() made at ~1 TB/s)
+__global__ void tail_rows_kernel(const float *__restrict__ d_tail, int E, int D, float *__restrict__ d_eemb) {
+  __shared__ float ta[32][33], tb[32][33];
+  const int d0 = blockIdx.x * 32, e0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int j = ty; j < 32; j += 8) {
+    const int d = d0 + j, e = e0 + tx;
+    const bool in = d < D && e < E;
+    ta[j][tx] = in ? d_tail[(int64_t)(2 * d) * E + e] : 0.f;
+    tb[j][tx] = in ? d_tail[(int64_t)(2 * d + 1) * E + e] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int e = e0 + j, d = d0 + tx;
+    if (e < E && d < D) {
+      d_eemb[(int64_t)e * 2 * D + d] = ta[tx][j];
+      d_eemb[(int64_t)e * 2 * D + D + d] = tb[tx][j];
+    }
+  }
+}
+
+// The chain rule from d(h o r) to the head rows of eemb and to remb
+// (embedding.py:55-61: phase = remb[r] / div, (cos, sin) of the phase, the
+// complex product), one thread per dim, the rows in order (deterministic
+// sums where a head entity or relation repeats in the batch):
+//   d re_h = g_re c + g_im s          d im_h = g_im c - g_re s
+//   d c = g_re re_h + g_im im_h       d s = g_im re_h - g_re im_h
+//   d remb[r][d] += (d s c - d c s) / div
+__global__ void head_grad_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D, float gamma,
+                                 const int64_t *__restrict__ all_h, const int64_t *__restrict__ all_r, int nq,
+                                 const float *__restrict__ d_hr, float *__restrict__ d_eemb,
+                                 float *__restrict__ d_remb) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  const float div = phase_div(gamma, D);
+  for (int q = 0; q < nq; ++q) {
+    const int64_t h = all_h[q], r = all_r[q];
+    const float rh = eemb[h * 2 * D + d], ih = eemb[h * 2 * D + D + d];
+    const float2 cs = rtab[r * D + d];
+    const float gre = d_hr[(int64_t)q * 2 * D + d], gim = d_hr[(int64_t)q * 2 * D + D + d];
+    if (d_eemb) {
+      d_eemb[h * 2 * D + d] += gre * cs.x + gim * cs.y;
+      d_eemb[h * 2 * D + D + d] += gim * cs.x - gre * cs.y;
+    }
+    if (d_remb) {
+      const float dc = gre * rh + gim * ih, ds = gim * rh - gre * ih;
+      d_remb[r * D + d] += (ds * cs.x - dc * cs.y) / div;
+    }
+  }
+}
+
+}  // namespace rnnl
 
 extern "C" {
 
@@ -849,6 +919,54 @@ int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const
   const unsigned bx = (unsigned)((E + BW_BS * BW_EPT - 1) / (BW_BS * BW_EPT));
   hipLaunchKernelGGL(rotate_backward_kernel, dim3(bx, (unsigned)D), dim3(BW_BS), 0, (hipStream_t)stream, planes, ld,
                      hr, grad, nq, E, D, d_hr, d_tail);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+static size_t grads_hr_bytes(int64_t nq, int D) { return ((size_t)nq * 2 * D * sizeof(float) + 255) / 256 * 256; }
+
+int rnnl_rotate_param_grads_scratch(int32_t nq, int32_t E, int32_t D, int32_t with_eemb, size_t *bytes) {
+  if (nq < 0 || E <= 0 || D <= 0 || !bytes) {
+    set_error("rnnl_rotate_param_grads_scratch: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = 2 * grads_hr_bytes(nq, D) + (with_eemb ? (size_t)2 * D * E * sizeof(float) : 0);
+  return RNNL_OK;
+}
+
+int rnnl_rotate_param_grads(const float *eemb, const float *planes, int32_t ld, const float *rtab, float gamma,
+                            const int64_t *all_h, const int64_t *all_r, int32_t nq, int32_t E, int32_t D,
+                            int32_t n_rel_total, const float *grad, void *scratch, size_t scratch_bytes,
+                            float *d_eemb, float *d_remb, void *stream) {
+  size_t need = 0;
+  if (!eemb || !planes || !rtab || !all_h || !all_r || !grad || nq < 0 || E <= 0 || D <= 0 || ld < E ||
+      n_rel_total <= 0 || (!d_eemb && !d_remb) ||
+      rnnl_rotate_param_grads_scratch(nq, E, D, d_eemb != nullptr, &need) != RNNL_OK || !scratch ||
+      scratch_bytes < need) {
+    set_error("rnnl_rotate_param_grads: bad arguments (see rnnl_rotate_param_grads_scratch)");
+    return RNNL_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (d_remb) RNNL_HIP_CHECK(hipMemsetAsync(d_remb, 0, (size_t)n_rel_total * D * sizeof(float), st));
+  if (nq == 0) {
+    if (d_eemb) RNNL_HIP_CHECK(hipMemsetAsync(d_eemb, 0, (size_t)E * 2 * D * sizeof(float), st));
+    return RNNL_OK;
+  }
+  unsigned char *ws = static_cast<unsigned char *>(scratch);
+  float *hr = reinterpret_cast<float *>(ws);
+  float *d_hr = reinterpret_cast<float *>(ws + grads_hr_bytes(nq, D));
+  float *d_tail = d_eemb ? reinterpret_cast<float *>(ws + 2 * grads_hr_bytes(nq, D)) : nullptr;
+  hipLaunchKernelGGL(hr_rows_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)nq), dim3(256), 0, st, eemb,
+                     (const float2 *)rtab, D, all_h, all_r, hr);
+  RNNL_HIP_CHECK(hipMemsetAsync(d_hr, 0, (size_t)nq * 2 * D * sizeof(float), st));
+  const unsigned bx = (unsigned)((E + BW_BS * BW_EPT - 1) / (BW_BS * BW_EPT));
+  hipLaunchKernelGGL(rotate_backward_kernel, dim3(bx, (unsigned)D), dim3(BW_BS), 0, st, planes, ld, hr, grad, nq, E, D,
+                     d_hr, d_tail);
+  if (d_eemb)
+    hipLaunchKernelGGL(tail_rows_kernel, dim3((unsigned)((D + 31) / 32), (unsigned)((E + 31) / 32)), dim3(256), 0, st,
+                       d_tail, E, D, d_eemb);
+  hipLaunchKernelGGL(head_grad_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, st, eemb,
+                     (const float2 *)rtab, D, gamma, all_h, all_r, nq, d_hr, d_eemb, d_remb);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

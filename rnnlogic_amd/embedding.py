@@ -17,45 +17,49 @@ from . import _native
 
 
 class _RotatEScore(torch.autograd.Function):
-    """score = gamma - sum_d |hr - t| for every (row, entity): forward by the
-    HIP scorer (rnnl_rotate_score), backward by rnnl_rotate_backward, which
-    writes dL/d(tail embeddings) and dL/d(h o r) without the (B, |E|, D)
-    difference tensors of the torch formulation; h o r is formed by torch
-    ops from eemb / remb so autograd carries d(h o r) on to h and r."""
+    """score = gamma - sum_d |h o r - t| for every (row, entity): forward by the
+    HIP scorer (rnnl_rotate_score), backward by rnnl_rotate_param_grads, which
+    writes dL/d eemb (tail term + head rows) and dL/d remb in eemb's / remb's
+    layouts — no (B, |E|, D) difference tensors, no dense embedding-gather
+    gradient, no transposing copy, and none of the torch launches that formed
+    h o r for autograd."""
 
     @staticmethod
-    def forward(ctx, eemb, hr_re, hr_im, module, all_h, all_r):
+    def forward(ctx, eemb, remb, module, all_h, all_r):
         out = torch.empty((all_h.numel(), module.num_entities), dtype=torch.float32, device=eemb.device)
         module.score_into(all_h, all_r, out)
         ctx.module = module
-        ctx.save_for_backward(eemb, hr_re, hr_im)
+        ctx.save_for_backward(all_h, all_r)
         return out
 
     @staticmethod
     def backward(ctx, grad):
-        eemb, hr_re, hr_im = ctx.saved_tensors
-        E, D = ctx.module.num_entities, ctx.module.emb_dim
-        nq = hr_re.size(0)
-        if ctx.module.mode == _native.ROTATE_DIRECT:
-            # the forward's entity planes [D][2][Ep] (rnnl_rotate_entity_table,
-            # cached for this weight version): no transposed copy of the table
-            planes = ctx.module._device_tables()[0]
-            ld = planes.numel() // (2 * D)
+        all_h, all_r = ctx.saved_tensors
+        m = ctx.module
+        E, D = m.num_entities, m.emb_dim
+        dev = grad.device
+        nq = all_h.numel()
+        need_e, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not (need_e or need_r):
+            return None, None, None, None, None
+        planes, rtab = m._device_tables()  # cached for this weight version by the forward
+        if m.mode == _native.ROTATE_DIRECT:
+            ld = planes.numel() // (2 * D)  # the forward's entity planes [D][2][ld]
         else:
-            planes = eemb.detach().view(E, 2, D).permute(2, 1, 0).contiguous()  # [D][2][E]
+            planes = m.eemb.detach().view(E, 2, D).permute(2, 1, 0).contiguous()
             ld = E
-        hr = torch.cat([hr_re, hr_im], dim=1).detach().float().contiguous()
         grad = grad.detach().float().contiguous()
-        d_hr = torch.zeros((nq, 2 * D), dtype=torch.float32, device=eemb.device)
-        # the tail gradient only when eemb is trained (a frozen table with a
-        # trained remb still needs d(h o r))
-        need_tail = ctx.needs_input_grad[0]
-        d_tail = torch.empty((D, 2, E), dtype=torch.float32, device=eemb.device) if need_tail else None
-        _native.call("rnnl_rotate_backward", planes.data_ptr(), ld, hr.data_ptr(), grad.data_ptr(), nq, E, D,
-                     d_hr.data_ptr(), d_tail.data_ptr() if need_tail else None,
-                     torch.cuda.current_stream(eemb.device).cuda_stream)
-        d_eemb = d_tail.permute(2, 1, 0).reshape(E, 2 * D) if need_tail else None
-        return d_eemb, d_hr[:, :D], d_hr[:, D:], None, None, None
+        nb = ctypes.c_size_t()
+        _native.call("rnnl_rotate_param_grads_scratch", nq, E, D, int(need_e), ctypes.byref(nb))
+        scratch = m._grad_scratch(nb.value)
+        d_eemb = torch.empty((E, 2 * D), dtype=torch.float32, device=dev) if need_e else None
+        d_remb = torch.empty_like(m.remb, dtype=torch.float32) if need_r else None
+        eemb = m.eemb.detach().contiguous()
+        _native.call("rnnl_rotate_param_grads", eemb.data_ptr(), planes.data_ptr(), ld, rtab.data_ptr(),
+                     float(m.gamma), all_h.data_ptr(), all_r.data_ptr(), nq, E, D, m.remb.size(0), grad.data_ptr(),
+                     scratch.data_ptr(), scratch.numel(), d_eemb.data_ptr() if need_e else None,
+                     d_remb.data_ptr() if need_r else None, torch.cuda.current_stream(dev).cuda_stream)
+        return d_eemb, d_remb, None, None, None
 
 
 class RotatE(torch.nn.Module):
@@ -116,6 +120,14 @@ class RotatE(torch.nn.Module):
             self._ws = torch.empty((need.value + 3) // 4, dtype=torch.float32, device=self.eemb.device)
         return self._ws.data_ptr(), need.value
 
+    def _grad_scratch(self, nbytes):
+        """Device scratch of rnnl_rotate_param_grads (kept across steps; the
+        stream orders its reuse)."""
+        g = getattr(self, "_gs", None)
+        if g is None or g.numel() < nbytes or g.device != self.eemb.device:
+            g = self._gs = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.eemb.device)
+        return g
+
     def native_args(self, nq, pieces=1, first_share=0.0):
         """rnnl_rotate_args for a launch over nq rows (the one-call forward,
         rnnl_predictorplus_forward_rotate): the weight tables and workspace
@@ -173,19 +185,11 @@ class RotatE(torch.nn.Module):
     @_native.on_input_device
     def forward_grad(self, all_h, all_r):
         """Differentiable (B, |E|) scores for training: the HIP scorer forward
-        and rnnl_rotate_backward (_RotatEScore); h o r by torch ops, as in
-        forward_torch, so autograd reaches eemb rows of h and remb."""
-        pi = 3.141592653589793238462643383279
-        D = self.emb_dim
-        all_h = all_h.to(self.eemb.device, torch.int64)
-        all_r = all_r.to(self.eemb.device, torch.int64)
-        h = self.eemb.index_select(0, all_h)
-        phase = self.remb.index_select(0, all_r) / (self.range / pi)
-        re_r, im_r = torch.cos(phase), torch.sin(phase)
-        re_h, im_h = h[:, :D], h[:, D:]
-        re_hr = re_h * re_r - im_h * im_r
-        im_hr = re_h * im_r + im_h * re_r
-        return _RotatEScore.apply(self.eemb, re_hr, im_hr, self, all_h, all_r)
+        and rnnl_rotate_param_grads (_RotatEScore), which carries the gradient
+        to the tail entities, the head rows and the relation phases."""
+        all_h = all_h.to(self.eemb.device, torch.int64).contiguous()
+        all_r = all_r.to(self.eemb.device, torch.int64).contiguous()
+        return _RotatEScore.apply(self.eemb, self.remb, self, all_h, all_r)
 
     @_native.on_input_device
     def forward(self, all_h, all_r):

@@ -1000,6 +1000,67 @@ class _PlusSumTrain(torch.autograd.Function):
         return (None,) * 7 + (g_base,) + tuple(grads)
 
 
+class _LstmRules(torch.autograd.Function):
+    """PredictorPlus.encode_rules (predictors.py:201-208) for type 'lstm' under
+    autograd: the top layer's output at each rule's last token for the rules
+    ridx, by rnnl_lstm_train_forward (the inference encoder's recurrence, each
+    step's gates and states saved), and its backward through time by
+    rnnl_lstm_train_backward — the gate-gradient and layer-input rows, then
+    dW = da^T [x | h_prev] and db = sum(da) as batched GEMMs, and the vocab
+    rows' gradient summed per token in position order.  Replaces the library
+    LSTM's per-layer / per-step kernels and its host work (~1.6 ms per step)."""
+
+    @staticmethod
+    def forward(ctx, module, ridx, tok, csr, vocab_w, *params):
+        L, T, n = module.num_layers, tok.size(1), ridx.numel()
+        dev = ridx.device
+        sizes = [ctypes.c_size_t() for _ in range(4)]
+        _native.call("rnnl_lstm_train_sizes", L, 16, T, n, *[ctypes.byref(x) for x in sizes])
+        act = torch.empty(sizes[0].value, dtype=torch.float32, device=dev)
+        out = torch.empty((n, 16), dtype=torch.float32, device=dev)
+        vocab = vocab_w.detach().float().contiguous()
+        ps = [p.detach().float().contiguous() for p in params]
+        arrs = _LstmRules._ptrs(ps, L)
+        ridx = ridx.contiguous()
+        _native.call("rnnl_lstm_train_forward", vocab.data_ptr(), *arrs, L, 16, tok.data_ptr(), T, module.padding_index,
+                     ridx.data_ptr(), n, out.data_ptr(), act.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        ctx.module, ctx.csr, ctx.tok, ctx.sizes = module, csr, tok, [x.value for x in sizes]
+        ctx.save_for_backward(ridx, act, vocab, *ps)
+        return out
+
+    @staticmethod
+    def _ptrs(ps, L):
+        arr = lambda k: (ctypes.c_void_p * 3)(*[ps[4 * l + k].data_ptr() for l in range(L)])  # noqa: E731
+        return [arr(0), arr(1), arr(2), arr(3)]
+
+    @staticmethod
+    def backward(ctx, d_out):
+        ridx, act, vocab, *ps = ctx.saved_tensors
+        m = ctx.module
+        L, T, n = m.num_layers, ctx.tok.size(1), ridx.numel()
+        dev = d_out.device
+        _, n_da, n_xh, n_dvx = ctx.sizes
+        da = torch.empty(n_da, dtype=torch.float32, device=dev)
+        xh = torch.empty(n_xh, dtype=torch.float32, device=dev)
+        dvx = torch.empty(n_dvx, dtype=torch.float32, device=dev)
+        d_vocab = torch.empty_like(vocab)
+        tok_id, ptr, pos, n_tok, _ = ctx.csr
+        d_out = d_out.detach().float().contiguous()
+        _native.call("rnnl_lstm_train_backward", vocab.data_ptr(), *_LstmRules._ptrs(ps, L), L, 16, ctx.tok.data_ptr(),
+                     T, m.padding_index, ridx.data_ptr(), n, act.data_ptr(), d_out.data_ptr(), da.data_ptr(),
+                     xh.data_ptr(), dvx.data_ptr(), tok_id.data_ptr(), ptr.data_ptr(), pos.data_ptr(), n_tok,
+                     d_vocab.data_ptr(), vocab.size(0), torch.cuda.current_stream(dev).cuda_stream)
+        da_t = da.view(L, n * T, 64).transpose(1, 2)
+        xh = xh.view(L, n * T, 32)
+        d_wih = torch.bmm(da_t, xh[:, :, :16])
+        d_whh = torch.bmm(da_t, xh[:, :, 16:])
+        d_b = da_t.sum(2)
+        grads = []
+        for k in range(L):
+            grads += [d_wih[k], d_whh[k], d_b[k], d_b[k].clone()]
+        return (None, None, None, None, d_vocab) + tuple(grads)
+
+
 class PredictorPlus(_HipGrounding, torch.nn.Module):
     """Reference src/predictors.py:121-271, forward on the HIP path."""
 
@@ -1431,7 +1492,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         else:
             rels = [head] if head >= 0 else torch.unique(all_r).tolist()
             ridx = self._rule_ids(rels, device)
-            x_f = self._encode_rules_padded(ridx, device)
+            x_f = self._encode_rules_padded(ridx, device, rels)
             emb = torch.zeros((self.num_rules, self.hidden_dim), dtype=x_f.dtype, device=device).index_copy(
                 0, ridx, x_f)
         if self.entity_feature == "bias":
@@ -1507,7 +1568,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if self.type == "emb":
             x_f = self.rule_emb.index_select(0, ridx)
         else:
-            x_f = self._encode_rules_padded(ridx, device)
+            x_f = self._encode_rules_padded(ridx, device, rels)
         nodes = nr.node_of_rule[ridx]
         H = self.hidden_dim
         # gathers of differentiable tables use index_select: its backward is an
@@ -1565,14 +1626,60 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             return hit
         return torch.tensor([i for q in rels for i, _ in self.relation2rules[q]], dtype=torch.long, device=device)
 
-    def _encode_rules_padded(self, ridx, device):
+    def _lstm_hip(self, device):
+        """The rule encoder's HIP training path applies: an LSTM of the fused
+        kernels' shape (hidden 16, 1-3 layers, rules of <= 7 tokens)."""
+        return (self.type == "lstm" and device.type == "cuda" and self.hidden_dim == 16 and
+                1 <= self.num_layers <= 3 and self.rule_features.size(1) <= 8 and self.rnn.bias and
+                not self.rnn.bidirectional and self.rnn.proj_size == 0)
+
+    def _token_csr(self, rels, device):
+        """Per-token positions (row T + t) of the non-pad tokens of the rules of
+        `rels` (in _rule_ids order), grouped by token id in position order:
+        (tok_id, ptr, pos) on the device — the vocab-row gradient's sum order
+        (rnnl_lstm_train_backward).  One relation's lists are cached."""
+        key = ("csr", self._device_index(device), tuple(rels))
+        hit = self._tok_cache.get(key)
+        if hit is not None:
+            return hit
+        ids = [i for q in rels for i, _ in self.relation2rules[q]]
+        tok = self.rule_features.numpy()[ids]
+        T = tok.shape[1]
+        flat = tok.reshape(-1)
+        pos = np.nonzero(flat != self.padding_index)[0]
+        order = np.argsort(flat[pos], kind="stable")
+        pos = pos[order]
+        vals = flat[pos]
+        tok_id, counts = np.unique(vals, return_counts=True)
+        ptr = np.concatenate([[0], np.cumsum(counts)])
+        packed = torch.from_numpy(np.concatenate([tok_id, ptr, pos]).astype(np.int32)).to(device)
+        u = tok_id.size
+        hit = (packed[:u], packed[u:2 * u + 1], packed[2 * u + 1:], u, T)
+        if len(rels) == 1:
+            self._tok_cache[key] = hit
+        return hit
+
+    def _encode_rules_padded(self, ridx, device, rels=None):
         """encode_rules over the rules `ridx` with autograd (the training
-        path).  The token table lives on the device (uploaded once), and the
+        path).  An LSTM of the fused shape runs the HIP recurrence and its
+        backward through time (_LstmRules); otherwise the torch modules.  The
+        token table lives on the device (uploaded once), and the
         LSTM input is padded to a fixed row count — the largest per-relation
         rule list, or a multiple of 512 beyond it — so the recurrent kernels
         see one shape, not one per relation (a new RNN shape costs a kernel
         selection on its first use).  The padding rows repeat rule 0; their
         outputs are dropped, so they add nothing to the gradients."""
+        if rels is not None and self._lstm_hip(device) and ridx.numel() > 0:
+            rnn = self.rnn
+            params = []
+            for k in range(self.num_layers):
+                params += [getattr(rnn, "%s_l%d" % (name, k)) for name in ("weight_ih", "weight_hh", "bias_ih",
+                                                                             "bias_hh")]
+            key = self._device_index(device)
+            tok = self._tok_cache.get(key)
+            if tok is None:
+                tok = self._tok_cache[key] = self.rule_features.to(dtype=torch.int32).contiguous().to(device)
+            return _LstmRules.apply(self, ridx, tok, self._token_csr(rels, device), self.vocab_emb.weight, *params)
         key = ("tok64", self._device_index(device))
         tok = self._tok_cache.get(key)
         if tok is None:

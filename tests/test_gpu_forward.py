@@ -373,3 +373,43 @@ def test_rotate_split_form_is_bitwise(data, dev):
             zero = torch.zeros_like(big)
             rot.score_into(h, r, zero, accumulate=2, pieces=pieces, first_share=share)
             assert torch.equal(zero, big), ("atomic", pieces, share)
+
+
+@pytest.mark.parametrize("data", ["umls", "FB15k-237"])
+def test_lstm_train_path_matches_torch(data, dev):
+    """_LstmRules (rnnl_lstm_train_forward / _backward) == torch's LSTM under
+    autograd (PredictorPlus.encode_rules) on the rules of single relations and
+    of a mixed relation set: the outputs and every parameter gradient (the
+    three layers' weights and biases and the vocab rows) for a random upstream
+    gradient.  The vocab's padding row gets no gradient in either."""
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.predictors import PredictorPlus, _LstmRules  # noqa: F401
+    torch.manual_seed(5)
+    graph = graph_for(datasets.materialize(data))
+    model = PredictorPlus(graph, type="lstm", num_layers=3, hidden_dim=16)
+    model.set_rules(datasets.rule_file(data))
+    model = model.to(dev).train()
+    counts = [len(x) for x in model.relation2rules]
+    order = np.argsort(counts)[::-1]
+    cases = [[int(order[0])], [int(order[len(order) // 3])], sorted(int(x) for x in order[1:4])]
+    names = ["vocab_emb.weight"] + ["rnn.%s_l%d" % (n, k) for k in range(3)
+                                    for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+    params = dict(model.named_parameters())
+    for rels in cases:
+        if sum(counts[q] for q in rels) == 0:
+            continue
+        ridx = model._rule_ids(rels, dev)
+        g = torch.randn(ridx.numel(), 16, generator=torch.Generator().manual_seed(len(rels))).to(dev)
+        res = []
+        for hip in (False, True):
+            model.zero_grad()
+            out = model._encode_rules_padded(ridx, dev, rels if hip else None)
+            (out * g).sum().backward()
+            res.append((out.detach().clone(), {n: params[n].grad.detach().clone() for n in names}))
+        (o0, g0), (o1, g1) = res
+        assert float((o0 - o1).abs().max()) <= 2e-6, rels
+        for n in names:
+            a, b = g0[n].cpu().numpy(), g1[n].cpu().numpy()
+            scale = float(np.abs(a).max())
+            np.testing.assert_allclose(b, a, atol=1e-5 * scale + 1e-6, rtol=1e-4, err_msg="%s %s" % (rels, n))
+        assert float(g1["vocab_emb.weight"][model.padding_index].abs().max()) == 0.0
