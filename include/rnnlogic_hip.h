@@ -122,6 +122,17 @@ int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, c
                      int32_t layers, int32_t hidden, const int32_t *tokens, int32_t n_rules, int32_t seq_len,
                      int32_t pad, float *out, int32_t ld_out, void *stream);
 
+/* rnnl_lstm_encode over the rule trie of r (the rules given to
+ * rnnl_rules_create, token order [head, body...]): one LSTM step per trie
+ * node (prefixes shared by many rules are computed once), one launch per
+ * depth.  out: the same n_rules x 16 rows as rnnl_lstm_encode of those
+ * rules, bitwise.  scratch: rnnl_lstm_encode_trie_scratch bytes (the
+ * per-node states). */
+int rnnl_lstm_encode_trie_scratch(rnnl_rules r, int32_t layers, size_t *bytes);
+int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *w_ih, const float *w_hh, const float *b_ih,
+                          const float *b_hh, int32_t layers, int32_t hidden, float *out, int32_t ld_out,
+                          void *scratch, size_t scratch_bytes, void *stream);
+
 /* The rule encoder under autograd (training; predictors.py:201-208 and
  * torch.nn.LSTM's backward): the rules ridx[0..n) (int64 rows of `tokens`).
  * Per-layer weights come as arrays of `layers` pointers (w_ih[l]: 64 x 16,

@@ -121,6 +121,81 @@ __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restric
 }
 
 // ---------------------------------------------------------------------------
+// The same encoder over the rule trie (rnnl_lstm_encode_trie).  The LSTM is
+// causal and a rule's tokens are [head, body...], so every prefix a trie node
+// stands for (the root: [head]) has one state, shared by all rules through
+// it: one step per trie node (FB15k-237: 183,810 nodes instead of 473,782
+// rule steps), one launch per depth.  A 16-lane row owns TK nodes of a level
+// and runs them layer by layer, so each layer's gate rows are read from LDS
+// once per TK nodes; the step reads the parent's (h, c) of every layer from
+// `state` [node][layer][h | c][16] and writes the node's.  The arithmetic of
+// a step is lstm_encode_kernel's, on the same inputs: the outputs are
+// bitwise those of rnnl_lstm_encode.  A node's top-layer h goes to every
+// rule ending there.
+constexpr int TK = 4;
+
+__global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__restrict__ vocab,
+                                                              const float *__restrict__ w_ih,
+                                                              const float *__restrict__ w_hh,
+                                                              const float *__restrict__ b_ih,
+                                                              const float *__restrict__ b_hh, RulesDev rl,
+                                                              int lv0, int n_level, int layers,
+                                                              float *__restrict__ state, float *__restrict__ out,
+                                                              int ld_out) {
+  __shared__ LstmLds S;
+  for (int i = threadIdx.x; i < layers * LG * 2 * LH; i += blockDim.x) {
+    const int l = i / (LG * 2 * LH), g = (i / (2 * LH)) % LG, k = i % (2 * LH);
+    S.w[l][g][k] = k < LH ? w_ih[(l * LG + g) * LH + k] : w_hh[(l * LG + g) * LH + (k - LH)];
+  }
+  for (int i = threadIdx.x; i < layers * LG; i += blockDim.x) S.b[i / LG][i % LG] = b_ih[i] + b_hh[i];
+  __syncthreads();
+  const int j = threadIdx.x & (LH - 1);
+  const int64_t n_groups = ((int64_t)n_level + TK - 1) / TK;
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 < n_groups * LH; g0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t grp = (g0 + threadIdx.x) / LH;  // uniform over the 16-lane row
+    int node[TK], par[TK];
+    float x[TK];
+#pragma unroll
+    for (int k = 0; k < TK; ++k) {
+      const int64_t i = grp * TK + k;
+      node[k] = i < n_level ? rl.level_nodes[lv0 + i] : -1;
+      par[k] = node[k] >= 0 ? rl.node_parent[node[k]] : -1;
+      x[k] = node[k] >= 0 ? vocab[(int64_t)rl.node_tok[node[k]] * LH + j] : 0.f;
+    }
+#pragma unroll 1
+    for (int l = 0; l < layers; ++l) {
+      float w[4][2 * LH], bias[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bias[q] = S.b[l][q * LH + j];
+#pragma unroll
+        for (int k = 0; k < 2 * LH; ++k) w[q][k] = S.w[l][q * LH + j][k];
+      }
+#pragma unroll
+      for (int k = 0; k < TK; ++k) {
+        if (node[k] >= 0) {  // uniform over the row
+          const float *ps = state + ((int64_t)par[k] * layers + l) * 2 * LH;
+          const float h = par[k] >= 0 ? ps[j] : 0.f, c0 = par[k] >= 0 ? ps[LH + j] : 0.f;
+          float a[4] = {bias[0], bias[1], bias[2], bias[3]};
+          gate_terms<0>(w, x[k], h, a);
+          const float c = fmaf(sigm(a[1]), c0, sigm(a[0]) * tanhf(a[2]));
+          const float hn = sigm(a[3]) * tanhf(c);
+          float *st = state + ((int64_t)node[k] * layers + l) * 2 * LH;
+          st[j] = hn;
+          st[LH + j] = c;
+          x[k] = hn;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < TK; ++k)
+      if (node[k] >= 0)
+        for (int m = rl.node_rule_ptr[node[k]]; m < rl.node_rule_ptr[node[k] + 1]; ++m)
+          out[(int64_t)rl.node_rules[m] * ld_out + j] = x[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Training (autograd through the rule encoder): the same recurrence over the
 // rules ridx[0..n) of one batch, saving each step's activations, and the
 // backward through time.  Activation / gradient rows are (row, t) = row T + t.
@@ -331,6 +406,37 @@ int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, c
   hipLaunchKernelGGL(lstm_encode_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      (hipStream_t)stream, vocab, w_ih,
                      w_hh, b_ih, b_hh, tokens, seq_len, pad, n_rules, layers, out, ld_out);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_lstm_encode_trie_scratch(rnnl_rules r, int32_t layers, size_t *bytes) {
+  if (!r || layers < 1 || layers > LMAXL || !bytes) {
+    set_error("rnnl_lstm_encode_trie_scratch: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = (size_t)std::max(r->d.n_nodes, 1) * layers * 2 * LH * sizeof(float);
+  return RNNL_OK;
+}
+
+int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *w_ih, const float *w_hh, const float *b_ih,
+                          const float *b_hh, int32_t layers, int32_t hidden, float *out, int32_t ld_out,
+                          void *scratch, size_t scratch_bytes, void *stream) {
+  size_t need = 0;
+  if (!r || !vocab || !w_ih || !w_hh || !b_ih || !b_hh || !out || hidden != LH || ld_out < LH ||
+      rnnl_lstm_encode_trie_scratch(r, layers, &need) != RNNL_OK || !scratch || scratch_bytes < need) {
+    set_error("rnnl_lstm_encode_trie: bad arguments (hidden 16, 1 <= layers <= 3, scratch: "
+              "rnnl_lstm_encode_trie_scratch)");
+    return RNNL_ERR_INVALID;
+  }
+  for (size_t d = 0; d + 1 < r->level_ptr.size(); ++d) {
+    const int lv0 = r->level_ptr[d], n = r->level_ptr[d + 1] - lv0;
+    if (n <= 0) continue;
+    const int64_t lanes = ((int64_t)n + TK - 1) / TK * LH;
+    const unsigned blocks = (unsigned)std::min<int64_t>((lanes + 255) / 256, 256 * LSTM_BLOCKS_PER_CU);
+    hipLaunchKernelGGL(lstm_trie_level_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, w_ih, w_hh,
+                       b_ih, b_hh, r->d, lv0, n, layers, static_cast<float *>(scratch), out, ld_out);
+  }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

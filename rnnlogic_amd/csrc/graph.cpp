@@ -179,6 +179,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   std::vector<int32_t> node_rel, node_child, node_nchild, node_nrules, node_rule_ptr(1, 0), node_rules;
   std::vector<uint64_t> node_fp;
   std::vector<int32_t> node_of_rule(n_rules, -1);
+  std::vector<int32_t> node_parent, node_tok, node_depth;
   int max_depth = 0;
   for (int r = 0; r < R; ++r) {
     auto &t = tries[r];
@@ -195,6 +196,9 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
     for (int loc : order) {
       const TNode &nd = t[loc];
       node_rel.push_back(nd.rel);
+      node_parent.push_back(nd.parent >= 0 ? newid[nd.parent] : -1);
+      node_tok.push_back(nd.parent >= 0 ? nd.rel : r);
+      node_depth.push_back(nd.depth);
       node_child.push_back(nd.child.empty() ? 0 : newid[nd.child.begin()->second]);
       node_nchild.push_back((int)nd.child.size());
       node_nrules.push_back((int)nd.rules.size());
@@ -249,6 +253,14 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
     }
   }
   head_leaf_ptr[R] = (int32_t)head_leaf_node.size();
+  // nodes by depth (ascending id within a depth): the encoder's levels
+  std::vector<int32_t> level_ptr(max_depth + 2, 0), level_nodes(n_nodes_total);
+  for (int n = 0; n < n_nodes_total; ++n) ++level_ptr[node_depth[n] + 1];
+  for (int d = 0; d <= max_depth; ++d) level_ptr[d + 1] += level_ptr[d];
+  {
+    std::vector<int32_t> fill(level_ptr.begin(), level_ptr.end() - 1);
+    for (int n = 0; n < n_nodes_total; ++n) level_nodes[fill[node_depth[n]]++] = n;
+  }
   auto *rs = new rnnl_rules_s;
   (void)hipGetDevice(&rs->device);
   rs->R = R;
@@ -260,6 +272,7 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
   rs->node_of_rule = std::move(node_of_rule);
   rs->head_root = head_root;
   rs->head_nodes = head_nodes;
+  rs->level_ptr = level_ptr;
   rs->d.max_leaves = max_leaves;
   rs->d.max_head_nodes = max_head_nodes;
   std::vector<int32_t> node_info(4 * node_rel.size());
@@ -284,7 +297,10 @@ int rnnl_rules_create(rnnl_graph g, const int32_t *tok, const int64_t *ptr, int3
       (rc = upload(head_leaf_ptr, &rs->mem[10], &rs->d.head_leaf_ptr)) ||
       (rc = upload(head_leaf_node, &rs->mem[11], &rs->d.head_leaf_node)) ||
       (rc = upload(node_leaf, &rs->mem[12], &rs->d.node_leaf)) ||
-      (rc = upload(node_info, &rs->mem[13], &node_info_dev))) {
+      (rc = upload(node_info, &rs->mem[13], &node_info_dev)) ||
+      (rc = upload(node_parent, &rs->mem[14], &rs->d.node_parent)) ||
+      (rc = upload(node_tok, &rs->mem[15], &rs->d.node_tok)) ||
+      (rc = upload(level_nodes, &rs->mem[16], &rs->d.level_nodes))) {
     rnnl_rules_destroy(rs);
     return rc;
   }

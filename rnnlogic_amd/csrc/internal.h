@@ -63,6 +63,12 @@ struct RulesDev {
   const int32_t *node_leaf = nullptr;       // n_nodes: local leaf index within its head, -1 if none
   // the grounding walk's per-node fields in one 16-B load: (rel, first child, nchild, nrules)
   const int4 *node_info = nullptr;
+  // the rule encoder over the trie (rnnl_lstm_encode_trie): per node its
+  // parent (-1 at a root) and LSTM input token (the head relation at a root,
+  // else node_rel); the nodes grouped by depth (level_nodes, host level_ptr)
+  const int32_t *node_parent = nullptr;
+  const int32_t *node_tok = nullptr;
+  const int32_t *level_nodes = nullptr;
 };
 
 // Node-weight records (bytes per node); see rnnl_node_weights.
@@ -85,8 +91,9 @@ struct rnnl_rules_s {
   rnnl::RulesDev d;
   int device = 0;
   int32_t R = 0, E = 0;
-  void *mem[16] = {};
+  void *mem[20] = {};
   std::vector<int32_t> node_of_rule;  // host: trie node where each rule's body ends
+  std::vector<int32_t> level_ptr;     // host: max_depth + 2 offsets into d.level_nodes
   std::vector<int32_t> head_root;     // host copy of d.head_root (R)
   std::vector<int32_t> head_nodes;    // host copy of d.head_nodes (R)
 };

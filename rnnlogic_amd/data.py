@@ -8,6 +8,7 @@ CSR once per GPU (rnnl_graph_create) and the PredictorPlus forward grounds
 rules there with the HIP kernel instead of the dense one-hot propagation of
 the reference (data.py:136-173).
 """
+import itertools
 import os
 import random
 
@@ -268,7 +269,8 @@ class _RowTable(object):
             lens = np.fromiter((len(b) for b in batches), dtype=np.int64, count=len(batches))
             off = np.zeros(len(batches) + 1, dtype=np.int64)
             np.cumsum(lens, out=off[1:])
-            flat = np.asarray([x for b in batches for x in b], dtype=np.int64).reshape(-1, 3)
+            chain = itertools.chain.from_iterable
+            flat = np.fromiter(chain(chain(batches)), dtype=np.int64, count=3 * int(off[-1])).reshape(-1, 3)
             self.tab = torch.from_numpy(flat).to(self.device)
             self.lens, self.off = lens, off
             self._src, self._refs = batches, tuple(batches)

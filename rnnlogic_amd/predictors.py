@@ -1143,6 +1143,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # the step reads its status and relation without waiting on the GPU
         self._pf = {}
         self.prefetch_depth = 2
+        # the inference rule encoder over the rule trie (rnnl_lstm_encode_trie,
+        # bitwise the per-rule rnnl_lstm_encode with 2.6x fewer LSTM steps on
+        # FB15k-237); False: one lane row per rule
+        self.encoder_trie = True
         self.prefetch_dropped = 0
 
     # ------------------------------------------------------------------ rules
@@ -1196,6 +1200,21 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                                         for k in range(L)]).contiguous()
         w_ih, w_hh, b_ih, b_hh = cat("weight_ih"), cat("weight_hh"), cat("bias_ih"), cat("bias_hh")
         vocab = self.vocab_emb.weight.detach().float().contiguous()
+        out = torch.empty((self.num_rules, self.hidden_dim), dtype=torch.float32, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if self.encoder_trie:
+            # one step per rule-trie node: prefixes shared by many rules run once
+            nr = self.native_rules(device)
+            key = ("trie_state", self._device_index(device))
+            st = self._side.get(key)
+            if st is None:
+                n = ctypes.c_size_t()
+                _native.call("rnnl_lstm_encode_trie_scratch", nr.ptr, L, ctypes.byref(n))
+                st = self._side[key] = torch.empty(n.value, dtype=torch.uint8, device=device)
+            _native.call("rnnl_lstm_encode_trie", nr.ptr, vocab.data_ptr(), w_ih.data_ptr(), w_hh.data_ptr(),
+                         b_ih.data_ptr(), b_hh.data_ptr(), L, self.hidden_dim, out.data_ptr(), out.stride(0),
+                         st.data_ptr(), st.numel(), stream)
+            return out
         # rule tokens depend only on the rule set: cached across invalidate_cache()
         # (a pageable host->device copy per forward costs 1-20 ms depending on the host)
         key = self._device_index(device)
@@ -1203,20 +1222,40 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if tok is None:
             tok = self.rule_features.to(dtype=torch.int32).contiguous().to(device)
             self._tok_cache[key] = tok
-        out = torch.empty((self.num_rules, self.hidden_dim), dtype=torch.float32, device=device)
         _native.call("rnnl_lstm_encode", vocab.data_ptr(), w_ih.data_ptr(), w_hh.data_ptr(), b_ih.data_ptr(),
                      b_hh.data_ptr(), L, self.hidden_dim, tok.data_ptr(), self.num_rules, tok.size(1),
-                     self.padding_index, out.data_ptr(), out.stride(0), torch.cuda.current_stream(device).cuda_stream)
+                     self.padding_index, out.data_ptr(), out.stride(0), stream)
         return out
+
+    def _source_lists(self):
+        """(node-weight sources, scoring-parameter sources): the tensors the
+        cached node records and parameter block are derived from.  The lists
+        are rebuilt when a direct submodule / parameter object or the rule set
+        is replaced (a per-batch forward otherwise walks no module tree); the
+        caches' keys then read each tensor's storage and version."""
+        struct = (tuple(map(id, self._modules.values())), tuple(map(id, self._parameters.values())),
+                  id(getattr(self, "rule_emb", None)))
+        hit = self.__dict__.get("_src_lists")
+        if hit is not None and hit[0] == struct:
+            return hit[1], hit[2]
+        rte, sm = self.rule_to_entity, self.score_model
+        # SUM records carry FuncToNodeSum's Linear weight (rnnl_node_weights)
+        node_srcs = self._embedding_sources() + ([rte.add_model.layers[0].weight] if self.aggregator == "sum" else [])
+        param_srcs = [rte.add_model.layers[0].weight, rte.add_model.layers[0].bias, rte.layer_norm.weight,
+                      rte.layer_norm.bias, sm.layers[0].weight, sm.layers[0].bias, sm.layers[1].weight,
+                      sm.layers[1].bias, self.relation_emb.weight]
+        if self.entity_feature == "bias":
+            param_srcs.append(self.bias)
+        self.__dict__["_src_lists"] = (struct, node_srcs, param_srcs)
+        return node_srcs, param_srcs
 
     def node_weights(self, device):
         """Per-trie-node aggregates of the rule embeddings (HIP), cached until a
         source parameter changes (optimizer steps bump `_version`)."""
         nr = self.native_rules(device)
-        # SUM records carry FuncToNodeSum's Linear weight (rnnl_node_weights)
-        srcs = self._embedding_sources() + ([self.rule_to_entity.add_model.layers[0].weight]
-                                            if self.aggregator == "sum" else [])
-        key = (self._device_index(device), self.aggregator, tuple((p.data_ptr(), p._version) for p in srcs))
+        srcs = self._source_lists()[0]
+        key = (self._device_index(device), self.aggregator, tuple([p.data_ptr() for p in srcs]),
+               tuple([p._version for p in srcs]))
         hit = self._node_cache.get(device)
         if hit is not None and hit[0] == key:
             return hit[1]
@@ -1238,14 +1277,9 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         """The fused kernels' parameter block (rnnl_predictor_params), cached
         while node_w and every source tensor keep their storage and version
         (a per-batch forward then builds nothing)."""
-        rte, sm = self.rule_to_entity, self.score_model
-        srcs = [rte.add_model.layers[0].weight, rte.add_model.layers[0].bias, rte.layer_norm.weight,
-                rte.layer_norm.bias, sm.layers[0].weight, sm.layers[0].bias, sm.layers[1].weight,
-                sm.layers[1].bias, self.relation_emb.weight]
-        if self.entity_feature == "bias":
-            srcs.append(self.bias)
-        key = (node_w.data_ptr(), self.aggregator, self.entity_feature,
-               tuple((t.data_ptr(), t._version) for t in srcs))
+        srcs = self._source_lists()[1]
+        key = (node_w.data_ptr(), self.aggregator, self.entity_feature, tuple([t.data_ptr() for t in srcs]),
+               tuple([t._version for t in srcs]))
         hit = self._side.get(("params", self._device_index(device)))
         if hit is not None and hit[0] == key:
             return hit[1], hit[2]

@@ -337,8 +337,12 @@ def test_lstm_encoder_matches_torch(data, dev):
     with torch.no_grad():
         want = model.encode_rules(model.rule_features.to(dev))
         got = model._encode_rules_hip(dev)
+        model.encoder_trie = False
+        per_rule = model._encode_rules_hip(dev)
     err = float((got - want).abs().max())
     assert err <= 2e-6, err
+    # the trie form (one step per prefix) is bitwise the per-rule encoder
+    assert torch.equal(got, per_rule)
 
 
 @pytest.mark.parametrize("data", ["FB15k-237", "umls"])
