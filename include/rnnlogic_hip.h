@@ -126,12 +126,13 @@ int rnnl_lstm_encode(const float *vocab, const float *w_ih, const float *w_hh, c
  * rnnl_rules_create, token order [head, body...]): one LSTM step per trie
  * node (prefixes shared by many rules are computed once), one launch per
  * depth.  out: the same n_rules x 16 rows as rnnl_lstm_encode of those
- * rules, bitwise.  scratch: rnnl_lstm_encode_trie_scratch bytes (the
- * per-node states). */
+ * rules, bitwise.  The weights come as arrays of `layers` pointers (as for
+ * rnnl_lstm_train_forward below: torch's per-layer parameters in place).
+ * scratch: rnnl_lstm_encode_trie_scratch bytes (the per-node states). */
 int rnnl_lstm_encode_trie_scratch(rnnl_rules r, int32_t layers, size_t *bytes);
-int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *w_ih, const float *w_hh, const float *b_ih,
-                          const float *b_hh, int32_t layers, int32_t hidden, float *out, int32_t ld_out,
-                          void *scratch, size_t scratch_bytes, void *stream);
+int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                          const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                          float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, void *stream);
 
 /* The rule encoder under autograd (training; predictors.py:201-208 and
  * torch.nn.LSTM's backward): the rules ridx[0..n) (int64 rows of `tokens`).

@@ -134,20 +134,23 @@ __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restric
 // rule ending there.
 constexpr int TK = 4;
 
-__global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__restrict__ vocab,
-                                                              const float *__restrict__ w_ih,
-                                                              const float *__restrict__ w_hh,
-                                                              const float *__restrict__ b_ih,
-                                                              const float *__restrict__ b_hh, RulesDev rl,
-                                                              int lv0, int n_level, int layers,
+// per-layer parameter pointers (torch's weight_ih_l{k} ... used in place)
+struct LstmLayerPtrs {
+  const float *w_ih[LMAXL], *w_hh[LMAXL], *b_ih[LMAXL], *b_hh[LMAXL];
+};
+
+
+__global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__restrict__ vocab, LstmLayerPtrs P,
+                                                              RulesDev rl, int lv0, int n_level, int layers,
                                                               float *__restrict__ state, float *__restrict__ out,
                                                               int ld_out) {
   __shared__ LstmLds S;
   for (int i = threadIdx.x; i < layers * LG * 2 * LH; i += blockDim.x) {
     const int l = i / (LG * 2 * LH), g = (i / (2 * LH)) % LG, k = i % (2 * LH);
-    S.w[l][g][k] = k < LH ? w_ih[(l * LG + g) * LH + k] : w_hh[(l * LG + g) * LH + (k - LH)];
+    S.w[l][g][k] = k < LH ? P.w_ih[l][g * LH + k] : P.w_hh[l][g * LH + (k - LH)];
   }
-  for (int i = threadIdx.x; i < layers * LG; i += blockDim.x) S.b[i / LG][i % LG] = b_ih[i] + b_hh[i];
+  for (int i = threadIdx.x; i < layers * LG; i += blockDim.x)
+    S.b[i / LG][i % LG] = P.b_ih[i / LG][i % LG] + P.b_hh[i / LG][i % LG];
   __syncthreads();
   const int j = threadIdx.x & (LH - 1);
   const int64_t n_groups = ((int64_t)n_level + TK - 1) / TK;
@@ -207,10 +210,6 @@ __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__res
 // The weight gradients are then dW_l = da_l^T xh_l and db_l = sum of da_l's
 // rows (a batched GEMM over the n T rows, host side), the vocab gradient a
 // per-token sum of dvx rows (vocab_grad_kernel).
-
-struct LstmLayerPtrs {
-  const float *w_ih[LMAXL], *w_hh[LMAXL], *b_ih[LMAXL], *b_hh[LMAXL];
-};
 
 __global__ __launch_bounds__(256) void lstm_train_fwd_kernel(const float *__restrict__ vocab, LstmLayerPtrs P,
                                                              const int32_t *__restrict__ tokens, int T, int pad,
@@ -419,12 +418,21 @@ int rnnl_lstm_encode_trie_scratch(rnnl_rules r, int32_t layers, size_t *bytes) {
   return RNNL_OK;
 }
 
-int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *w_ih, const float *w_hh, const float *b_ih,
-                          const float *b_hh, int32_t layers, int32_t hidden, float *out, int32_t ld_out,
-                          void *scratch, size_t scratch_bytes, void *stream) {
+int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                          const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                          float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, void *stream) {
   size_t need = 0;
-  if (!r || !vocab || !w_ih || !w_hh || !b_ih || !b_hh || !out || hidden != LH || ld_out < LH ||
-      rnnl_lstm_encode_trie_scratch(r, layers, &need) != RNNL_OK || !scratch || scratch_bytes < need) {
+  LstmLayerPtrs P{};
+  bool ok = r && vocab && w_ih && w_hh && b_ih && b_hh && out && hidden == LH && ld_out >= LH &&
+            rnnl_lstm_encode_trie_scratch(r, layers, &need) == RNNL_OK && scratch && scratch_bytes >= need;
+  for (int l = 0; ok && l < layers; ++l) {
+    ok = w_ih[l] && w_hh[l] && b_ih[l] && b_hh[l];
+    P.w_ih[l] = w_ih[l];
+    P.w_hh[l] = w_hh[l];
+    P.b_ih[l] = b_ih[l];
+    P.b_hh[l] = b_hh[l];
+  }
+  if (!ok) {
     set_error("rnnl_lstm_encode_trie: bad arguments (hidden 16, 1 <= layers <= 3, scratch: "
               "rnnl_lstm_encode_trie_scratch)");
     return RNNL_ERR_INVALID;
@@ -434,8 +442,8 @@ int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *w_ih, c
     if (n <= 0) continue;
     const int64_t lanes = ((int64_t)n + TK - 1) / TK * LH;
     const unsigned blocks = (unsigned)std::min<int64_t>((lanes + 255) / 256, 256 * LSTM_BLOCKS_PER_CU);
-    hipLaunchKernelGGL(lstm_trie_level_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, w_ih, w_hh,
-                       b_ih, b_hh, r->d, lv0, n, layers, static_cast<float *>(scratch), out, ld_out);
+    hipLaunchKernelGGL(lstm_trie_level_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, P, r->d, lv0,
+                       n, layers, static_cast<float *>(scratch), out, ld_out);
   }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;

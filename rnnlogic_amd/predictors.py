@@ -1196,13 +1196,16 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
     def _encode_rules_hip(self, device):
         L = self.num_layers
         rnn = self.rnn
-        cat = lambda name: torch.stack([getattr(rnn, "%s_l%d" % (name, k)).detach().float()  # noqa: E731
-                                        for k in range(L)]).contiguous()
-        w_ih, w_hh, b_ih, b_hh = cat("weight_ih"), cat("weight_hh"), cat("bias_ih"), cat("bias_hh")
         vocab = self.vocab_emb.weight.detach().float().contiguous()
         out = torch.empty((self.num_rules, self.hidden_dim), dtype=torch.float32, device=device)
         stream = torch.cuda.current_stream(device).cuda_stream
         if self.encoder_trie:
+            # torch's per-layer parameters in place (no stacked copies)
+            ps = []
+            for k in range(L):
+                ps += [getattr(rnn, "%s_l%d" % (n, k)).detach().float().contiguous()
+                       for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+            arrs = _LstmRules._ptrs(ps, L)
             # one step per rule-trie node: prefixes shared by many rules run once
             nr = self.native_rules(device)
             key = ("trie_state", self._device_index(device))
@@ -1211,10 +1214,12 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 n = ctypes.c_size_t()
                 _native.call("rnnl_lstm_encode_trie_scratch", nr.ptr, L, ctypes.byref(n))
                 st = self._side[key] = torch.empty(n.value, dtype=torch.uint8, device=device)
-            _native.call("rnnl_lstm_encode_trie", nr.ptr, vocab.data_ptr(), w_ih.data_ptr(), w_hh.data_ptr(),
-                         b_ih.data_ptr(), b_hh.data_ptr(), L, self.hidden_dim, out.data_ptr(), out.stride(0),
-                         st.data_ptr(), st.numel(), stream)
+            _native.call("rnnl_lstm_encode_trie", nr.ptr, vocab.data_ptr(), *arrs, L, self.hidden_dim, out.data_ptr(),
+                         out.stride(0), st.data_ptr(), st.numel(), stream)
             return out
+        cat = lambda name: torch.stack([getattr(rnn, "%s_l%d" % (name, k)).detach().float()  # noqa: E731
+                                        for k in range(L)]).contiguous()
+        w_ih, w_hh, b_ih, b_hh = cat("weight_ih"), cat("weight_hh"), cat("bias_ih"), cat("bias_hh")
         # rule tokens depend only on the rule set: cached across invalidate_cache()
         # (a pageable host->device copy per forward costs 1-20 ms depending on the host)
         key = self._device_index(device)
