@@ -435,6 +435,25 @@ def train_step_line(model, solver, dev, n_steps=10, warmup=2):
                     "Adam): forward + loss + backward + step, each step synchronised"}
 
 
+def recorded_em_full(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                        "r05_em_full_fb.json")):
+    """Config 5 end to end (tools/em_full_fb.py: the whole run_rnnlogic.py flow
+    with config/FB15k-237.yaml's settings, 5 EM + 5 final iterations) — a
+    recorded run (~170 s on one MI355X, too long for the default bench), read
+    from profiles/, with the final PredictorPlus stage per batch."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ph = d.get("phases_s", {})
+    n_batches = 17258 * d.get("final_iters", 5)  # FB15k-237 train batches per final iteration
+    return {"s": d.get("wall_s"), "phases_s": ph,
+            "final_train_ms_per_batch": round(ph.get("final_train", 0.0) * 1e3 / n_batches, 3),
+            "best_valid_mrr": d.get("best_valid_mrr"), "source": os.path.relpath(path, os.path.dirname(path) + "/.."),
+            "note": "recorded run of tools/em_full_fb.py (not re-run by bench.py); " + d.get("workload", "")}
+
+
 def em_iteration_line(dev, pre_epochs=200):
     """One EM iteration of run_rnnlogic.py (src/run_rnnlogic.py:61-91) with
     config/FB15k-237.yaml's settings on FB15k-237 (BASELINE.json config 5):
@@ -789,6 +808,7 @@ def main():
         del solver
         # config 5: one EM iteration of run_rnnlogic.py on FB15k-237
         extra["em_iteration"] = em_iteration_line(dev)
+        extra["em_full_fb"] = recorded_em_full()
 
     if rank != 0:
         if distributed:
