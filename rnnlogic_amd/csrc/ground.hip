@@ -721,6 +721,16 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
   __shared__ int s_off[CHB + 1];  // the block's rows' exclusive chunk prefix
   __shared__ long long s_pb[CHB / 64], s_pt[CHB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // the scoring pass's launch state, cleared here rather than by two
+  // dispatches of their own (each one waits for a slot beside RotatE): its
+  // chunk dequeue counter and, when it uses one, the pair-memo table
+  if (blockIdx.x == 0 && tid == 0) reinterpret_cast<unsigned int *>(p.ws)[H_DEQUEUE2] = 0u;
+  if (p.ptab) {
+    const int64_t words = (int64_t)1 << (p.psbits - 1);  // 16-B words of the 2^psbits 8-B slots
+    uint4 *t = reinterpret_cast<uint4 *>(p.ptab);
+    for (int64_t i = (int64_t)blockIdx.x * CHB + tid; i < words; i += (int64_t)gridDim.x * CHB)
+      t[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   // this block's prefix and the list total from the per-block totals (one
   // block, bsum == nullptr: the total is this block's own sum, below)
   long long pb = 0, pt = 0;
@@ -1211,8 +1221,7 @@ int rnnl_predictorplus_score(rnnl_graph g, rnnl_rules r, const rnnl_predictor_pa
   set_score_params(p, pp, score, mask, digest);
   p.atomic_out = deferred == 2;
   hipStream_t st = (hipStream_t)stream;
-  RNNL_HIP_CHECK(hipMemsetAsync(p.ws + 4 * H_DEQUEUE2, 0, 4, st));  // the scoring dequeue counter
-  launch_score(p, r->d, st, workgroups);
+  launch_score(p, r->d, st, workgroups);  // (its chunk-list kernel resets the scoring dequeue counter)
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
@@ -1477,20 +1486,22 @@ static int forward_rotate_enqueue(HostSide *h, rnnl_graph g, rnnl_rules r, const
   if (int rc = rnnl_predictorplus_ground(g, r, pp->aggregator, all_h, all_r, etr, nq, n_cand, ws, ws_bytes, scale,
                                          ground_wg, h->a))
     return rc;
-  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->zero, 0));
-  if (int rc = rnnl_predictorplus_score(g, r, pp, all_h, all_r, nq, score, nullptr, n_cand, digest, ws, ws_bytes,
-                                        scale, score_wg, 2, h->a))
-    return rc;
+  // RotatE next, so that it starts while the scoring chain is still being
+  // enqueued (that chain waits for the grounding on stream A anyway)
   RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->zero, 0));
-  if (mask) {  // the all-True mask on side stream B beside RotatE (not behind it on `stream`)
-    RNNL_HIP_CHECK(hipMemsetAsync(mask, 1, (size_t)nq * (size_t)E, h->b));
-    RNNL_HIP_CHECK(hipEventRecord(h->mask, h->b));
-  }
   if (int rc = rnnl_rotate_score_pieces(rot->eemb, rot->etab, rot->rtab, rot->dim, rot->gamma, all_h, all_r, nq, E,
                                         score, 2, rot->mode, rot->workspace, rot->workspace_bytes, rot->pieces,
                                         rot->first_share, main))
     return rc;
   RNNL_HIP_CHECK(mark(1));
+  if (mask) {  // the all-True mask on side stream B beside RotatE (not behind it on `stream`)
+    RNNL_HIP_CHECK(hipMemsetAsync(mask, 1, (size_t)nq * (size_t)E, h->b));
+    RNNL_HIP_CHECK(hipEventRecord(h->mask, h->b));
+  }
+  RNNL_HIP_CHECK(hipStreamWaitEvent(h->a, h->zero, 0));
+  if (int rc = rnnl_predictorplus_score(g, r, pp, all_h, all_r, nq, score, nullptr, n_cand, digest, ws, ws_bytes,
+                                        scale, score_wg, 2, h->a))
+    return rc;
   RNNL_HIP_CHECK(hipEventRecord(h->side, h->a));
   RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->side, 0));
   if (mask) RNNL_HIP_CHECK(hipStreamWaitEvent(main, h->mask, 0));

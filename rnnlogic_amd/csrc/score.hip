@@ -1138,6 +1138,11 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
     hipLaunchKernelGGL(pack_weights_kernel, dim3((W_FLOATS + 255) / 256), dim3(256), 0, st, p, Wp);
     W = Wp;
   }
+  // the pair memo (SUM; not with the test digest, which needs every
+  // candidate's entries); a key needs >= 2 count bits per entry.  Its table
+  // is zeroed by the chunk-list kernel.
+  const bool pair = p.agg == RNNL_AGG_SUM && !p.digest && g_pair_memo && p.pbc >= 2;
+  p.ptab = pair ? p.ptab_region : nullptr;
   launch_chunk_list(p, st);
   if (p.digest) (void)hipMemsetAsync(p.digest, 0, sizeof(uint64_t) * (size_t)nq, st);  // sums over chunks
   const unsigned cgrid = (unsigned)(grid > 0 ? grid : NUM_CU * SCORE_WG_PER_CU);
@@ -1145,9 +1150,6 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
     hipLaunchKernelGGL(score_pna_chunk_kernel, dim3(cgrid), dim3(BS), 0, st, p, W);
     return;
   }
-  // the pair memo (not with the test digest, which needs every candidate's
-  // entries); a key needs >= 2 count bits per entry
-  const bool pair = !p.digest && g_pair_memo && p.pbc >= 2;
   // few rows (e.g. one reference batch per call) with the pair memo on: no
   // memo pass (one workgroup per relation, on the call's critical path); the
   // single-path candidates take pair-memo keys instead — the same outputs
@@ -1156,10 +1158,6 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
     p.memo = nullptr;
   else
     hipLaunchKernelGGL(memo_sum_kernel, dim3((unsigned)std::max(p.g.R, 1)), dim3(BS), 0, st, p, W);
-  if (pair) {
-    p.ptab = p.ptab_region;
-    (void)hipMemsetAsync(p.ptab, 0, 8ull << p.psbits, st);
-  }
   // one reference batch per call: the wave-cooperative walk of long entry lists
   // (bit-identical features); large launches keep the per-lane walk
   if (p.digest && small)

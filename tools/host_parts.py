@@ -1,0 +1,47 @@
+"""Host time of the pieces of one per-batch PredictorPlus.forward call (the
+reference call pattern, tools/per_batch_forward.py's model) — each piece
+timed alone over many calls with the caches warm (diagnostic; GPU box)."""
+import contextlib
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+dev = torch.device("cuda:0")
+with contextlib.redirect_stdout(sys.stderr):
+    graph, test_set, model, rows = bench.build_workload("RotatE")
+model = model.to(dev).eval()
+b = test_set.batches[100]
+h = torch.tensor([x[0] for x in b], device=dev)
+r = torch.tensor([x[1] for x in b], device=dev)
+N = 2000
+
+
+def t(name, fn):
+    with torch.no_grad():
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(N):
+            fn()
+        el = time.perf_counter() - t0
+        torch.cuda.synchronize()
+    print("%-40s %8.2f us per call" % (name, el / N * 1e6))
+
+
+with torch.no_grad():
+    model(h, r, None)
+nw = model.node_weights(dev)
+t("forward (whole call, GPU-synchronised)", lambda: model(h, r, None))
+t("node_weights (cache hit)", lambda: model.node_weights(dev))
+t("_params (cache hit)", lambda: model._params(dev, nw))
+t("RotatE.native_args", lambda: model.RotatE.native_args(h.numel(), 1, 0.0))
+t("torch.empty (32 x |E|) f32", lambda: torch.empty((32, model.num_entities), device=dev))
+t("_needs_grad", lambda: model._needs_grad())
+t("graph.device_graph + native_rules", lambda: (model.graph.device_graph(dev), model.native_rules(dev)))
+t("torch.cuda.current_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)

@@ -42,3 +42,10 @@ print("calls %d: period %.1f us, kernel span %.1f us, busy %.1f us" % (
     n, period / 1e3, sum(spans) / n / 1e3, sum(busy) / n / 1e3))
 for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
     print("  %-45s n/call %.2f  mean %.1f us" % (k[-45:], len(v) / n, sum(v) / len(v) / 1e3))
+# two consecutive calls, kernel by kernel (offsets in us from the first's rotate_hr start)
+if len(starts) > 12:
+    a, b = starts[10], starts[12]
+    t0 = rows[a][0]
+    print("two calls (offsets in us from rotate_hr start):")
+    for r in rows[a - 8:b - 8]:
+        print("  %9.1f %9.1f  %s" % ((r[0] - t0) / 1e3, (r[1] - t0) / 1e3, r[2][-60:]))

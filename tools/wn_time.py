@@ -1,0 +1,23 @@
+"""WN18RR (config 3) forward step time, as bench.py's wn18rr_forward times it
+(diagnostic; GPU box; A/B builds through tools/ab_run.py)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+dev = torch.device("cuda:0")
+model, h, r = bench.wn18rr_model(dev)
+
+
+def step():
+    model.invalidate_cache()
+    with torch.no_grad():
+        return model.forward_rows(h, r, None)
+
+
+ms = [bench.time_forward(step, 10) * 1e3 for _ in range(3)]
+print("%s WN18RR step %s ms" % (os.path.basename(__import__("rnnlogic_amd._native")._native.LIB_PATH),
+                                " / ".join("%.3f" % x for x in ms)))
