@@ -716,7 +716,8 @@ __global__ __launch_bounds__(CHB) void chunk_sum_kernel(KParams p, int *__restri
   }
 }
 
-__global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *__restrict__ bsum) {
+// Blocks past nrb (the row blocks) only clear the pair-memo table.
+__global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *__restrict__ bsum, int nrb) {
   __shared__ int s_ws[CHB / 64];
   __shared__ int s_off[CHB + 1];  // the block's rows' exclusive chunk prefix
   __shared__ long long s_pb[CHB / 64], s_pt[CHB / 64];
@@ -731,10 +732,11 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
     for (int64_t i = (int64_t)blockIdx.x * CHB + tid; i < words; i += (int64_t)gridDim.x * CHB)
       t[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  if ((int)blockIdx.x >= nrb) return;  // block-uniform, before any barrier
   // this block's prefix and the list total from the per-block totals (one
   // block, bsum == nullptr: the total is this block's own sum, below)
   long long pb = 0, pt = 0;
-  for (int k = tid; bsum && k < (int)gridDim.x; k += CHB) {
+  for (int k = tid; bsum && k < nrb; k += CHB) {
     const int v = bsum[k];
     pt += v;
     if (k < (int)blockIdx.x) pb += v;
@@ -796,13 +798,15 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
 
 void launch_chunk_list(const KParams &p, hipStream_t st) {
   const unsigned nb = (unsigned)((p.nq + CHB - 1) / CHB);
-  if (nb == 1) {  // one block (<= 256 rows, e.g. a reference batch per call): one launch
-    hipLaunchKernelGGL(chunk_fill_kernel, dim3(1), dim3(CHB), 0, st, p, (const int *)nullptr);
+  // extra blocks for the pair-memo table (2^psbits 8-B slots): ~64 KB each
+  const unsigned zb = p.ptab ? (unsigned)std::min<int64_t>(64, ((8ll << p.psbits) >> 16) + 1) : 0u;
+  if (nb == 1) {  // one row block (<= 256 rows, e.g. a reference batch per call): one launch
+    hipLaunchKernelGGL(chunk_fill_kernel, dim3(1 + zb), dim3(CHB), 0, st, p, (const int *)nullptr, 1);
     return;
   }
   int *bsum = reinterpret_cast<int *>(p.chunks + p.chunk_cap);  // nb ints after the list (layout)
   hipLaunchKernelGGL(chunk_sum_kernel, dim3(nb), dim3(CHB), 0, st, p, bsum);
-  hipLaunchKernelGGL(chunk_fill_kernel, dim3(nb), dim3(CHB), 0, st, p, (const int *)bsum);
+  hipLaunchKernelGGL(chunk_fill_kernel, dim3(nb + zb), dim3(CHB), 0, st, p, (const int *)bsum, (int)nb);
 }
 
 // ---------------------------------------------------------------- node weights
