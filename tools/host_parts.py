@@ -45,3 +45,29 @@ t("torch.empty (32 x |E|) f32", lambda: torch.empty((32, model.num_entities), de
 t("_needs_grad", lambda: model._needs_grad())
 t("graph.device_graph + native_rules", lambda: (model.graph.device_graph(dev), model.native_rules(dev)))
 t("torch.cuda.current_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)
+
+
+def recompute():
+    model.invalidate_cache()
+    w = model.node_weights(dev)
+    return model._params(dev, w)
+
+
+t("invalidate + node_weights + _params", recompute)
+t("_encode_rules_hip", lambda: model._encode_rules_hip(dev))
+big_h = torch.cat([torch.tensor([x[0] for x in bb], device=dev) for bb in test_set.batches[:200]])
+big_r = torch.cat([torch.tensor([x[1] for x in bb], device=dev) for bb in test_set.batches[:200]])
+
+
+def step():
+    model.invalidate_cache()
+    return model.forward_rows(big_h, big_r, None)
+
+
+ev = {}
+with torch.no_grad():
+    for _ in range(3):
+        model.invalidate_cache()
+        model.forward_rows(big_h, big_r, None, events=ev)
+torch.cuda.synchronize()
+print("events start->base (the step's head on the GPU timeline): %.3f ms" % ev["start"].elapsed_time(ev["base"]))
