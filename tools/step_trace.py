@@ -3,7 +3,9 @@
 step); per step the period (rotate_hr start to the next one's), the RotatE
 pass, the span from the step's first kernel to its last, the idle time
 (period minus the union of kernel intervals) and where the idle sits (before
-RotatE starts / after it ends).  Usage: python tools/step_trace.py DIR"""
+RotatE starts / after it ends).  Usage: python tools/step_trace.py DIR
+[SPLIT_KERNEL [EVERY]] — split at every EVERY-th launch of another kernel
+(e.g. lstm_trie_level_kernel 4 for a step without RotatE)."""
 import collections
 import csv
 import glob
@@ -15,7 +17,9 @@ for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]))
 rows.sort()
-hr = [i for i, r in enumerate(rows) if "rotate_hr_kernel" in r[2]]
+split = sys.argv[2] if len(sys.argv) > 2 else "rotate_hr_kernel"
+every = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+hr = [i for i, r in enumerate(rows) if split in r[2]][::every]
 rot = [i for i, r in enumerate(rows) if "rotate_direct_kernel" in r[2] or "rotate_mfma_kernel" in r[2]]
 
 
