@@ -293,10 +293,10 @@ __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
 // its buckets at pool indices qbase + beg + [0, end - beg).  degree_only (PNA
 // sweep 1) accumulates sum log(degree) instead.  Returns nc.
 template <int G>
-__device__ int window_pass(const KParams &p, SmemT<G> &S, const Slot &sl, int lo, int beg, int end, int64_t cbase,
+__device__ int window_pass(const KParams &p, SmemT<G> &S, const Ent *w, int lo, int beg, int end, int64_t cbase,
                            bool degree_only) {
+  // w: contributions (entity | node key, count), window-sorted or (one window) raw
   const int tid = threadIdx.x;
-  const Ent *w = sl.f(0);  // window-sorted contributions: a = entity, b = node, c = count
   if (p.prof && tid == 0) S.tp[7] = __builtin_amdgcn_s_memtime();
   for (int i = tid; i < WIN; i += G) S.u.b.map[i] = 0;
   __syncthreads();
@@ -513,6 +513,9 @@ __device__ int candidates_phase(const KParams &p, SmemT<G> &S, const Slot &sl, i
   // bound the hash load) — one read of the raw list instead of a sorted copy
   if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only, 0, p.g.E) : 0;
   const int nwin = (p.g.E + WIN - 1) >> WBITS;
+  // a graph of at most one window (kinship, UMLS): the dense pass over the
+  // raw list, without the window-sorted copy
+  if (nwin == 1) return window_pass(p, S, sl.ct, 0, 0, P, S.qbase, degree_only);
   if (!sorted) {
     for (int i = tid; i < nwin; i += G) S.whist[i] = 0;
     __syncthreads();
@@ -543,7 +546,7 @@ __device__ int candidates_phase(const KParams &p, SmemT<G> &S, const Slot &sl, i
   for (int w = 0; w < nwin;) {
     const int beg = S.wbeg[w];
     if (S.wbeg[w + 1] - beg > HB_LOAD) {
-      ncand += window_pass(p, S, sl, w << WBITS, beg, S.wbeg[w + 1], S.qbase + ncand, degree_only);
+      ncand += window_pass(p, S, sl.f(0), w << WBITS, beg, S.wbeg[w + 1], S.qbase + ncand, degree_only);
       ++w;
       continue;
     }
