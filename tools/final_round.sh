@@ -4,7 +4,13 @@
 # (tools/profile_round.sh) and the per-kernel VALU counts (tools/pmc_valu.sh).
 # Usage (GPU box, repo root): COMMIT=<id> bash tools/final_round.sh rNN
 set -o pipefail
-tag=${1:-r04}
+tag=${1:-r05}
+mkdir -p gpurun_out/$tag
+# the library rebuilt from source on the box (build() as the driver runs it), logged
+( set -x; rm -rf rnnlogic_amd/_build oracle/_build; hipcc --version | head -2; \
+  timeout -k 10 900 python -u -c "import time, __graft_entry__ as g; t = time.time(); g.build(); print('build() %.1f s' % (time.time() - t))"; \
+  ls -la rnnlogic_amd/_build/librnnlogic_hip.so ) > gpurun_out/$tag/build_on_box.log 2>&1 || { tail -20 gpurun_out/$tag/build_on_box.log; exit 1; }
+tail -2 gpurun_out/$tag/build_on_box.log
 bash tools/gpu_check.sh $tag || exit 1
 bash tools/profile_round.sh $tag > gpurun_out/prof_$tag.log 2>&1 || { tail -5 gpurun_out/prof_$tag.log; exit 1; }
 tail -2 gpurun_out/prof_$tag.log | cut -c1-200
