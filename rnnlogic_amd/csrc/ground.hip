@@ -719,7 +719,9 @@ __global__ __launch_bounds__(CHB) void chunk_sum_kernel(KParams p, int *__restri
   }
 }
 
-// Blocks past nrb (the row blocks) only clear the pair-memo table.
+// Blocks past nrb (the row blocks) only clear the pair-memo table (when it is
+// small: one launch's rows up to a few hundred; larger tables take a memset).
+constexpr int PTAB_KERNEL_ZERO_BITS = 16;
 __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *__restrict__ bsum, int nrb) {
   __shared__ int s_ws[CHB / 64];
   __shared__ int s_off[CHB + 1];  // the block's rows' exclusive chunk prefix
@@ -729,7 +731,7 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
   // dispatches of their own (each one waits for a slot beside RotatE): its
   // chunk dequeue counter and, when it uses one, the pair-memo table
   if (blockIdx.x == 0 && tid == 0) reinterpret_cast<unsigned int *>(p.ws)[H_DEQUEUE2] = 0u;
-  if (p.ptab) {
+  if (p.ptab && p.psbits <= PTAB_KERNEL_ZERO_BITS) {
     const int64_t words = (int64_t)1 << (p.psbits - 1);  // 16-B words of the 2^psbits 8-B slots
     uint4 *t = reinterpret_cast<uint4 *>(p.ptab);
     for (int64_t i = (int64_t)blockIdx.x * CHB + tid; i < words; i += (int64_t)gridDim.x * CHB)
@@ -801,8 +803,11 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
 
 void launch_chunk_list(const KParams &p, hipStream_t st) {
   const unsigned nb = (unsigned)((p.nq + CHB - 1) / CHB);
-  // extra blocks for the pair-memo table (2^psbits 8-B slots): ~64 KB each
-  const unsigned zb = p.ptab ? (unsigned)std::min<int64_t>(64, ((8ll << p.psbits) >> 16) + 1) : 0u;
+  // extra blocks for a small pair-memo table (2^psbits 8-B slots): ~64 KB
+  // each; a larger table (large launches) is cleared by a memset
+  const bool zk = p.ptab && p.psbits <= PTAB_KERNEL_ZERO_BITS;
+  const unsigned zb = zk ? (unsigned)(((8ll << p.psbits) >> 16) + 1) : 0u;
+  if (p.ptab && !zk) (void)hipMemsetAsync(p.ptab, 0, 8ull << p.psbits, st);
   if (nb == 1) {  // one row block (<= 256 rows, e.g. a reference batch per call): one launch
     hipLaunchKernelGGL(chunk_fill_kernel, dim3(1 + zb), dim3(CHB), 0, st, p, (const int *)nullptr, 1);
     return;
