@@ -724,7 +724,6 @@ __global__ __launch_bounds__(CHB) void chunk_sum_kernel(KParams p, int *__restri
 constexpr int PTAB_KERNEL_ZERO_BITS = 16;
 __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *__restrict__ bsum, int nrb) {
   __shared__ int s_ws[CHB / 64];
-  __shared__ int s_off[CHB + 1];  // the block's rows' exclusive chunk prefix
   __shared__ long long s_pb[CHB / 64], s_pt[CHB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // the scoring pass's launch state, cleared here rather than by two
@@ -783,22 +782,8 @@ __global__ __launch_bounds__(CHB) void chunk_fill_kernel(KParams p, const int *_
       *reinterpret_cast<unsigned long long *>(reinterpret_cast<unsigned int *>(p.ws) + H_CHUNKS) = total;
   }
   __syncthreads();
-  s_off[tid] = s_ws[wid] + v - n;
-  if (tid == CHB - 1) s_off[CHB] = s_ws[wid] + v;
-  __syncthreads();
-  // the block's chunks written by all lanes (a row of 14,541 candidates has
-  // 228 chunks: one lane per row left the heaviest row's stores serial)
-  const long long base = s_pb[0];
-  const int q0 = blockIdx.x * CHB, total_b = s_off[CHB];
-  for (int k = tid; k < total_b; k += CHB) {
-    int lo = 0, hi = CHB - 1;  // the last row whose prefix is <= k
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= k) lo = mid;
-      else hi = mid - 1;
-    }
-    p.chunks[base + k] = make_int2(q0 + lo, (k - s_off[lo]) << 6);
-  }
+  const long long off = s_pb[0] + s_ws[wid] + v - n;
+  for (int k = 0; k < n; ++k) p.chunks[off + k] = make_int2(q, k << 6);
 }
 
 void launch_chunk_list(const KParams &p, hipStream_t st) {
