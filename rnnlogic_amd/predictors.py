@@ -1119,13 +1119,18 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # pass run on a side stream beside the RotatE kernel, both adding into
         # rows zeroed beside the rule encoder
         self.overlap = True
-        # persistent workgroups of the side-stream kernels: one per CU leaves
-        # RotatE its waves (it needs ~6 per SIMD to reach its floor); the
-        # grounding then takes ~18 ms, well inside the RotatE launch
-        # (measured 88.1 vs 91.1 ms/step at full occupancy), and the scoring
-        # pass 256 vs 512 / 768 workgroups 80.6-80.8 vs 81.25 / 81.1-81.7 ms
-        self.overlap_ground_wg = 256
-        self.overlap_score_wg = 256
+        # persistent workgroups of the side-stream kernels: at most one per CU
+        # leaves RotatE its waves (it needs ~6 per SIMD to reach its floor;
+        # 88.1 vs 91.1 ms/step at full occupancy).  Round 5: one per two CUs
+        # (128 / 128) — the chain still ends well inside RotatE, and half of
+        # the CUs keep RotatE's full occupancy: one N = 8 shard (5,261 rows)
+        # 11.04-11.16 vs 11.39-11.79 ms, the full split 81.38-81.63 vs
+        # 82.00-82.27 (96 / 96: 13.0 / 81.4; 64 / 64: the chain outlasts
+        # RotatE, 17.4 / 108 ms; tools/shard_run.py, profiles/r05_overlap_ab.txt)
+        # The PNA scoring pass is the chain's long pole beside RotatE and keeps
+        # one per CU (WN18RR 18.43 vs 20.63 ms at 128).
+        self.overlap_ground_wg = 128
+        self.overlap_score_wg = 128 if aggregator == "sum" else 256
         # pna aggregator: RotatE in two launches (rnnl_rotate_score_pieces;
         # bitwise the same scores).  The PNA scoring pass needs ~230 registers
         # per wave and finds no room beside RotatE's waves (6 x 80 per SIMD)

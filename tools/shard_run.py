@@ -18,6 +18,7 @@ import bench  # noqa: E402
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 rank = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+wgs = [(int(a), int(b)) for a, b in (x.split("/") for x in sys.argv[4:])] or [None]  # ground/score workgroups
 dev = torch.device("cuda:0")
 with contextlib.redirect_stdout(sys.stderr):
     graph, test_set, model, _ = bench.build_workload("RotatE")
@@ -33,11 +34,16 @@ def st():
         return model.forward_rows(sh, sr, None)
 
 
-for _ in range(2):
-    st()
-torch.cuda.synchronize()
-t = time.perf_counter()
-for _ in range(steps):
-    st()
-torch.cuda.synchronize()
-print("N=%d rank %d: %d rows, %.3f ms per step" % (world, rank, len(rows), (time.perf_counter() - t) * 1e3 / steps))
+for wg in wgs:
+    if wg is not None:
+        model.overlap_ground_wg, model.overlap_score_wg = wg
+    for _ in range(2):
+        st()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        st()
+    torch.cuda.synchronize()
+    print("N=%d rank %d: %d rows, %.3f ms per step (ground / score workgroups %d / %d)"
+          % (world, rank, len(rows), (time.perf_counter() - t) * 1e3 / steps, model.overlap_ground_wg,
+             model.overlap_score_wg))
