@@ -1208,8 +1208,10 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             # torch's per-layer parameters in place (no stacked copies)
             ps = []
             for k in range(L):
-                ps += [getattr(rnn, "%s_l%d" % (n, k)).detach().float().contiguous()
-                       for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+                for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+                    t = getattr(rnn, "%s_l%d" % (n, k))
+                    # fp32 contiguous parameters are read in place (no copy, no detach)
+                    ps.append(t if t.dtype == torch.float32 and t.is_contiguous() else t.detach().float().contiguous())
             arrs = _LstmRules._ptrs(ps, L)
             # one step per rule-trie node: prefixes shared by many rules run once
             nr = self.native_rules(device)
@@ -1276,7 +1278,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             if self.aggregator == "sum" else None
         nbytes = ctypes.c_size_t()
         _native.call("rnnl_node_weights_size", nr.ptr, agg, ctypes.byref(nbytes))
-        w = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+        # the previous table's buffer is rewritten in place (every forward that
+        # read it has ended: they end with their status read), so the records'
+        # address — and with it the cached parameter block — stays the same
+        w = hit[1] if hit is not None and hit[1].numel() == nbytes.value else \
+            torch.empty(nbytes.value, dtype=torch.uint8, device=device)
         _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg,
                      add_w.data_ptr() if add_w is not None else None, w.data_ptr(),
                      torch.cuda.current_stream(device).cuda_stream)
