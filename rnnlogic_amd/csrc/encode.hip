@@ -126,13 +126,17 @@ __global__ __launch_bounds__(256) void lstm_encode_kernel(const float *__restric
 // stands for (the root: [head]) has one state, shared by all rules through
 // it: one step per trie node (FB15k-237: 183,810 nodes instead of 473,782
 // rule steps), one launch per depth.  A 16-lane row owns TK nodes of a level
-// and runs them layer by layer, so each layer's gate rows are read from LDS
-// once per TK nodes; the step reads the parent's (h, c) of every layer from
+// (TK_WIDE; one on small levels) and runs them layer by layer, so each
+// layer's gate rows are read from LDS once per TK nodes; the step reads the parent's (h, c) of every layer from
 // `state` [node][layer][h | c][16] and writes the node's.  The arithmetic of
 // a step is lstm_encode_kernel's, on the same inputs: the outputs are
 // bitwise those of rnnl_lstm_encode.  A node's top-layer h goes to every
 // rule ending there.
-constexpr int TK = 4;
+// Levels of fewer than TK1_NODES nodes (kinship's whole trie; the top
+// levels of larger ones) take one node per row instead: the grid is far
+// below the chip there, and a row's TK steps per layer are a serial chain.
+constexpr int TK_WIDE = 4;
+constexpr int TK1_NODES = 8192;  // 4,096 / 32,768 / all levels: no better (kinship 0.60 / 0.60 / 0.60 ms)
 
 // per-layer parameter pointers (torch's weight_ih_l{k} ... used in place)
 struct LstmLayerPtrs {
@@ -140,6 +144,7 @@ struct LstmLayerPtrs {
 };
 
 
+template <int TK>
 __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__restrict__ vocab, LstmLayerPtrs P,
                                                               RulesDev rl, int lv0, int n_level, int layers,
                                                               float *__restrict__ state, float *__restrict__ out,
@@ -165,6 +170,21 @@ __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__res
       par[k] = node[k] >= 0 ? rl.node_parent[node[k]] : -1;
       x[k] = node[k] >= 0 ? vocab[(int64_t)rl.node_tok[node[k]] * LH + j] : 0.f;
     }
+    // the parents' (h, c) of every layer, loaded before this group's first
+    // store: the stores below may alias `state` as far as the compiler knows,
+    // so a load issued after one waits for it — one memory latency per
+    // (node, layer) step instead of one per group
+    static_assert(LMAXL == 3, "the layer select below");
+    float ph[TK][LMAXL], pc[TK][LMAXL];
+#pragma unroll
+    for (int k = 0; k < TK; ++k)
+#pragma unroll
+      for (int l = 0; l < LMAXL; ++l) {
+        const bool ld = par[k] >= 0 && l < layers;
+        const float *ps = state + ((int64_t)(ld ? par[k] : 0) * layers + l) * 2 * LH;
+        ph[k][l] = ld ? ps[j] : 0.f;
+        pc[k][l] = ld ? ps[LH + j] : 0.f;
+      }
 #pragma unroll 1
     for (int l = 0; l < layers; ++l) {
       float w[4][2 * LH], bias[4];
@@ -177,8 +197,8 @@ __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__res
 #pragma unroll
       for (int k = 0; k < TK; ++k) {
         if (node[k] >= 0) {  // uniform over the row
-          const float *ps = state + ((int64_t)par[k] * layers + l) * 2 * LH;
-          const float h = par[k] >= 0 ? ps[j] : 0.f, c0 = par[k] >= 0 ? ps[LH + j] : 0.f;
+          const float h = l == 0 ? ph[k][0] : l == 1 ? ph[k][1] : ph[k][2];
+          const float c0 = l == 0 ? pc[k][0] : l == 1 ? pc[k][1] : pc[k][2];
           float a[4] = {bias[0], bias[1], bias[2], bias[3]};
           gate_terms<0>(w, x[k], h, a);
           const float c = fmaf(sigm(a[1]), c0, sigm(a[0]) * tanhf(a[2]));
@@ -440,10 +460,15 @@ int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *
   for (size_t d = 0; d + 1 < r->level_ptr.size(); ++d) {
     const int lv0 = r->level_ptr[d], n = r->level_ptr[d + 1] - lv0;
     if (n <= 0) continue;
-    const int64_t lanes = ((int64_t)n + TK - 1) / TK * LH;
+    const int tk = n < TK1_NODES ? 1 : TK_WIDE;
+    const int64_t lanes = ((int64_t)n + tk - 1) / tk * LH;
     const unsigned blocks = (unsigned)std::min<int64_t>((lanes + 255) / 256, 256 * LSTM_BLOCKS_PER_CU);
-    hipLaunchKernelGGL(lstm_trie_level_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, P, r->d, lv0,
-                       n, layers, static_cast<float *>(scratch), out, ld_out);
+    if (tk == 1)
+      hipLaunchKernelGGL(lstm_trie_level_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, P, r->d,
+                         lv0, n, layers, static_cast<float *>(scratch), out, ld_out);
+    else
+      hipLaunchKernelGGL(lstm_trie_level_kernel<TK_WIDE>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, P,
+                         r->d, lv0, n, layers, static_cast<float *>(scratch), out, ld_out);
   }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;

@@ -2,7 +2,8 @@
 rocprofv3 --kernel-trace CSV: per call, the span from its first kernel's start
 to its last kernel's end, the busy time (union of kernel intervals) and the
 per-kernel mean durations.  Calls are split at the rotate_hr_kernel launches
-(one per call).  Usage: python tools/per_batch_trace.py DIR"""
+(one per call; or at MARKER, with BACK kernels before it counted in the
+call).  Usage: python tools/per_batch_trace.py DIR [MARKER BACK]"""
 import collections
 import csv
 import glob
@@ -13,11 +14,13 @@ for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]))
 rows.sort()
-starts = [i for i, r in enumerate(rows) if "rotate_hr_kernel" in r[2]]
+marker = sys.argv[2] if len(sys.argv) > 2 else "rotate_hr_kernel"
+back = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+starts = [i for i, r in enumerate(rows) if marker in r[2]]
 spans, busy, gaps = [], [], []
 per = collections.defaultdict(list)
 for a, b in zip(starts[5:-2], starts[6:-1]):
-    call = rows[a - 8:b - 8]  # the kernels before rotate_hr belong to the call too
+    call = rows[a - back:b - back]  # the kernels before rotate_hr belong to the call too
     if not call:
         continue
     s0 = min(c[0] for c in call)
@@ -46,6 +49,6 @@ for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
 if len(starts) > 12:
     a, b = starts[10], starts[12]
     t0 = rows[a][0]
-    print("two calls (offsets in us from rotate_hr start):")
-    for r in rows[a - 8:b - 8]:
+    print("two calls (offsets in us from the marker start):")
+    for r in rows[a - back:b - back]:
         print("  %9.1f %9.1f  %s" % ((r[0] - t0) / 1e3, (r[1] - t0) / 1e3, r[2][-60:]))
