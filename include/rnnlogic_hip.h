@@ -133,6 +133,15 @@ int rnnl_lstm_encode_trie_scratch(rnnl_rules r, int32_t layers, size_t *bytes);
 int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
                           const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
                           float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, void *stream);
+/* rnnl_lstm_encode_trie followed by rnnl_node_weights(r, out, ld_out,
+ * RNNL_AGG_SUM, add_w, node_w) in the same launches: each trie node's SUM
+ * record is formed where its embedding is (the rules ending at a node share
+ * its top-layer h), with node_weights' arithmetic — node_w is bitwise that
+ * call's table. */
+int rnnl_lstm_encode_trie_sum(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                              const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                              float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, const float *add_w,
+                              void *node_w, void *stream);
 
 /* The rule encoder under autograd (training; predictors.py:201-208 and
  * torch.nn.LSTM's backward): the rules ridx[0..n) (int64 rows of `tokens`).

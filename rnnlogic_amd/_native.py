@@ -46,6 +46,8 @@ SIGNATURES = [
      [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _I32, _P]),
     ("rnnl_lstm_encode_trie_scratch", ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_size_t)]),
     ("rnnl_lstm_encode_trie", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _P, ctypes.c_size_t, _P]),
+    ("rnnl_lstm_encode_trie_sum", ctypes.c_int,
+     [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _P, ctypes.c_size_t, _P, _P, _P]),
     ("rnnl_lstm_encode", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _I32, _P]),
     ("rnnl_forward_workspace_size", ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     ("rnnl_predictorplus_forward", ctypes.c_int,

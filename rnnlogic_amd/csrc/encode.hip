@@ -148,7 +148,8 @@ template <int TK>
 __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__restrict__ vocab, LstmLayerPtrs P,
                                                               RulesDev rl, int lv0, int n_level, int layers,
                                                               float *__restrict__ state, float *__restrict__ out,
-                                                              int ld_out) {
+                                                              int ld_out, const float *__restrict__ add_w,
+                                                              unsigned char *__restrict__ rec) {
   __shared__ LstmLds S;
   for (int i = threadIdx.x; i < layers * LG * 2 * LH; i += blockDim.x) {
     const int l = i / (LG * 2 * LH), g = (i / (2 * LH)) % LG, k = i % (2 * LH);
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__res
     S.b[i / LG][i % LG] = P.b_ih[i / LG][i % LG] + P.b_hh[i / LG][i % LG];
   __syncthreads();
   const int j = threadIdx.x & (LH - 1);
+  unsigned int rm = 0, rm2 = 0;  // max |record|, max |node sum| bits (rec)
   const int64_t n_groups = ((int64_t)n_level + TK - 1) / TK;
   for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 < n_groups * LH; g0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t grp = (g0 + threadIdx.x) / LH;  // uniform over the 16-lane row
@@ -212,9 +214,41 @@ __global__ __launch_bounds__(256) void lstm_trie_level_kernel(const float *__res
     }
 #pragma unroll
     for (int k = 0; k < TK; ++k)
-      if (node[k] >= 0)
-        for (int m = rl.node_rule_ptr[node[k]]; m < rl.node_rule_ptr[node[k] + 1]; ++m)
+      if (node[k] >= 0) {  // uniform over the row
+        float s1 = 0.f;
+        for (int m = rl.node_rule_ptr[node[k]]; m < rl.node_rule_ptr[node[k] + 1]; ++m) {
           out[(int64_t)rl.node_rules[m] * ld_out + j] = x[k];
+          s1 += x[k];
+        }
+        if (rec) {  // the SUM record: node_weights_kernel's arithmetic on the rows just written
+          float y = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) y = fmaf(__shfl(s1, i, 16), add_w[j * 16 + i], y);
+          reinterpret_cast<float *>(rec + (int64_t)node[k] * kStrideSum)[j] = y;
+          rm = max(rm, __float_as_uint(fabsf(y)));
+          rm2 = max(rm2, __float_as_uint(fabsf(s1)));
+        }
+      }
+  }
+  if (rec) {  // table maxima into the trailer (node_fix_kernel's shift), as node_weights_kernel
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      rm = max(rm, (unsigned int)__shfl_xor((int)rm, o, 64));
+      rm2 = max(rm2, (unsigned int)__shfl_xor((int)rm2, o, 64));
+    }
+    __shared__ unsigned int s_m[4], s_m2[4];
+    if ((threadIdx.x & 63) == 0) {
+      s_m[threadIdx.x >> 6] = rm;
+      s_m2[threadIdx.x >> 6] = rm2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned int *trailer = reinterpret_cast<unsigned int *>(rec + (int64_t)rl.n_nodes * kStrideSum);
+      rm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+      rm2 = max(max(s_m2[0], s_m2[1]), max(s_m2[2], s_m2[3]));
+      if (rm) atomicMax(trailer, rm);
+      if (rm2) atomicMax(trailer + 3, rm2);
+    }
   }
 }
 
@@ -438,9 +472,10 @@ int rnnl_lstm_encode_trie_scratch(rnnl_rules r, int32_t layers, size_t *bytes) {
   return RNNL_OK;
 }
 
-int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
-                          const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
-                          float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, void *stream) {
+static int encode_trie(const char *who, rnnl_rules r, const float *vocab, const float *const *w_ih,
+                       const float *const *w_hh, const float *const *b_ih, const float *const *b_hh, int32_t layers,
+                       int32_t hidden, float *out, int32_t ld_out, void *scratch, size_t scratch_bytes,
+                       const float *add_w, unsigned char *rec, void *stream) {
   size_t need = 0;
   LstmLayerPtrs P{};
   bool ok = r && vocab && w_ih && w_hh && b_ih && b_hh && out && hidden == LH && ld_out >= LH &&
@@ -453,10 +488,12 @@ int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *
     P.b_hh[l] = b_hh[l];
   }
   if (!ok) {
-    set_error("rnnl_lstm_encode_trie: bad arguments (hidden 16, 1 <= layers <= 3, scratch: "
+    set_error(std::string(who) + ": bad arguments (hidden 16, 1 <= layers <= 3, scratch: "
               "rnnl_lstm_encode_trie_scratch)");
     return RNNL_ERR_INVALID;
   }
+  if (rec)  // the trailer's maxima (node_fix_kernel's shift) start from zero
+    RNNL_HIP_CHECK(hipMemsetAsync(rec + (int64_t)r->d.n_nodes * kStrideSum, 0, 32, (hipStream_t)stream));
   for (size_t d = 0; d + 1 < r->level_ptr.size(); ++d) {
     const int lv0 = r->level_ptr[d], n = r->level_ptr[d + 1] - lv0;
     if (n <= 0) continue;
@@ -465,13 +502,34 @@ int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *
     const unsigned blocks = (unsigned)std::min<int64_t>((lanes + 255) / 256, 256 * LSTM_BLOCKS_PER_CU);
     if (tk == 1)
       hipLaunchKernelGGL(lstm_trie_level_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, P, r->d,
-                         lv0, n, layers, static_cast<float *>(scratch), out, ld_out);
+                         lv0, n, layers, static_cast<float *>(scratch), out, ld_out, add_w, rec);
     else
       hipLaunchKernelGGL(lstm_trie_level_kernel<TK_WIDE>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, vocab, P,
-                         r->d, lv0, n, layers, static_cast<float *>(scratch), out, ld_out);
+                         r->d, lv0, n, layers, static_cast<float *>(scratch), out, ld_out, add_w, rec);
   }
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
+}
+
+int rnnl_lstm_encode_trie(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                          const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                          float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, void *stream) {
+  return encode_trie("rnnl_lstm_encode_trie", r, vocab, w_ih, w_hh, b_ih, b_hh, layers, hidden, out, ld_out, scratch,
+                     scratch_bytes, nullptr, nullptr, stream);
+}
+
+int rnnl_lstm_encode_trie_sum(rnnl_rules r, const float *vocab, const float *const *w_ih, const float *const *w_hh,
+                              const float *const *b_ih, const float *const *b_hh, int32_t layers, int32_t hidden,
+                              float *out, int32_t ld_out, void *scratch, size_t scratch_bytes, const float *add_w,
+                              void *node_w, void *stream) {
+  if (!add_w || !node_w) {
+    set_error("rnnl_lstm_encode_trie_sum: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  if (int rc = encode_trie("rnnl_lstm_encode_trie_sum", r, vocab, w_ih, w_hh, b_ih, b_hh, layers, hidden, out, ld_out,
+                           scratch, scratch_bytes, add_w, static_cast<unsigned char *>(node_w), stream))
+    return rc;
+  return node_fix_enqueue(r, node_w, stream);
 }
 
 static bool lstm_train_args(const float *vocab, const float *const *w_ih, const float *const *w_hh,

@@ -1092,6 +1092,16 @@ KParams export_params(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand
 
 }  // namespace rnnl
 
+int rnnl::node_fix_enqueue(rnnl_rules r, void *node_w, void *stream) {
+  const int64_t n = (int64_t)r->d.n_nodes * 16;
+  if (n == 0) return RNNL_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(node_fix_kernel, dim3((unsigned)std::min<int64_t>((n + bs - 1) / bs, 4096)), dim3(bs), 0,
+                     (hipStream_t)stream, r->d.n_nodes, 0, r->d.n_nodes, static_cast<unsigned char *>(node_w));
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
 using namespace rnnl;
 
 extern "C" {

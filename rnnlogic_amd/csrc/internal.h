@@ -79,6 +79,10 @@ constexpr int kStridePna = 256;  // int32 fix(sum x)[16] | int32 fix(sum x^2)[16
 
 void set_error(const std::string &msg);
 
+// The SUM node records' fixed-point pass (node_fix_kernel, ground.hip) over
+// every node of the table (rnnl_lstm_encode_trie_sum's last launch).
+int node_fix_enqueue(rnnl_rules r, void *node_w, void *stream);
+
 }  // namespace rnnl
 
 struct rnnl_graph_s {

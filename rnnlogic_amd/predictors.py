@@ -1198,7 +1198,9 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             return self._encode_rules_hip(device)
         return self.encode_rules(self.rule_features.to(device))
 
-    def _encode_rules_hip(self, device):
+    def _encode_rules_hip(self, device, add_w=None, node_w=None):
+        """The HIP rule encoder's (num_rules, 16) rows; with add_w and node_w
+        (trie form only) also node_w's SUM records (rnnl_lstm_encode_trie_sum)."""
         L = self.num_layers
         rnn = self.rnn
         vocab = self.vocab_emb.weight.detach().float().contiguous()
@@ -1221,8 +1223,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 n = ctypes.c_size_t()
                 _native.call("rnnl_lstm_encode_trie_scratch", nr.ptr, L, ctypes.byref(n))
                 st = self._side[key] = torch.empty(n.value, dtype=torch.uint8, device=device)
-            _native.call("rnnl_lstm_encode_trie", nr.ptr, vocab.data_ptr(), *arrs, L, self.hidden_dim, out.data_ptr(),
-                         out.stride(0), st.data_ptr(), st.numel(), stream)
+            if node_w is not None:
+                _native.call("rnnl_lstm_encode_trie_sum", nr.ptr, vocab.data_ptr(), *arrs, L, self.hidden_dim,
+                             out.data_ptr(), out.stride(0), st.data_ptr(), st.numel(), add_w.data_ptr(),
+                             node_w.data_ptr(), stream)
+            else:
+                _native.call("rnnl_lstm_encode_trie", nr.ptr, vocab.data_ptr(), *arrs, L, self.hidden_dim,
+                             out.data_ptr(), out.stride(0), st.data_ptr(), st.numel(), stream)
             return out
         cat = lambda name: torch.stack([getattr(rnn, "%s_l%d" % (name, k)).detach().float()  # noqa: E731
                                         for k in range(L)]).contiguous()
@@ -1271,8 +1278,6 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         hit = self._node_cache.get(device)
         if hit is not None and hit[0] == key:
             return hit[1]
-        with torch.no_grad():
-            emb = self.all_rule_embeddings().detach().float().contiguous()
         agg = _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA
         add_w = self.rule_to_entity.add_model.layers[0].weight.detach().float().contiguous() \
             if self.aggregator == "sum" else None
@@ -1283,9 +1288,16 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # address — and with it the cached parameter block — stays the same
         w = hit[1] if hit is not None and hit[1].numel() == nbytes.value else \
             torch.empty(nbytes.value, dtype=torch.uint8, device=device)
-        _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg,
-                     add_w.data_ptr() if add_w is not None else None, w.data_ptr(),
-                     torch.cuda.current_stream(device).cuda_stream)
+        with torch.no_grad():
+            if (self.type == "lstm" and self.aggregator == "sum" and self.encoder_trie and device.type == "cuda"
+                    and not self._needs_grad()):
+                # the SUM records formed by the trie encoder's launches (rnnl_lstm_encode_trie_sum)
+                emb = self._encode_rules_hip(device, add_w, w)
+            else:
+                emb = self.all_rule_embeddings().detach().float().contiguous()
+                _native.call("rnnl_node_weights", nr.ptr, emb.data_ptr(), emb.stride(0), agg,
+                             add_w.data_ptr() if add_w is not None else None, w.data_ptr(),
+                             torch.cuda.current_stream(device).cuda_stream)
         self._node_cache[device] = (key, w, emb, add_w)
         return w
 

@@ -343,6 +343,27 @@ def test_lstm_encoder_matches_torch(data, dev):
     assert err <= 2e-6, err
     # the trie form (one step per prefix) is bitwise the per-rule encoder
     assert torch.equal(got, per_rule)
+    # the SUM node records formed inside the trie encoder's launches
+    # (rnnl_lstm_encode_trie_sum) are bitwise rnnl_node_weights' table of its rows
+    import ctypes
+    from rnnlogic_amd import _native
+    model.encoder_trie = True
+    assert model.aggregator == "sum"
+    nr = model.native_rules(dev)
+    add_w = model.rule_to_entity.add_model.layers[0].weight.detach().float().contiguous()
+    nbytes = ctypes.c_size_t()
+    _native.call("rnnl_node_weights_size", nr.ptr, _native.AGG_SUM, ctypes.byref(nbytes))
+    fused = torch.full((nbytes.value,), 0xAB, dtype=torch.uint8, device=dev)
+    with torch.no_grad():
+        emb = model._encode_rules_hip(dev, add_w, fused)
+    assert torch.equal(emb, got)
+    sep = torch.full_like(fused, 0xCD)
+    _native.call("rnnl_node_weights", nr.ptr, got.data_ptr(), got.stride(0), _native.AGG_SUM, add_w.data_ptr(),
+                 sep.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    n_rec = nbytes.value - 64  # the records; then the trailer's 32 written bytes
+    assert torch.equal(fused[:n_rec + 32], sep[:n_rec + 32])
+    assert torch.equal(model.node_weights(dev)[:n_rec + 32], sep[:n_rec + 32])
 
 
 @pytest.mark.parametrize("data", ["FB15k-237", "umls"])

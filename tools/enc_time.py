@@ -22,6 +22,7 @@ with torch.no_grad():
         res[trie] = bench.time_forward(lambda: model._encode_rules_hip(dev), 20) * 1e3
     got = model._encode_rules_hip(dev)
     want = model.encode_rules(model.rule_features.to(dev))
+    model.encoder_trie = True  # the bench's head: the trie encoder with the SUM records in its launches
     nw = bench.time_forward(lambda: (model.invalidate_cache(), model.node_weights(dev)), 20) * 1e3
 print("encoder: trie %.3f ms, per-rule %.3f ms; encoder + node weights %.3f ms; max |hip - torch| %.2e"
       % (res[True], res[False], nw, (got - want).abs().max().item()))
