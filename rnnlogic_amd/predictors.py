@@ -1131,6 +1131,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # one per CU (WN18RR 18.43 vs 20.63 ms at 128).
         self.overlap_ground_wg = 128
         self.overlap_score_wg = 128 if aggregator == "sum" else 256
+        # the score rows' zero fill: issued before the rule encoder (beside it)
+        # or by the forward call, after the encoder (beside rotate_hr and the
+        # grounding's start).  SUM: by the call — FB15k-237 step 80.5-80.8 ->
+        # 79.4-79.7 ms, N = 8 shard 11.03-11.21 -> 10.97-11.03 (the encoder
+        # runs without the fill's 2.4 GB beside it, the grounding is resident
+        # before RotatE starts); PNA (WN18RR) 18.37-18.43 early vs 18.41-18.47
+        self.zero_early = aggregator != "sum"
         # pna aggregator: RotatE in two launches (rnnl_rotate_score_pieces;
         # bitwise the same scores).  The PNA scoring pass needs ~230 registers
         # per wave and finds no room beside RotatE's waves (6 x 80 per SIMD)
@@ -1416,7 +1423,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         rec("start")
         score = torch.empty((nq, self.num_entities), dtype=torch.float32, device=device)
         overlap = self.entity_feature == "RotatE" and self.overlap and nq >= 2
-        if overlap:  # zero the rows on a side stream beside the rule encoder
+        if overlap and self.zero_early:  # zero the rows on a side stream beside the rule encoder
             _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(),
                          torch.cuda.current_stream(device).cuda_stream)
         node_w = self.node_weights(device)
@@ -1494,7 +1501,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             for e in evs:  # torch creates an event's handle on its first record
                 e.record(main)
             ev = (ctypes.c_void_p * 3)(*[e.cuda_event for e in evs])
-        zeroed = 1
+        zeroed = 1 if self.zero_early else 0
         while True:
             scale = self.capacity_scale
             ws = self._overlap_workspace(device, nq, scale)

@@ -21,9 +21,10 @@ steps = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 wgs = [(int(a), int(b)) for a, b in (x.split("/") for x in sys.argv[4:])] or [None]  # ground/score workgroups
 dev = torch.device("cuda:0")
 with contextlib.redirect_stdout(sys.stderr):
-    graph, test_set, model, _ = bench.build_workload("RotatE")
+    graph, test_set, model, full = bench.build_workload("RotatE")
 model = model.to(dev).eval()
-rows, _ = bench.shard_rows(test_set, world, rank)
+model.zero_early = os.environ.get("ZERO_EARLY", "1") == "1"
+rows = bench.shard_rows(test_set, world, rank)[0] if world > 1 else full  # N = 1: the bench's row order
 sh = torch.from_numpy(np.ascontiguousarray(rows[:, 0])).to(dev)
 sr = torch.from_numpy(np.ascontiguousarray(rows[:, 1])).to(dev)
 
@@ -44,6 +45,6 @@ for wg in wgs:
     for _ in range(steps):
         st()
     torch.cuda.synchronize()
-    print("N=%d rank %d: %d rows, %.3f ms per step (ground / score workgroups %d / %d)"
+    print("N=%d rank %d: %d rows, %.3f ms per step (ground / score workgroups %d / %d, zero_early %d)"
           % (world, rank, len(rows), (time.perf_counter() - t) * 1e3 / steps, model.overlap_ground_wg,
-             model.overlap_score_wg))
+             model.overlap_score_wg, model.zero_early))

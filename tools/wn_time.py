@@ -10,6 +10,7 @@ import bench  # noqa: E402
 
 dev = torch.device("cuda:0")
 model, h, r = bench.wn18rr_model(dev)
+model.zero_early = os.environ.get("ZERO_EARLY", "1") == "1"  # A/B of the zero fill's issue point
 
 
 def step():
