@@ -20,7 +20,8 @@ dev = torch.device("cuda:0")
 with contextlib.redirect_stdout(sys.stderr):
     graph, test_set, model, rows = bench.build_workload(FEATURE)
 model = model.to(dev).eval()
-model.zero_early = os.environ.get("ZERO_EARLY", "1") == "1"  # A/B of the zero fill's issue point
+if "ZERO_EARLY" in os.environ:  # A/B of the zero fill's issue point
+    model.zero_early = os.environ["ZERO_EARLY"] == "1"
 batches = test_set.batches[:N] if N else test_set.batches
 hs = [torch.tensor([x[0] for x in b], device=dev) for b in batches]
 rs = [torch.tensor([x[1] for x in b], device=dev) for b in batches]

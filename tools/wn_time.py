@@ -10,7 +10,8 @@ import bench  # noqa: E402
 
 dev = torch.device("cuda:0")
 model, h, r = bench.wn18rr_model(dev)
-model.zero_early = os.environ.get("ZERO_EARLY", "1") == "1"  # A/B of the zero fill's issue point
+if "ZERO_EARLY" in os.environ:  # A/B of the zero fill's issue point
+    model.zero_early = os.environ["ZERO_EARLY"] == "1"
 
 
 def step():
