@@ -1138,6 +1138,9 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # runs without the fill's 2.4 GB beside it, the grounding is resident
         # before RotatE starts); PNA (WN18RR) 18.37-18.43 early vs 18.41-18.47
         self.zero_early = aggregator != "sum"
+        # without RotatE: the grounding on a side stream beside the rule
+        # encoder (_forward_rows_fused)
+        self.ground_early = True
         # pna aggregator: RotatE in two launches (rnnl_rotate_score_pieces;
         # bitwise the same scores).  The PNA scoring pass needs ~230 registers
         # per wave and finds no room beside RotatE's waves (6 x 80 per SIMD)
@@ -1426,27 +1429,54 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         if overlap and self.zero_early:  # zero the rows on a side stream beside the rule encoder
             _native.call("rnnl_forward_rotate_zero", score.data_ptr(), score.numel(),
                          torch.cuda.current_stream(device).cuda_stream)
+        early = None
+        if not overlap and self.ground_early and events is None and nq >= 2:
+            # the grounding reads no rule weights: on a side stream beside the
+            # rule encoder and node records, the scoring pass on the current
+            # stream after both (the split halves of rnnl_predictorplus_forward)
+            main = torch.cuda.current_stream(device)
+            side = self._ground_stream(device)
+            scale = self.capacity_scale
+            ws = self._workspace(device, nq, scale)
+            n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+            side.wait_stream(main)
+            _native.call("rnnl_predictorplus_ground", g, nr.ptr,
+                         _native.AGG_SUM if self.aggregator == "sum" else _native.AGG_PNA, all_h.data_ptr(),
+                         all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(),
+                         ws.data_ptr(), ws.numel(), scale, 0, side.cuda_stream)
+            early = (side, ws, scale)
         node_w = self.node_weights(device)
         params, keep = self._params(device, node_w)
         stream = torch.cuda.current_stream(device).cuda_stream
         none_mode = params.feature == _native.FEATURE_NONE
-        n_cand = torch.empty(nq, dtype=torch.int32, device=device)
+        if early is None:
+            n_cand = torch.empty(nq, dtype=torch.int32, device=device)
         if overlap:
             mask = self._forward_overlap(device, g, nr, params, all_h, all_r, etr, score, n_cand, digest, events)
             del keep
             return (score, mask, n_cand) if return_ncand else (score, mask)
         while True:
             mask8 = torch.zeros((nq, self.num_entities), dtype=torch.uint8, device=device) if none_mode else None
-            scale = self.capacity_scale
-            ws = self._workspace(device, nq, scale)
-            rec("base")
-            self.base_score(all_h, all_r, score)
-            rec("ground")
-            _native.call("rnnl_predictorplus_forward", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
-                         all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
-                         mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(),
-                         digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
-                         stream)
+            if early is not None:  # the grounding was enqueued beside the encoder: score after it
+                side, ws, scale = early
+                early = None
+                self.base_score(all_h, all_r, score)
+                torch.cuda.current_stream(device).wait_stream(side)
+                _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
+                             all_r.data_ptr(), nq, score.data_ptr(), mask8.data_ptr() if mask8 is not None else None,
+                             n_cand.data_ptr(), digest.data_ptr() if digest is not None else None, ws.data_ptr(),
+                             ws.numel(), scale, 0, 0, stream)
+            else:
+                scale = self.capacity_scale
+                ws = self._workspace(device, nq, scale)
+                rec("base")
+                self.base_score(all_h, all_r, score)
+                rec("ground")
+                _native.call("rnnl_predictorplus_forward", g, nr.ptr, ctypes.byref(params), all_h.data_ptr(),
+                             all_r.data_ptr(), etr.data_ptr() if etr is not None else None, nq, score.data_ptr(),
+                             mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(),
+                             digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
+                             stream)
             rec("end")
             rc = self._status(ws, stream)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
@@ -1461,6 +1491,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         else:
             mask = torch.ones((nq, self.num_entities), dtype=torch.bool, device=device)
         return (score, mask, n_cand) if return_ncand else (score, mask)
+
+    def _ground_stream(self, device):
+        key = ("ground_stream", self._device_index(device))
+        st = self._side.get(key)
+        if st is None:
+            st = self._side[key] = torch.cuda.Stream(device)
+        return st
 
     def _overlap_workspace(self, device, nq, scale):
         sk = ("need", self._device_index(device), nq, scale)
