@@ -10,6 +10,8 @@ import bench  # noqa: E402
 
 dev = torch.device("cuda:0")
 model, h, r = bench.wn18rr_model(dev)
+if "ROTATE_SHARE" in os.environ:  # A/B of the PNA yield point
+    model.rotate_share = float(os.environ["ROTATE_SHARE"])
 if "ZERO_EARLY" in os.environ:  # A/B of the zero fill's issue point
     model.zero_early = os.environ["ZERO_EARLY"] == "1"
 
@@ -21,5 +23,6 @@ def step():
 
 
 ms = [bench.time_forward(step, 10) * 1e3 for _ in range(3)]
-print("%s WN18RR step %s ms" % (os.path.basename(__import__("rnnlogic_amd._native")._native.LIB_PATH),
+print("%s share %.2f zero_early %d: WN18RR step %s ms" % (os.path.basename(__import__("rnnlogic_amd._native")._native.LIB_PATH),
+                                model.rotate_share, model.zero_early,
                                 " / ".join("%.3f" % x for x in ms)))
