@@ -166,6 +166,29 @@ def test_stream_overlap_is_bit_identical(case, dev):
     np.testing.assert_array_equal(outs[0][3].view(np.uint64), want_d)
 
 
+@pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "kinship_lstm_sum_none", "wn_emb_pna_bias"])
+def test_ground_early_is_bit_identical(case, dev):
+    """Without RotatE the grounding runs on a side stream beside the rule
+    encoder (PredictorPlus.ground_early, the split ground / score entries):
+    scores, masks and candidate counts equal the one-call launch's."""
+    fx = Fixture(case)
+    model = build_model(fx, dev)
+    test = np.asarray(graph_for(fx.dataset_path()).test_facts, dtype=np.int64)[:6000]
+    h = torch.from_numpy(test[:, 0]).to(dev)
+    r = torch.from_numpy(test[:, 1]).to(dev)
+    outs = []
+    for early in (False, True):
+        model.ground_early = early
+        model.invalidate_cache()
+        with torch.no_grad():
+            score, mask, n = model.forward_rows(h, r, None, return_ncand=True)
+        torch.cuda.synchronize()
+        outs.append((score.cpu().numpy(), mask.cpu().numpy(), n.cpu().numpy()))
+    model.ground_early = True
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("case", ["fb_lstm_sum_bias", "fb_lstm_sum_rotate", "kinship_lstm_sum_none",
                                   "umls_lstm_sum_bias"])
 def test_pair_memo_is_bit_identical(case, dev):
