@@ -135,6 +135,24 @@ def shard_balance_line(model, test_set, dev, full_ms, worlds=(2, 4, 8), reps=3):
     return out
 
 
+def rank_info(model, dev, local, world, backend):
+    """This rank's placement: LOCAL_RANK, the device it runs on, the device
+    of its graph handle and of the forward's side streams
+    (rnnl_forward_host_info), and the process group's world size."""
+    import ctypes
+    import socket
+    from rnnlogic_amd import _native
+    info = (ctypes.c_int32 * 4)()
+    _native.call("rnnl_forward_host_info", model.graph.device_graph(dev), info)
+    return {"rank": dist.get_rank() if dist.is_initialized() else 0, "local_rank": local,
+            "host": socket.gethostname(), "cuda_device": dev.index,
+            "graph_device": int(info[0]), "side_stream_devices": [int(info[1]), int(info[2])],
+            "devices_with_forward_resources": int(info[3]),
+            "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
+            "world_size_env": world, "backend": dist.get_backend() if dist.is_initialized() else None,
+            "placement_ok": int(info[0]) == dev.index and all(x in (-1, dev.index) for x in info[1:3])}
+
+
 def train_rows(train_set, n_rows):
     """The first train batches (sampler order of trainer.py:51-56 is a
     permutation; batch order does not matter for throughput) up to n_rows:
@@ -637,7 +655,14 @@ def main():
         idx_all = [None] * world
         dist.all_gather_object(idx_all, list(shard))
         flat = [i for part in idx_all for i in part]
+        # per-rank self-check: the rank's device, where its graph handle and the
+        # forward's side streams live, and the world the process group saw
+        me = rank_info(model, dev, local, world, backend)
+        info_all = [None] * world
+        dist.all_gather_object(info_all, me)
         shards = {"batches_per_rank": [len(x) for x in idx_all],
+                  "ranks": info_all,
+                  "devices_distinct": len({(x["host"], x["cuda_device"]) for x in info_all}) == world,
                   "union_is_split": sorted(set(flat)) == list(range(len(test_set))),
                   "padding_batches": len(flat) - len(test_set),
                   "rows_total_with_padding": int(sum(rows_per_rank)), "rows_counted": n_split}
@@ -904,6 +929,7 @@ def main():
                                   model.num_rules, " and RotatE tables" if args.feature == "RotatE" else ""),
                    "batch_size": 32, "parallelism": "dp%d (test batches sharded, KG replicated)" % world,
                    "rows_per_rank": rows_per_rank, "batches_per_rank": len(shard), "shards": shards,
+                   "placement": shards["ranks"] if shards else [rank_info(model, dev, local, world, backend)],
                    "process_group": backend if distributed else None},
         "roofline": dominant,
         "kernels_ms": {"rule_encoder+node_weights": round(nodes_ms, 3), "base_score": round(base_ms, 3),

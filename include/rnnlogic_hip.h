@@ -265,6 +265,11 @@ int rnnl_forward_status_host(const void *header, int64_t *totals);
 #define RNNL_FLAG_MIXED 1
 int rnnl_forward_status_flags(void *workspace, void *stream, int64_t *totals, uint32_t *flags);
 int rnnl_forward_flags_host(const void *header, uint32_t *flags);
+/* Where the calling thread's forward resources for graph g live (a
+ * multi-GPU self-check): out[0] = g's device, out[1] / out[2] = the devices
+ * of the RotatE overlap's side streams for g's device (-1: not created),
+ * out[3] = the number of devices this thread holds forward resources for. */
+int rnnl_forward_host_info(rnnl_graph g, int32_t *out);
 /* Grounding only (reference data.py:136-173 for every rule of every row,
  * predictors.py:221-244): fills the workspace's COO of the stacked rule_count
  * matrix and n_cand (per row candidate count, -1/-2 on overflow/error; check
@@ -301,6 +306,10 @@ int rnnl_debug_clock(void *dev_counters);
  * Affects the sizes computed by later rnnl_forward_workspace_size / launches
  * in this process. */
 int rnnl_debug_capacity(int64_t frontier_base, int64_t contrib_base, int64_t pool_per_query);
+/* Phase B's sort-window width 2^bits entities for launches after the call
+ * (A/B measurements; -1 = the default: the smallest width giving at most
+ * 1024 windows).  Results do not depend on it. */
+int rnnl_debug_sort_bits(int32_t bits);
 /* Test hook: turn the SUM scoring pass's pair memo (score_model outputs
  * reused between candidates with equal bucket entries) off (0) or on (1,
  * the default), so that a test can compare the outputs both ways. */
@@ -334,7 +343,10 @@ int rnnl_debug_pair_memo(int32_t on);
  * rnnl_predictor_backward: after rnnl_predictor_forward on the same
  * workspace, the gradient of the scores with respect to the per-node weight
  * sums: grad_node[n] += sum over every (q, t) of count_n(q, t) x
- * grad_score[q * n_entities + t] (fp64; caller zero-fills n_nodes values).
+ * grad_score[q * n_entities + t] (fp64; caller zero-fills n_nodes values;
+ * summed as int64 fixed point at one scale per launch, so the result is
+ * run-to-run bitwise; the workspace header's words 20..23 hold the scale's
+ * statistics).
  * A rule's weight gradient is its node's (rules ending at one node share their
  * counts) — the backward of `score += x * rule_weights[index]`
  * (predictors.py:62-66) that trainer.py:90's loss.backward() takes. */
@@ -572,20 +584,25 @@ int rnnl_nll_backward(const float *logits, const float *target, const int64_t *a
  * The entity feature's gradient (bias: column sums of grad_score; RotatE:
  * rnnl_rotate_backward) is the caller's.  head >= 0: every row is of that
  * relation (a training batch; only its trie is touched), -1: any rows.
- * scratch: rnnl_predictorplus_backward_size bytes.  Deterministic except for
- * the fp64 atomic sums of the per-node and relation_emb gradients (order-
- * dependent in the last fp64 bits only). */
+ * scratch: rnnl_predictorplus_backward_size bytes; rows_scratch:
+ * rnnl_predictorplus_backward_rows_size(n_queries, n_cand_total) bytes (one
+ * dL/dy slot per scoring chunk).  Run-to-run deterministic for head >= 0 (a
+ * training batch): fixed-order partial sums, and the per-node gradients as
+ * int64 fixed-point sums at one scale per launch (order-independent integer
+ * adds); with head = -1 the relation_emb gradient takes fp64 atomics per
+ * relation run (order-dependent in the last fp64 bits). */
 typedef struct {
   float *emb;
   int32_t emb_ld;
   float *add_w, *add_b, *ln_w, *ln_b, *s0_w, *s0_b, *s1_w, *s1_b, *rel_emb;
 } rnnl_sum_grads;
 int rnnl_predictorplus_backward_size(rnnl_rules r, int32_t n_relations, size_t *bytes);
+int rnnl_predictorplus_backward_rows_size(int32_t n_queries, int64_t n_cand_total, size_t *bytes);
 int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *p, const float *emb,
                                 int32_t emb_ld, const int64_t *all_r, int32_t n_queries, const float *grad_score,
                                 const int32_t *n_cand, int64_t n_cand_total, void *workspace, size_t workspace_bytes,
                                 int32_t capacity_scale, int32_t head, void *scratch, size_t scratch_bytes,
-                                const rnnl_sum_grads *grads, void *stream);
+                                void *rows_scratch, size_t rows_bytes, const rnnl_sum_grads *grads, void *stream);
 
 /* ------------------------------------------------ 64-bit path counts --
  * Rows whose path counts (or PNA degree) reach 2^32 fail the forward with

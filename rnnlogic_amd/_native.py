@@ -62,6 +62,7 @@ SIGNATURES = [
     ("rnnl_forward_rotate_zero", ctypes.c_int, [_P, ctypes.c_size_t, _P]),
     ("rnnl_forward_status", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_status_totals", ctypes.c_int, [_P, _P, _P]),
+    ("rnnl_forward_host_info", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_header_bytes", ctypes.c_int, [_P]),
     ("rnnl_forward_status_host", ctypes.c_int, [_P, _P]),
     ("rnnl_forward_status_flags", ctypes.c_int, [_P, _P, _P, _P]),
@@ -81,6 +82,7 @@ SIGNATURES = [
     ("rnnl_debug_profile", ctypes.c_int, [_P]),
     ("rnnl_debug_clock", ctypes.c_int, [_P]),
     ("rnnl_debug_capacity", ctypes.c_int, [_I64, _I64, _I64]),
+    ("rnnl_debug_sort_bits", ctypes.c_int, [_I32]),
     ("rnnl_debug_pair_memo", ctypes.c_int, [_I32]),
     ("rnnl_fill_rows", ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     ("rnnl_fill_value", ctypes.c_int, [_F32, _I64, _P, _P]),
@@ -114,8 +116,10 @@ SIGNATURES = [
      [_P, _P, _P, _P, _P, _P, _I32, _P, ctypes.c_size_t, _P, _P, _P, _P, _I64, _P, _P]),
     ("rnnl_forward_error_bits", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_predictorplus_backward_size", ctypes.c_int, [_P, _I32, _P]),
+    ("rnnl_predictorplus_backward_rows_size", ctypes.c_int, [_I32, _I64, _P]),
     ("rnnl_predictorplus_backward", ctypes.c_int,
-     [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I64, _P, ctypes.c_size_t, _I32, _I32, _P, ctypes.c_size_t, _P, _P]),
+     [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I64, _P, ctypes.c_size_t, _I32, _I32, _P, ctypes.c_size_t, _P,
+      ctypes.c_size_t, _P, _P]),
 ]
 
 

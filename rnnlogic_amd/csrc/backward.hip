@@ -15,14 +15,22 @@
 //       differentiated: dL/dy_c from the score gradient at (row, entity).
 //       Then, lane-owned: lane l owns score_model.layers.0 rows 2l, 2l + 1 and
 //       walks the chunk's 64 staged candidates (z_c, g_c) — weight gradients
-//       as register sums, no atomics.  Per bucket entry (node n, count k) of a
-//       candidate: G_n += k dL/dy_c (fp64 atomics: G_n is the gradient of the
-//       node's un-folded rule-embedding sum before the Linear).
+//       as register sums, no atomics.  Each candidate's dL/dy_c goes to a
+//       per-chunk slot, with the launch's max |dL/dy| and its sum of path
+//       counts (order-independent: a max and an integer sum).
+//   node_accum_kernel     per bucket entry (node n, count k) of a candidate:
+//       G_n += k dL/dy_c, as int64 fixed point at one scale for the launch
+//       (2^s with sum k x max |dL/dy| x 2^s < 2^62): integer sums, so the
+//       result does not depend on the order of the adds — run-to-run bitwise
+//       (G_n is the gradient of the node's un-folded rule-embedding sum
+//       before the Linear).
 //   node_grad_kernel      per trie node: dL/dx_rule = W_add^T G_n for each
 //       member rule (the reference's index_select / matmul backward), and
 //       dL/dW_add = sum_n G_n (x) s_n with s_n the node's embedding sum.
 //   grad_reduce_kernel    the per-block partials summed in a fixed order into
-//       the parameter gradients (relation_emb's from fp64 sums).
+//       the parameter gradients; rel_grad_kernel: relation_emb's gradient of a
+//       one-relation launch (a training batch) as W0[:, 16:]^T dL/db0, in a
+//       fixed order (mixed-relation launches: fp64 atomics per relation run).
 //
 // Not differentiated here: the grounding (integer, no gradient: data.py:138
 // torch.no_grad), the entity feature (bias: column sums; RotatE: its own HIP
@@ -52,11 +60,27 @@ constexpr int BW_BIG = 24;      // bucket lists longer than this are walked by t
 // batch's head relation.  Many candidates of a batch share a node (a short
 // rule reaches most of them), so per-entry global atomics serialise on a few
 // addresses (2.4 ms per FB15k-237 batch); summed in LDS first, each
-// workgroup writes one partial row.  fp64, so that the sums do not depend on
-// the atomics' order beyond the last fp64 bits; the trie's breadth-first
-// numbering puts the short (most shared) rule prefixes first, and nodes past
-// the LDS range take fp64 HBM atomics.
+// workgroup writes one partial row.  int64 fixed point (node_accum_kernel):
+// exact integer sums in any order; the trie's breadth-first numbering puts
+// the short (most shared) rule prefixes first, and nodes past the LDS range
+// take int64 HBM atomics.
 constexpr int BW_LDS_NODES = 768;
+// stats words (scratch): u32 max |dL/dy| bits, pad, u64 sum of the path counts
+// of the entries of candidates with a non-zero score gradient
+struct BwStats {
+  unsigned int maxgy, pad;
+  unsigned long long sumk;
+};
+
+// The launch's fixed-point scale: 2^s with sum k x max|dL/dy| x 2^s < 2^62, so
+// every term and every partial sum of count x dL/dy fits int64.  `bad`: a
+// non-finite dL/dy (the gradients are then NaN, as the reference's would be).
+__device__ __forceinline__ int bw_scale(const BwStats *st, bool &bad) {
+  const float mg = __uint_as_float(st->maxgy);
+  bad = st->maxgy >= 0x7f800000u;
+  const double total = (double)st->sumk * (double)mg;
+  return (bad || !(total > 0.0)) ? 0 : 61 - ilogb(total);
+}
 constexpr int NG_GRID = 128;    // node_grad_kernel workgroups (max)
 
 struct BwdLds {
@@ -66,7 +90,6 @@ struct BwdLds {
   float relb[BW_WAVES][128];    // per wave: b0 + W0[:, 16:] . rel_emb[r]
   float stage[BW_WAVES][64][20];  // per wave: candidate c's z[16] | g | pad
   float red[BWB];               // block reduction
-  double gacc[BW_LDS_NODES][16];  // G_n of the head's first nodes (lo + i)
 };
 
 __device__ __forceinline__ float relu_f(float x) { return x > 0.f ? x : 0.f; }
@@ -94,31 +117,15 @@ __device__ __forceinline__ float block_sum_lane(BwdLds &S, float v) {
   return t;  // valid in wave 0
 }
 
-// lo, nl: the head's node range held in LDS (nl = 0: global atomics only)
-// One bucket entry (node, count) of a candidate: G_node += count x dL/dy —
-// in LDS for the head's first nl nodes, else fp64 HBM atomics.
-__device__ __forceinline__ void node_grad_add(BwdLds &S, double *gnode, const int2 be, int lo, int nl,
-                                              const float (&gy)[16]) {
-  const unsigned ln = (unsigned)(be.x - lo);
-  if (ln < (unsigned)nl) {
-    const double k = (double)(uint32_t)be.y;
-#pragma unroll
-    for (int d = 0; d < 16; ++d) atomicAdd(&S.gacc[ln][d], k * (double)gy[d]);
-  } else {
-    const double k = (double)(uint32_t)be.y;
-    double *gn = gnode + (int64_t)be.x * 16;
-#pragma unroll
-    for (int d = 0; d < 16; ++d) unsafeAtomicAdd(gn + d, k * (double)gy[d]);
-  }
-}
-
+// gy: per chunk c of the chunk list, lane l: dL/dy of candidate s0 + l at
+// gy[(c * 16 + d) * 64 + l] (chunk capacity gy_cap).  single: every row is of
+// one relation (relation_emb's gradient is then rel_grad_kernel's).
 __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const float *__restrict__ grad,
-                                                            double *__restrict__ gnode, double *__restrict__ grel,
-                                                            float *__restrict__ part, float *__restrict__ gpart,
-                                                            int lo, int nl) {
+                                                            double *__restrict__ grel, float *__restrict__ part,
+                                                            float *__restrict__ gy_out, int64_t gy_cap,
+                                                            BwStats *__restrict__ stats, int single) {
   __shared__ BwdLds S;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < nl * 16; i += BWB) (&S.gacc[0][0])[i] = 0.0;
   for (int i = tid; i < 128 * 32; i += BWB) S.w0[i >> 5][i & 31] = p.s0_w[i];
   for (int i = tid; i < 128; i += BWB) {
     S.w1[i] = p.s1_w[i];
@@ -159,6 +166,14 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
   // layers.0 and relation_emb) flushed when the relation changes / at the end
   auto flush_rel = [&](int r) {
     if (r < 0) return;
+    if (single) {  // relation_emb's gradient from dL/db0 (rel_grad_kernel)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a_rel[j][i] = fmaf(run_s[j], p.rel_emb[r * 16 + i], a_rel[j][i]);
+      run_s[0] = run_s[1] = 0.f;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -173,8 +188,10 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
     run_s[0] = run_s[1] = 0.f;
   };
   const long long nw = (long long)gridDim.x * BW_WAVES;
+  unsigned int my_max = 0u;         // lane max |dL/dy| bits
+  unsigned long long my_k = 0ull;   // lane sum of the path counts
 #pragma unroll 1
-  for (long long c = (long long)blockIdx.x * BW_WAVES + wv; c < nchunks; c += nw) {
+  for (long long c = (long long)blockIdx.x * BW_WAVES + wv; c < nchunks && c < gy_cap; c += nw) {
     const int2 ck = p.chunks[c];
     const int q = __builtin_amdgcn_readfirstlane(ck.x);
     const int s0 = __builtin_amdgcn_readfirstlane(ck.y);
@@ -199,6 +216,7 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
     double acc[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) acc[d] = 0.0;
+    unsigned long long ksum = 0ull;  // the candidate's sum of path counts
     if (live) {
       cr = p.cand[qb + s];
       g = grad[(int64_t)q * E + cr.x];
@@ -206,6 +224,7 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
 #pragma unroll 1
         for (int e = cr.y; e < cr.y + cr.z; ++e) {
           const int2 be = p.bent[e];
+          ksum += (uint32_t)be.y;
           const double k = (double)(uint32_t)be.y;
           const int *x = reinterpret_cast<const int *>(p.node_w + (uint32_t)be.x * (uint32_t)kStrideSum);
 #pragma unroll
@@ -221,14 +240,18 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
       double a[16];
 #pragma unroll
       for (int d = 0; d < 16; ++d) a[d] = 0.0;
+      unsigned long long kk = 0ull;
 #pragma unroll 1
       for (int e = beg + lane; e < beg + cnt; e += 64) {
         const int2 be = p.bent[e];
+        kk += (uint32_t)be.y;
         const double k = (double)(uint32_t)be.y;
         const int *x = reinterpret_cast<const int *>(p.node_w + (uint32_t)be.x * (uint32_t)kStrideSum);
 #pragma unroll
         for (int d = 0; d < 16; ++d) a[d] = fma(k, (double)x[d], a[d]);
       }
+      kk = wave_sum(kk);
+      if (lane == owner) ksum = kk;
 #pragma unroll
       for (int d = 0; d < 16; ++d) {
         const double t = wave_sum(a[d]);
@@ -282,26 +305,20 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
     float gy[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) {
-      gy[d] = rstd * (gxh[d] - m1 - xh[d] * m2);
+      gy[d] = rstd * (gxh[d] - m1 - xh[d] * m2);  // NaN-preserving |.| max below
       a_addb[d] += gy[d];
     }
     a_b1 += g;
-    // the candidate's bucket entries: G_n += count x dL/dy (LDS for the
-    // head's nodes, fp64 HBM atomics past BW_LDS_NODES)
-    if (live && g != 0.f && cr.z <= BW_BIG)
-#pragma unroll 1
-      for (int e = cr.y; e < cr.y + cr.z; ++e) node_grad_add(S, gnode, p.bent[e], lo, nl, gy);
-    // long lists: the whole wave adds the owner's dL/dy into its entries
-#pragma unroll 1
-    for (uint64_t big = __ballot(live && g != 0.f && cr.z > BW_BIG); big; big &= big - 1) {
-      const int owner = __builtin_ctzll(big);
-      const int beg = __builtin_amdgcn_readlane(cr.y, owner), cnt = __builtin_amdgcn_readlane(cr.z, owner);
-      float go[16];
+    // the candidate's dL/dy for node_accum_kernel (0 where there is no score
+    // gradient: those candidates add nothing to G_n)
+    const bool adds = live && g != 0.f;
 #pragma unroll
-      for (int d = 0; d < 16; ++d) go[d] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gy[d]), owner));
-#pragma unroll 1
-      for (int e = beg + lane; e < beg + cnt; e += 64) node_grad_add(S, gnode, p.bent[e], lo, nl, go);
+    for (int d = 0; d < 16; ++d) {
+      const float v = adds ? gy[d] : 0.f;
+      gy_out[((int64_t)c * 16 + d) * 64 + lane] = v;
+      my_max = max(my_max, __float_as_uint(fabsf(v)));
     }
+    if (adds) my_k += ksum;
     // stage (z, g) for the lane-owned weight sums
 #pragma unroll
     for (int d = 0; d < 16; ++d) stage[lane][d] = z[d];
@@ -332,12 +349,17 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
     wave_lds_sync();  // the next chunk rewrites the stage
   }
   flush_rel(cur_r);
-  __syncthreads();  // every wave's LDS node sums are in
-  // this workgroup's G_n of the head's first nl nodes: one partial row
-  // (summed per node by node_grad_kernel; atomics from every workgroup to
-  // the same node words serialised at ~0.3 ms per FB15k-237 batch)
-  float *grow = gpart + (int64_t)blockIdx.x * nl * 16;
-  for (int i = tid; i < nl * 16; i += BWB) grow[i] = (float)(&S.gacc[0][0])[i];
+  // the launch's max |dL/dy| and sum of path counts: one atomic per wave
+  // (a max and an integer sum: order-independent)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    my_max = max(my_max, (unsigned int)__shfl_xor((int)my_max, o, 64));
+    my_k += __shfl_xor(my_k, o, 64);
+  }
+  if (lane == 0) {
+    if (my_max) atomicMax(&stats->maxgy, my_max);
+    if (my_k) atomicAdd(&stats->sumk, my_k);
+  }
   // block partial row: lane-owned fields summed over the waves (fixed order),
   // lane-local fields summed over the lanes, then over the waves
   // field-major partials: field f of this workgroup at part[f * BW_GRID + block]
@@ -374,21 +396,98 @@ __global__ __launch_bounds__(BWB) void sum_backward_kernel(KParams p, const floa
   }
 }
 
+// G_n += k dL/dy_c per bucket entry (node n, count k) of the candidates of
+// the chunk list, as int64 fixed point at the launch's scale (bw_scale):
+// LDS sums for the head's first nl nodes (one int64 partial row per
+// workgroup, summed by node_grad_kernel), int64 HBM atomics past them.
+// Integer adds: the sums do not depend on their order.
+__global__ __launch_bounds__(BWB) void node_accum_kernel(KParams p, const float *__restrict__ gy, int64_t gy_cap,
+                                                          const BwStats *__restrict__ stats,
+                                                          unsigned long long *__restrict__ gnode,
+                                                          long long *__restrict__ gpart, int lo, int nl) {
+  __shared__ unsigned long long gacc[BW_LDS_NODES * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < nl * 16; i += BWB) gacc[i] = 0ull;
+  __syncthreads();
+  bool bad;
+  const int sc = bw_scale(stats, bad);
+  const unsigned int *hdr = reinterpret_cast<const unsigned int *>(p.ws);
+  const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
+  // bad (a non-finite dL/dy): fp64 sums in the same words instead, so that
+  // NaN / inf reach exactly the nodes the reference's would
+  auto add = [&](const int2 be, const float (&g)[16]) {
+    const double k = (double)(uint32_t)be.y;
+    const unsigned ln = (unsigned)(be.x - lo);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      if (g[d] == 0.f) continue;
+      unsigned long long *w = ln < (unsigned)nl ? &gacc[ln * 16 + d] : &gnode[(int64_t)be.x * 16 + d];
+      if (bad)
+        atomicAdd(reinterpret_cast<double *>(w), k * (double)g[d]);
+      else
+        atomicAdd(w, (unsigned long long)llrint(ldexp(k * (double)g[d], sc)));
+    }
+  };
+  const long long nw = (long long)gridDim.x * BW_WAVES;
+#pragma unroll 1
+    for (long long c = (long long)blockIdx.x * BW_WAVES + wv; c < nchunks && c < gy_cap; c += nw) {
+      const int2 ck = p.chunks[c];
+      const int q = __builtin_amdgcn_readfirstlane(ck.x);
+      const int s0 = __builtin_amdgcn_readfirstlane(ck.y);
+      const int nc = p.n_cand[q];
+      const bool live = s0 + lane < nc;
+      float g[16];
+      bool any = false;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        g[d] = gy[((int64_t)c * 16 + d) * 64 + lane];
+        any = any || g[d] != 0.f;
+      }
+      int4 cr = make_int4(0, 0, 0, 0);
+      if (live && any) cr = p.cand[p.q_base[q] + s0 + lane];
+      if (live && any && cr.z <= BW_BIG)
+#pragma unroll 1
+        for (int e = cr.y; e < cr.y + cr.z; ++e) add(p.bent[e], g);
+      // long lists: the whole wave adds the owner's dL/dy into its entries
+#pragma unroll 1
+      for (uint64_t big = __ballot(live && any && cr.z > BW_BIG); big; big &= big - 1) {
+        const int owner = __builtin_ctzll(big);
+        const int beg = __builtin_amdgcn_readlane(cr.y, owner), cnt = __builtin_amdgcn_readlane(cr.z, owner);
+        float go[16];
+#pragma unroll
+        for (int d = 0; d < 16; ++d)
+          go[d] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, g[d]), owner));
+#pragma unroll 1
+        for (int e = beg + lane; e < beg + cnt; e += 64) add(p.bent[e], go);
+      }
+    }
+  __syncthreads();
+  // this workgroup's G_n of the head's first nl nodes: one partial row
+  // (summed per node by node_grad_kernel; atomics from every workgroup to
+  // the same node words serialised at ~0.3 ms per FB15k-237 batch)
+  long long *grow = gpart + (int64_t)blockIdx.x * nl * 16;
+  for (int i = tid; i < nl * 16; i += BWB) grow[i] = (long long)gacc[i];
+}
+
 // Per trie node n of [lo, hi) (16 lanes per node, lane d = dimension d):
 // member rules' gradient rows W_add^T G_n, and the block's partial of
 // dL/dW_add = sum_n G_n (x) s_n (s_n: the members' embedding sum, f32 in
 // rule order as node_weights_kernel forms it).  part: 256 floats per block.
-// G_n = the fp64 HBM sums (nodes past the LDS range) + the sum of the
-// backward workgroups' partial rows gpart[b][n - lo] (b < nrow, n < lo + nl),
-// in workgroup order.
-__global__ __launch_bounds__(BWB) void node_grad_kernel(RulesDev rl, int lo, int hi, const double *__restrict__ gnode,
-                                                         const float *__restrict__ gpart, int nrow, int nl,
+// G_n = (the int64 HBM sums (nodes past the LDS range) + the accumulation
+// workgroups' int64 partial rows gpart[b][n - lo] (b < nrow, n < lo + nl))
+// x 2^-s: exact integer sums, then one rounding.
+__global__ __launch_bounds__(BWB) void node_grad_kernel(RulesDev rl, int lo, int hi,
+                                                         const long long *__restrict__ gnode,
+                                                         const long long *__restrict__ gpart, int nrow, int nl,
+                                                         const BwStats *__restrict__ stats,
                                                          const float *__restrict__ emb, int ld,
                                                          const float *__restrict__ add_w, float *__restrict__ gemb,
                                                          int gld, float *__restrict__ part) {
   __shared__ float s_w[256];
   __shared__ float s_red[BW_WAVES][256];
   const int tid = threadIdx.x, d = tid & 15;
+  bool bad;
+  const int sc = bw_scale(stats, bad);
   s_w[tid] = add_w[tid];  // (16 x 16) row-major: y[i] = sum_j W[i][j] f[j]
   __syncthreads();
   float acc[16];  // lane d: sum_n G_n[d] s_n[j]
@@ -399,15 +498,24 @@ __global__ __launch_bounds__(BWB) void node_grad_kernel(RulesDev rl, int lo, int
   // and leave the loop together, as the width-16 shuffles need)
   for (int64_t gid = (int64_t)blockIdx.x * BWB + tid; gid < total; gid += (int64_t)gridDim.x * BWB) {
     const int n = lo + (int)(gid >> 4);
-    float gn = (float)gnode[(int64_t)n * 16 + d];
-    if (gid < (int64_t)nl * 16) {
-      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      int b = 0;
-      for (; b + 8 <= nrow; b += 8)
+    float gn;
+    if (!bad) {
+      long long gi = gnode[(int64_t)n * 16 + d];
+      if (gid < (int64_t)nl * 16) {
+        long long a[4] = {0, 0, 0, 0};
+        int b = 0;
+        for (; b + 4 <= nrow; b += 4)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] += gpart[(int64_t)(b + u) * nl * 16 + gid];
-      for (; b < nrow; ++b) a[0] += gpart[(int64_t)b * nl * 16 + gid];
-      gn += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+          for (int u = 0; u < 4; ++u) a[u] += gpart[(int64_t)(b + u) * nl * 16 + gid];
+        for (; b < nrow; ++b) a[0] += gpart[(int64_t)b * nl * 16 + gid];
+        gi += (a[0] + a[1]) + (a[2] + a[3]);
+      }
+      gn = (float)ldexp((double)gi, -sc);
+    } else {  // non-finite dL/dy: the fp64 sums of node_accum_kernel's fallback
+      double gd = __longlong_as_double(gnode[(int64_t)n * 16 + d]);
+      if (gid < (int64_t)nl * 16)
+        for (int b = 0; b < nrow; ++b) gd += __longlong_as_double(gpart[(int64_t)b * nl * 16 + gid]);
+      gn = (float)gd;
     }
     float s = 0.f;
     const int kb = rl.node_rule_ptr[n], ke = rl.node_rule_ptr[n + 1];
@@ -471,10 +579,23 @@ __global__ __launch_bounds__(BWB) void grad_reduce_kernel(const float *__restric
   if (k < R * 16) gr.rel_emb[k] = (float)grel[k];
 }
 
-// Scratch carve-up (bytes): gnode f64 [n_nodes x 16] | grel f64 [R x 16] |
-// partial rows f32 [BW_GRID x PB_N] | node partials f32 [NG_GRID x 256]
+// relation_emb's gradient of a one-relation launch: the relation half of
+// score_model.layers.0 sees rel_emb[head] in every candidate, so
+// dL/drel_emb[head][i] = sum_o W0[o][16 + i] dL/db0[o] (dL/db0 from
+// grad_reduce_kernel; o ascending), every other relation 0.
+__global__ void rel_grad_kernel(const float *__restrict__ s0_w, int head, rnnl_sum_grads gr) {
+  const int i = threadIdx.x;
+  if (i >= 16) return;
+  float t = 0.f;
+  for (int o = 0; o < 128; ++o) t = fmaf(s0_w[o * 32 + 16 + i], gr.s0_b[o], t);
+  gr.rel_emb[head * 16 + i] = t;
+}
+
+// Scratch carve-up (bytes): gnode i64 [n_nodes x 16] | grel f64 [R x 16] |
+// partial rows f32 [BW_GRID x PB_N] | node partials f32 [NG_GRID x 256] |
+// LDS-node partial rows i64 [BW_GRID x BW_LDS_NODES x 16] | stats
 struct BwdLayout {
-  int64_t gnode, grel, part, npart, gpart, total;
+  int64_t gnode, grel, part, npart, gpart, stats, total;
 };
 
 static BwdLayout bwd_layout(int64_t n_nodes, int64_t R) {
@@ -489,7 +610,9 @@ static BwdLayout bwd_layout(int64_t n_nodes, int64_t R) {
   L.npart = o;
   o = align256(o + 4 * (int64_t)NG_GRID * 256);
   L.gpart = o;
-  o = align256(o + 4 * (int64_t)BW_GRID * BW_LDS_NODES * 16);
+  o = align256(o + 8 * (int64_t)BW_GRID * BW_LDS_NODES * 16);
+  L.stats = o;
+  o = align256(o + (int64_t)sizeof(BwStats));
   L.total = o;
   return L;
 }
@@ -509,33 +632,50 @@ int rnnl_predictorplus_backward_size(rnnl_rules r, int32_t n_relations, size_t *
   return RNNL_OK;
 }
 
+// per-call scratch: one dL/dy slot of 16 x 64 floats per scoring chunk
+// (<= n_cand_total / 64 + one per row)
+static int64_t gy_chunks(int64_t nq, int64_t n_cand_total) { return n_cand_total / 64 + nq + 1; }
+
+int rnnl_predictorplus_backward_rows_size(int32_t nq, int64_t n_cand_total, size_t *bytes) {
+  if (!bytes || nq < 0 || n_cand_total < 0) {
+    set_error("rnnl_predictorplus_backward_rows_size: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *bytes = (size_t)gy_chunks(nq, n_cand_total) * 16 * 64 * sizeof(float);
+  return RNNL_OK;
+}
+
 int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor_params *pp, const float *emb,
                                 int32_t ld, const int64_t *all_r, int32_t nq, const float *grad_score,
                                 const int32_t *n_cand, int64_t n_cand_total, void *ws, size_t ws_bytes,
-                                int32_t scale, int32_t head,
-                                void *scratch, size_t scratch_bytes, const rnnl_sum_grads *gr, void *stream) {
+                                int32_t scale, int32_t head, void *scratch, size_t scratch_bytes,
+                                void *rows_scratch, size_t rows_bytes, const rnnl_sum_grads *gr, void *stream) {
   if (!g || !r || !pp || !emb || ld < 16 || !all_r || nq < 0 || !grad_score || !n_cand || !ws || scale < 1 ||
       !scratch || !gr || !gr->emb || gr->emb_ld < 16 || !gr->add_w || !gr->add_b || !gr->ln_w || !gr->ln_b ||
       !gr->s0_w || !gr->s0_b || !gr->s1_w || !gr->s1_b || !gr->rel_emb || pp->aggregator != RNNL_AGG_SUM ||
       !pp->node_w || !pp->add_w || !pp->add_b || !pp->ln_w || !pp->ln_b || !pp->s0_w || !pp->s0_b || !pp->s1_w ||
-      !pp->rel_emb || head >= g->d.R || n_cand_total < 0) {
+      !pp->rel_emb || head >= g->d.R || n_cand_total < 0 || !rows_scratch) {
     set_error("rnnl_predictorplus_backward: bad arguments");
     return RNNL_ERR_INVALID;
   }
   const int R = g->d.R;
   const BwdLayout B = bwd_layout(r->d.n_nodes, R);
   const Layout Ly = make_layout(nq, scale, r->d.n_nodes);
-  if (scratch_bytes < (size_t)B.total || ws_bytes < (size_t)Ly.total) {
+  const int64_t gy_cap = gy_chunks(nq, n_cand_total);
+  if (scratch_bytes < (size_t)B.total || ws_bytes < (size_t)Ly.total ||
+      rows_bytes < (size_t)gy_cap * 16 * 64 * sizeof(float)) {
     set_error("rnnl_predictorplus_backward: scratch or workspace too small");
     return RNNL_ERR_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;
   unsigned char *sb = static_cast<unsigned char *>(scratch);
-  double *gnode = reinterpret_cast<double *>(sb + B.gnode);
+  unsigned long long *gnode = reinterpret_cast<unsigned long long *>(sb + B.gnode);
   double *grel = reinterpret_cast<double *>(sb + B.grel);
   float *part = reinterpret_cast<float *>(sb + B.part);
   float *npart = reinterpret_cast<float *>(sb + B.npart);
-  float *gpart = reinterpret_cast<float *>(sb + B.gpart);
+  long long *gpart = reinterpret_cast<long long *>(sb + B.gpart);
+  BwStats *stats = reinterpret_cast<BwStats *>(sb + B.stats);
+  float *gy = static_cast<float *>(rows_scratch);
   // the nodes whose gradient can be non-zero: the head's trie (training
   // batches are one relation), else every node
   int lo = 0, hi = r->d.n_nodes;
@@ -545,8 +685,9 @@ int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor
     if (lo < 0) lo = 0;
   }
   RNNL_HIP_CHECK(hipMemsetAsync(gr->emb, 0, sizeof(float) * (size_t)gr->emb_ld * (size_t)r->d.n_rules, st));
-  if (hi > lo) RNNL_HIP_CHECK(hipMemsetAsync(gnode + (int64_t)lo * 16, 0, sizeof(double) * 16 * (size_t)(hi - lo), st));
+  if (hi > lo) RNNL_HIP_CHECK(hipMemsetAsync(gnode + (int64_t)lo * 16, 0, sizeof(long long) * 16 * (size_t)(hi - lo), st));
   RNNL_HIP_CHECK(hipMemsetAsync(grel, 0, sizeof(double) * 16 * (size_t)R, st));
+  RNNL_HIP_CHECK(hipMemsetAsync(stats, 0, sizeof(BwStats), st));
   KParams p{};
   p.g = g->d;
   p.rl = r->d;
@@ -575,15 +716,19 @@ int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor
   const int64_t nchunk = n_cand_total / 64 + nq;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(BW_GRID, (nchunk + BW_WAVES - 1) / BW_WAVES));
   const int nl = head >= 0 ? std::min(std::max(hi - lo, 0), BW_LDS_NODES) : 0;
-  hipLaunchKernelGGL(sum_backward_kernel, dim3(grid), dim3(BWB), 0, st, p, grad_score, gnode, grel, part, gpart, lo,
-                     nl);
+  hipLaunchKernelGGL(sum_backward_kernel, dim3(grid), dim3(BWB), 0, st, p, grad_score, grel, part, gy, gy_cap, stats,
+                     head >= 0 ? 1 : 0);
+  hipLaunchKernelGGL(node_accum_kernel, dim3(grid), dim3(BWB), 0, st, p, (const float *)gy, gy_cap,
+                     (const BwStats *)stats, gnode, gpart, lo, nl);
   const int64_t nthreads = (int64_t)std::max(hi - lo, 0) * 16;
   const int ngrid = (int)std::max<int64_t>(1, std::min<int64_t>(NG_GRID, (nthreads + BWB - 1) / BWB));
-  hipLaunchKernelGGL(node_grad_kernel, dim3(ngrid), dim3(BWB), 0, st, r->d, lo, std::max(hi, lo), gnode, gpart, grid,
-                     nl, emb, ld, pp->add_w, gr->emb, gr->emb_ld, npart);
+  hipLaunchKernelGGL(node_grad_kernel, dim3(ngrid), dim3(BWB), 0, st, r->d, lo, std::max(hi, lo),
+                     (const long long *)gnode, (const long long *)gpart, grid, nl, (const BwStats *)stats, emb, ld,
+                     pp->add_w, gr->emb, gr->emb_ld, npart);
   const int nwaves = PB_N + 256 + (R * 16 + 63) / 64;  // one wave per field (relation_emb: per 64 entries)
   hipLaunchKernelGGL(grad_reduce_kernel, dim3((nwaves + BW_WAVES - 1) / BW_WAVES), dim3(BWB), 0, st, part, grid,
                      npart, ngrid, grel, R, *gr);
+  if (head >= 0) hipLaunchKernelGGL(rel_grad_kernel, dim3(1), dim3(64), 0, st, pp->s0_w, head, *gr);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -26,8 +26,16 @@ constexpr int HCAP = 1 << HBITS;  // phase-A hash slots ((node, entity) -> count
 constexpr int OCC_CAP = 1024;     // phase-A occupied-slot list (fuller levels scan all HCAP slots)
 constexpr int WBITS = 11;         // phase-B entity window: WIN entities
 constexpr int WIN = 1 << WBITS;
-constexpr int MAXE_BITS = 19;
-constexpr int MAXWIN = (1 << MAXE_BITS) >> WBITS;  // windows per graph (|E| <= 2^MAXE_BITS)
+constexpr int MAXE_BITS = 19;   // |E| <= 2^MAXE_BITS
+// Phase B's counting sort of a large query's contributions: by sort window of
+// 2^sbits entities, sbits the smallest with at most SORT_WINS windows
+// (FB15k-237: 16 entities, WN18RR: 64, kinship / UMLS: 1), so that
+// consecutive windows fill LDS hash passes (which merge a candidate's
+// duplicate (node, entity) entries) and only a window of more than HB_LOAD
+// contributions takes the dense direct-mapped pass.
+constexpr int SORT_WINS = 1024;
+constexpr int MAX_SBITS = MAXE_BITS - 10;  // 2^MAXE_BITS / SORT_WINS entities per window at most
+static_assert((1 << MAX_SBITS) <= WIN, "a sort window must fit the dense pass's direct map");
 constexpr int HB = WIN;                // phase-B candidate hash slots
 constexpr int HB_LOAD = HB * 3 / 4;    // max contributions per hash pass
 constexpr int WG_PER_CU = 2;           // grounding workgroups per CU at SOLO_GBS lanes (LDS-bound)
@@ -41,7 +49,11 @@ constexpr int WIDE_ROWS = 256;  // launches of at most this many rows ground wit
 constexpr int sort_words(int G) { return (9 * G * 4 / 6) & ~(G - 1); }
 
 // Workspace header words (uint32), then a 64-bit pool counter at byte 64.
-enum { H_STATUS = 0, H_DEQUEUE = 1, H_FLAGS = 2, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6, H_NCAND = 8 };
+enum {
+  H_STATUS = 0, H_DEQUEUE = 1, H_FLAGS = 2, H_ERRBITS = 3, H_ERRQ = 4, H_DEQUEUE2 = 5, H_CHUNKS = 6, H_NCAND = 8,
+  H_NENT = 10,  // 64-bit: bucket entries written (<= the pool reserved: duplicates merge in phase B)
+  H_BW_MAXG = 20, H_BW_SUMK = 22  // EM Predictor backward's fixed-point stats (past the status read-back)
+};
 // H_FLAGS bit 0: the launch's rows hold more than one relation (the
 // reference forward's one-relation-per-batch check, predictors.py:54-55 /
 // 211-212, read back with the status instead of a separate reduction)
@@ -91,6 +103,7 @@ struct KParams {
   int32_t nq;
   int32_t ebits;     // entity bits of the packed (trie node, entity) keys
   uint32_t emask;    // (1 << ebits) - 1
+  int32_t sbits;     // phase B's sort windows: 2^sbits entities (SORT_WINS)
   float *score;
   uint8_t *mask;
   int32_t *n_cand;

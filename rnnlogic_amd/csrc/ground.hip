@@ -24,11 +24,13 @@
 #include <string>
 
 #include "fwd.h"
+#include "hostside.h"
 
 namespace rnnl {
 
 unsigned long long *g_prof = nullptr;
 int64_t g_fcap_base = FCAP_BASE, g_pcap_base = PCAP_BASE, g_pool_per_query = POOL_PER_QUERY;
+int g_sort_bits = -1;  // rnnl_debug_sort_bits (-1: SORT_WINS windows)
 
 template <int G>
 struct __align__(16) SmemT {
@@ -67,9 +69,10 @@ struct __align__(16) SmemT {
   };
   int ws[(G / 64) + 1];
   int q, nd, np, ovf, err, root, nocc;
+  int nent;  // bucket entries of the current query written so far (phase B)
   long long qbase;
   unsigned long long t0;
-  int whist[MAXWIN], wbeg[MAXWIN + 1], wfill[MAXWIN];
+  int whist[SORT_WINS], wbeg[SORT_WINS + 1], wfill[SORT_WINS];
   unsigned long long sumlog;
   unsigned long long tp[8];  // diagnostic sub-phase cycles (thread 0)
 };
@@ -334,10 +337,10 @@ __device__ int window_pass(const KParams &p, SmemT<G> &S, const Ent *w, int lo, 
   for (int i = tid; i < WIN; i += G) S.u.b.off[i] = S.u.b.cnt[i];
   __syncthreads();
   scan_win<G>(S.u.b.off, S.ws);
-  // candidate records
-  const int64_t qb = S.qbase;
+  // candidate records; the pass's entries follow the query's earlier ones
+  const int64_t qb = S.qbase + S.nent;
   for (int s2 = tid; s2 < nc; s2 += G) {
-    p.cand[cbase + s2] = make_int4(S.u.b.st[s2], (int32_t)(qb + beg + S.u.b.off[s2]), S.u.b.cnt[s2], 0);
+    p.cand[cbase + s2] = make_int4(S.u.b.st[s2], (int32_t)(qb + S.u.b.off[s2]), S.u.b.cnt[s2], 0);
   }
   __syncthreads();
   for (int i = tid; i < WIN; i += G) S.u.b.cnt[i] = 0;
@@ -345,9 +348,11 @@ __device__ int window_pass(const KParams &p, SmemT<G> &S, const Ent *w, int lo, 
   PSTAMP(1);
   for (int i = beg + tid; i < end; i += G) {  // scatter (node, count) into the buckets
     const int s2 = S.u.b.map[(int)(w[i].k & p.emask) - lo];
-    const int64_t pos = qb + beg + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
+    const int64_t pos = qb + S.u.b.off[s2] + atomicAdd(&S.u.b.cnt[s2], 1);
     p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
   }
+  __syncthreads();
+  if (tid == 0) S.nent += end - beg;
   __syncthreads();
   PSTAMP(2);
   return nc;
@@ -376,6 +381,10 @@ __device__ __forceinline__ int hb_slot(SmemT<G> &S, int t, bool insert) {
 }
 
 template <int G>
+__device__ int hash_pass_merged(const KParams &p, SmemT<G> &S, const Ent *w, int beg, int end, int64_t cbase,
+                                int lo, int hi);
+
+template <int G>
 __device__ int hash_pass(const KParams &p, SmemT<G> &S, const Ent *w, int beg, int end, int64_t cbase,
                          bool degree_only, int lo, int hi) {
   // w: contributions (a = entity, b = node, c = count), window-sorted or raw;
@@ -385,6 +394,7 @@ __device__ int hash_pass(const KParams &p, SmemT<G> &S, const Ent *w, int beg, i
   // candidates in ascending entity order (the reference's nonzero order, and
   // neighbouring lanes of the scoring pass then touch neighbouring score entries)
   const bool by_rank = !degree_only && nw <= sort_words(G);
+  if (by_rank) return hash_pass_merged(p, S, w, beg, end, cbase, lo, hi);
   for (int i = tid; i < HB; i += G) {
     S.u.c.key[i] = EMPTY;
     S.u.c.cnt[i] = 0;
@@ -483,13 +493,14 @@ __device__ int hash_pass(const KParams &p, SmemT<G> &S, const Ent *w, int beg, i
     __syncthreads();
     return nc;
   }
-  // bucket start of hash slot i: off is indexed by rank (by_rank) or by slot
-  const int64_t qb = S.qbase;
+  // bucket start of hash slot i: off is indexed by rank (by_rank) or by slot;
+  // the pass's entries follow the query's earlier ones
+  const int64_t qb = S.qbase + S.nent;
   for (int i = tid; i < HB; i += G) {
     if (S.u.c.key[i] != EMPTY) {
       const int cid = S.u.c.cid[i];
       const int64_t c = cbase + cid;
-      p.cand[c] = make_int4(S.u.c.key[i], (int32_t)(qb + beg + S.u.c.off[by_rank ? cid : i]), S.u.c.cnt[i], 0);
+      p.cand[c] = make_int4(S.u.c.key[i], (int32_t)(qb + S.u.c.off[by_rank ? cid : i]), S.u.c.cnt[i], 0);
     }
   }
   __syncthreads();
@@ -497,45 +508,168 @@ __device__ int hash_pass(const KParams &p, SmemT<G> &S, const Ent *w, int beg, i
   __syncthreads();
   for (int i = beg + tid; i < end; i += G) {  // scatter (node, count) into the buckets
     const int sl2 = hb_slot(S, (int)(w[i].k & p.emask), false);
-    const int64_t pos = qb + beg + S.u.c.off[by_rank ? S.u.c.cid[sl2] : sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
+    const int64_t pos = qb + S.u.c.off[by_rank ? S.u.c.cid[sl2] : sl2] + atomicAdd(&S.u.c.cnt[sl2], 1);
     p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
   }
+  __syncthreads();
+  if (tid == 0) S.nent += end - beg;
   __syncthreads();
   return nc;
 }
 
-// Counting sort of the contributions by entity window into fn/fv/fc[0]
-// (free during phase B), then window_pass over every non-empty window.
+// hash_pass with the candidates ranked by entity (the pass's entity range
+// within sort_words(G) x 32) and the contributions MERGED: phase A emits a
+// rule-end (trie node, entity) once per path prefix that reaches it (its
+// hash merges only the inner levels), so one candidate's bucket can hold one
+// node several times.  Here the LDS hash is keyed by the whole (node, entity)
+// key and sums the counts (u32, carry-checked as in phase A), so every
+// bucket holds each node once — the reference's stacked rule_count has one
+// entry per (rule, candidate) (predictors.py:239-244).  Counts add exactly,
+// and every consumer of the buckets (features, memos, digests, EM scores and
+// statistics, backward) is a sum over the entries: results are unchanged.
+// Writes the pass's distinct entries after the query's earlier ones.
+template <int G>
+__device__ int hash_pass_merged(const KParams &p, SmemT<G> &S, const Ent *w, int beg, int end, int64_t cbase,
+                                int lo, int hi) {
+  const int tid = threadIdx.x;
+  const int w0 = lo >> 5, nw = ((hi - 1) >> 5) - w0 + 1;
+  constexpr int PER = HB / G;
+  for (int i = tid; i < HB; i += G) {
+    S.u.c.key[i] = EMPTY;
+    S.u.c.cnt[i] = 0;
+    S.u.c.off[i] = 0;
+  }
+  for (int i = tid; i < nw; i += G) S.sbits[i] = 0u;
+  __syncthreads();
+  // (node, entity) keys (< 2^31: never EMPTY), counts summed
+  for (int i = beg + tid; i < end; i += G) {
+    const Ent e = w[i];
+    const int sl = hb_slot(S, (int)e.k, true);
+    const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(&S.u.c.cnt[sl]), e.c);
+    if (old + e.c < old) atomicOr(&S.err, ERR_COUNT_WIDTH);  // carry out of the u32 path count
+  }
+  __syncthreads();
+  for (int i = tid; i < HB; i += G) {
+    const int k = S.u.c.key[i];
+    if (k != EMPTY) {
+      const int t = k & (int)p.emask;
+      atomicOr(&S.sbits[(t >> 5) - w0], 1u << (t & 31));
+    }
+  }
+  __syncthreads();
+  // rank of an entity = popcounts of the words before it + of its word below it
+  const int per = (nw + G - 1) / G;
+  int sum = 0;
+  for (int j = 0; j < per; ++j) {
+    const int i = tid * per + j;
+    if (i < nw) sum += __popc(S.sbits[i]);
+  }
+  int nc;
+  int base = block_scan<G>(sum, S.ws, nc);
+  for (int j = 0; j < per; ++j) {
+    const int i = tid * per + j;
+    if (i < nw) {
+      S.spre[i] = (unsigned short)base;
+      base += __popc(S.sbits[i]);
+    }
+  }
+  __syncthreads();
+  // per key its candidate (rank); bucket sizes (distinct nodes) by rank
+  for (int i = tid; i < HB; i += G) {
+    const int k = S.u.c.key[i];
+    if (k != EMPTY) {
+      const int kk = (k & (int)p.emask) - (w0 << 5), wd = kk >> 5;
+      const int rank = S.spre[wd] + __popc(S.sbits[wd] & ((1u << (kk & 31)) - 1u));
+      S.u.c.cid[i] = rank;
+      atomicAdd(&S.u.c.off[rank], 1);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the bucket sizes (rank order): off[rank] = bucket start
+  int loc[PER];
+  int s2 = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    loc[j] = S.u.c.off[tid * PER + j];
+    s2 += loc[j];
+  }
+  int nd;
+  int run = block_scan<G>(s2, S.ws, nd);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    S.u.c.off[tid * PER + j] = run;
+    run += loc[j];
+  }
+  // this thread's keys' counts to registers: cnt becomes the buckets' fill counters
+  uint32_t mine[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) mine[j] = (uint32_t)S.u.c.cnt[tid + j * G];
+  __syncthreads();
+  for (int i = tid; i < HB; i += G) S.u.c.cnt[i] = 0;
+  __syncthreads();
+  const int64_t qb = S.qbase + S.nent;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + j * G;
+    const int k = S.u.c.key[i];
+    if (k != EMPTY) {
+      const int rank = S.u.c.cid[i];
+      const int start = S.u.c.off[rank];
+      const int at = atomicAdd(&S.u.c.cnt[rank], 1);
+      p.bent[qb + start + at] = make_int2(S.root + (int)((uint32_t)k >> p.ebits), (int)mine[j]);
+      if (at == 0) {  // the bucket's first writer writes its candidate record
+        const int size = (rank + 1 < nc ? S.u.c.off[rank + 1] : nd) - start;
+        p.cand[cbase + rank] = make_int4(k & (int)p.emask, (int32_t)(qb + start), size, 0);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) S.nent += nd;
+  __syncthreads();
+  return nc;
+}
+
+// Counting sort of the contributions by sort window (2^sbits entities,
+// fwd.h SORT_WINS) into the frontier buffer f(0) (free during phase B), then
+// consecutive windows in hash passes of up to HB_LOAD contributions (which
+// merge duplicate (node, entity) entries, hash_pass_merged), a window of
+// more than HB_LOAD contributions alone in the dense window_pass.
 template <int G>
 __device__ int candidates_phase(const KParams &p, SmemT<G> &S, const Slot &sl, int P, bool degree_only, bool sorted) {
   const int tid = threadIdx.x;
   // all contributions fit one hash pass: no window sort (it exists only to
   // bound the hash load) — one read of the raw list instead of a sorted copy
   if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only, 0, p.g.E) : 0;
-  const int nwin = (p.g.E + WIN - 1) >> WBITS;
-  // a graph of at most one window (kinship, UMLS): the dense pass over the
-  // raw list, without the window-sorted copy
-  if (nwin == 1) return window_pass(p, S, sl.ct, 0, 0, P, S.qbase, degree_only);
+  const int sb = p.sbits;
+  const int nwin = (p.g.E + (1 << sb) - 1) >> sb;
   if (!sorted) {
     for (int i = tid; i < nwin; i += G) S.whist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < P; i += G) atomicAdd(&S.whist[(int)(sl.ct[i].k & p.emask) >> WBITS], 1);
+    for (int i = tid; i < P; i += G) atomicAdd(&S.whist[(int)(sl.ct[i].k & p.emask) >> sb], 1);
     __syncthreads();
-    if (tid == 0) {
-      int acc = 0;
-      for (int w = 0; w < nwin; ++w) {
-        const int c = S.whist[w];
-        S.wbeg[w] = acc;
-        S.wfill[w] = acc;
-        acc += c;
-      }
-      S.wbeg[nwin] = acc;
+    // window starts: a block scan of the histogram (consecutive windows per thread)
+    const int per = (nwin + G - 1) / G;
+    int loc = 0;
+    for (int j = 0; j < per; ++j) {
+      const int i = tid * per + j;
+      if (i < nwin) loc += S.whist[i];
     }
+    int total;
+    int acc = block_scan<G>(loc, S.ws, total);
+    for (int j = 0; j < per; ++j) {
+      const int i = tid * per + j;
+      if (i < nwin) {
+        S.wbeg[i] = acc;
+        S.wfill[i] = acc;
+        acc += S.whist[i];
+      }
+    }
+    if (tid == 0) S.wbeg[nwin] = total;
     __syncthreads();
     for (int i = tid; i < P; i += G) {
       const Ent ce = sl.ct[i];
       const int t = (int)(ce.k & p.emask);
-      const int pos = atomicAdd(&S.wfill[t >> WBITS], 1);
+      const int pos = atomicAdd(&S.wfill[t >> sb], 1);
       sl.f(0)[pos] = ce;
     }
     wg_sync_global();
@@ -546,15 +680,15 @@ __device__ int candidates_phase(const KParams &p, SmemT<G> &S, const Slot &sl, i
   for (int w = 0; w < nwin;) {
     const int beg = S.wbeg[w];
     if (S.wbeg[w + 1] - beg > HB_LOAD) {
-      ncand += window_pass(p, S, sl.f(0), w << WBITS, beg, S.wbeg[w + 1], S.qbase + ncand, degree_only);
+      ncand += window_pass(p, S, sl.f(0), w << sb, beg, S.wbeg[w + 1], S.qbase + ncand, degree_only);
       ++w;
       continue;
     }
     int w2 = w + 1;
     while (w2 < nwin && S.wbeg[w2 + 1] - beg <= HB_LOAD) ++w2;
     if (S.wbeg[w2] > beg)
-      ncand += hash_pass(p, S, sl.f(0), beg, S.wbeg[w2], S.qbase + ncand, degree_only, w << WBITS,
-                         min(w2 << WBITS, p.g.E));
+      ncand += hash_pass(p, S, sl.f(0), beg, S.wbeg[w2], S.qbase + ncand, degree_only, w << sb,
+                         min(w2 << sb, p.g.E));
     w = w2;
   }
   return ncand;
@@ -621,6 +755,7 @@ __global__ __launch_bounds__(G) void ground_kernel(KParams p) {
       S.nd = 0;
       S.nocc = 0;
       S.ovf = 0;
+      S.nent = 0;
       S.sumlog = 0ull;
     }
     __syncthreads();
@@ -667,6 +802,7 @@ __global__ __launch_bounds__(G) void ground_kernel(KParams p) {
     } else if (tid == 0) {
       p.n_cand[q] = ncand;
       atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_NCAND), (unsigned long long)ncand);
+      atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_NENT), (unsigned long long)S.nent);
       p.q_base[q] = S.qbase;
       if (p.prof) {
         pr[2] += __builtin_amdgcn_s_memtime() - t_a;
@@ -964,7 +1100,7 @@ int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all
     set_error(std::string(who) + ": bad arguments");
     return RNNL_ERR_INVALID;
   }
-  if ((int64_t)g->d.E > (int64_t)MAXWIN * WIN) {
+  if ((int64_t)g->d.E > (int64_t)SORT_WINS << MAX_SBITS) {
     set_error(std::string(who) + ": more entities than the kernel's window table supports");
     return RNNL_ERR_INVALID;
   }
@@ -990,6 +1126,9 @@ int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all
   p.g = g->d;
   p.ebits = ebits;
   p.emask = (uint32_t)((1u << ebits) - 1u);
+  p.sbits = 0;
+  while (((int64_t)g->d.E + (1ll << p.sbits) - 1) >> p.sbits > SORT_WINS) ++p.sbits;
+  if (g_sort_bits >= p.sbits && g_sort_bits <= WBITS) p.sbits = g_sort_bits;
   p.rl = r->d;
   p.all_h = all_h;
   p.all_r = all_r;
@@ -1082,6 +1221,7 @@ KParams export_params(void *ws, int32_t nq, int32_t scale, const int32_t *n_cand
   const Layout Ly = make_layout(nq, scale);
   unsigned char *base = static_cast<unsigned char *>(ws);
   KParams p{};
+  p.ws = base;
   p.nq = nq;
   p.n_cand = const_cast<int32_t *>(n_cand);
   p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
@@ -1279,6 +1419,11 @@ int rnnl_debug_pair_memo(int32_t on) {
   return RNNL_OK;
 }
 
+int rnnl_debug_sort_bits(int32_t bits) {
+  g_sort_bits = bits;
+  return RNNL_OK;
+}
+
 int rnnl_debug_profile(void *dev_counters) {
   g_prof = static_cast<unsigned long long *>(dev_counters);
   return RNNL_OK;
@@ -1316,43 +1461,34 @@ struct HostSide {
   hipEvent_t in = nullptr, zero = nullptr, side = nullptr, mask = nullptr;
 };
 
-// Makes `dev` the current device for the guard's scope (restored after).
-// The host-side resources, the side streams and a null `stream` argument all
-// belong to the current device, which need not be the device of the tensors
-// (a caller on cuda:k that never called set_device).
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    int cur = 0;
-    if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
+// The HIP device API of hostside.h's keying: the host-side resources, the
+// side streams and a null `stream` argument all belong to the current device,
+// which need not be the device of the tensors (a caller on cuda:k that never
+// called set_device) — every entry point holds a DeviceGuard for the device
+// of its stream / graph first.
+struct HipDeviceApi {
+  static int get_device(int *dev) { return hipGetDevice(dev) == hipSuccess ? 0 : 1; }
+  static int set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : 1; }
+  static int stream_device(void *s, int *dev) { return hipStreamGetDevice((hipStream_t)s, dev) == hipSuccess ? 0 : 1; }
 };
+using DeviceGuard = DeviceGuardT<HipDeviceApi>;
+static int stream_device(void *stream) { return stream_device_of<HipDeviceApi>(stream); }
 
-// The device of a stream argument: a null stream is the current device's.
-static int stream_device(void *stream) {
-  int dev = 0;
-  if (stream) {
-    if (hipStreamGetDevice((hipStream_t)stream, &dev) == hipSuccess) return dev;
-    return -1;
-  }
-  return hipGetDevice(&dev) == hipSuccess ? dev : -1;
+static std::map<int, HostSide> &host_sides() {
+  thread_local std::map<int, HostSide> all;
+  return all;
 }
 
 // The current device's resources (callers hold a DeviceGuard for the device
 // of their data / stream).
 static HostSide *host_side() {
-  thread_local std::map<int, HostSide> all;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  HostSide &h = all[dev];
-  if (!h.pinned && hipHostMalloc(reinterpret_cast<void **>(&h.pinned), 256, hipHostMallocDefault) != hipSuccess) {
-    h.pinned = nullptr;
+  HostSide *h = current_device_entry<HipDeviceApi>(host_sides());
+  if (!h) return nullptr;
+  if (!h->pinned && hipHostMalloc(reinterpret_cast<void **>(&h->pinned), 256, hipHostMallocDefault) != hipSuccess) {
+    h->pinned = nullptr;
     return nullptr;
   }
-  return &h;
+  return h;
 }
 
 // The launch header's status words into st (one read-back on `stream`).
@@ -1379,9 +1515,9 @@ static int status_from_header(const unsigned int *st, int64_t *totals) {
   if (totals) {
     unsigned long long c, e;
     memcpy(&c, st + H_NCAND, 8);
-    memcpy(&e, st + 16, 8);
+    memcpy(&e, st + H_NENT, 8);
     totals[0] = (int64_t)c;  // candidates (sum of n_cand)
-    totals[1] = (int64_t)e;  // bucket entries (every contribution is one entry of its candidate's bucket)
+    totals[1] = (int64_t)e;  // bucket entries (distinct (node, candidate) pairs where phase B merged them)
   }
   if (st[H_STATUS] & 2u) {
     const unsigned bits = st[H_ERRBITS];
@@ -1548,6 +1684,28 @@ int rnnl_predictorplus_forward_rotate(rnnl_graph g, rnnl_rules r, const rnnl_pre
     return rc;
   }
   return rnnl_forward_status_flags(ws, main, totals, flags);
+}
+
+// Where this thread's forward resources for graph g live (the N-GPU bench's
+// self-check): out[0] = the graph's device, out[1] / out[2] = the devices of
+// the side streams A / B of g's device (-1: not created yet), out[3] = the
+// number of devices this thread holds forward resources for.
+int rnnl_forward_host_info(rnnl_graph g, int32_t *out) {
+  if (!g || !out) {
+    set_error("rnnl_forward_host_info: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  out[0] = g->device;
+  out[1] = out[2] = -1;
+  auto &all = host_sides();
+  auto it = all.find(g->device);
+  if (it != all.end()) {
+    int d = -1;
+    if (it->second.a && hipStreamGetDevice(it->second.a, &d) == hipSuccess) out[1] = d;
+    if (it->second.b && hipStreamGetDevice(it->second.b, &d) == hipSuccess) out[2] = d;
+  }
+  out[3] = (int32_t)all.size();
+  return RNNL_OK;
 }
 
 int rnnl_forward_flags_host(const void *header, uint32_t *flags) {

@@ -130,17 +130,65 @@ __global__ __launch_bounds__(BS) void rule_stats_kernel(KParams p, const int64_t
 // rules ending at one trie node share the count, so per node
 // grad_node[n] = sum over (q, t) of count_n(q, t) x grad_score[q, t].  One
 // workgroup per row (grid-stride): the row's contributions are summed in LDS
-// (fp64, one slot per node of the head's trie), then one global fp64 atomic
-// per (row, touched node).  The caller zero-fills grad_node.
+// (one slot per node of the head's trie), then one global atomic per (row,
+// touched node), both int64 fixed point (order-independent).  The caller
+// zero-fills grad_node.
+//
+// The launch's max |grad| at candidates and sum of their entries' path counts
+// (a max and an integer sum: order-independent), for the fixed-point scale.
+__global__ __launch_bounds__(BS) void predictor_bw_stats_kernel(KParams p, const float *__restrict__ grad) {
+  unsigned int m = 0u;
+  unsigned long long k = 0ull;
+  for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
+    const int nc = p.n_cand[q];
+    const int64_t qb = p.q_base[q];
+    for (int s = threadIdx.x; s < nc; s += BS) {
+      const int4 cr = p.cand[qb + s];
+      const float g = grad[(int64_t)q * p.g.E + cr.x];
+      if (g == 0.f) continue;
+      m = max(m, __float_as_uint(fabsf(g)));
+      for (int e = cr.y; e < cr.y + cr.z; ++e) k += (uint32_t)p.bent[e].y;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+    k += __shfl_xor(k, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
+    if (m) atomicMax(&hdr[H_BW_MAXG], m);
+    if (k) atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_BW_SUMK), k);
+  }
+}
+
+// 2^s with sum k x max |grad| x 2^s < 2^62 (bad: a non-finite gradient)
+__device__ __forceinline__ int pred_bw_scale(const KParams &p, bool &bad) {
+  const unsigned int *hdr = reinterpret_cast<const unsigned int *>(p.ws);
+  const unsigned int mb = hdr[H_BW_MAXG];
+  const unsigned long long k = *reinterpret_cast<const unsigned long long *>(hdr + H_BW_SUMK);
+  bad = mb >= 0x7f800000u;
+  const double total = (double)k * (double)__uint_as_float(mb);
+  return (bad || !(total > 0.0)) ? 0 : 61 - ilogb(total);
+}
+
+// Per row (one workgroup per query, grid-stride): G_n += count x grad at
+// (row, candidate) for the row's head trie in LDS, then added per node into
+// grad_node — as int64 fixed point at the launch's scale, so the sums do not
+// depend on the order of the adds (run-to-run bitwise); predictor_bw_fix_kernel
+// turns them into fp64.  A non-finite gradient takes fp64 sums instead (NaN /
+// inf reach the nodes the reference's would).
 __global__ __launch_bounds__(BS) void predictor_backward_kernel(KParams p, const float *__restrict__ grad, int ld,
-                                                                double *__restrict__ grad_node) {
-  extern __shared__ double s_g[];
+                                                                unsigned long long *__restrict__ grad_node) {
+  extern __shared__ unsigned long long s_g[];
+  bool bad;
+  const int sc = pred_bw_scale(p, bad);
   for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
     const int nc = p.n_cand[q];
     if (nc <= 0) continue;
     const int r = (int)p.all_r[q];
     const int root = p.rl.head_root[r], nh = min(p.rl.head_nodes[r], ld);
-    for (int i = threadIdx.x; i < nh; i += BS) s_g[i] = 0.0;
+    for (int i = threadIdx.x; i < nh; i += BS) s_g[i] = 0ull;
     __syncthreads();
     const int64_t qb = p.q_base[q];
     const float *__restrict__ gq = grad + (int64_t)q * p.g.E;
@@ -150,13 +198,33 @@ __global__ __launch_bounds__(BS) void predictor_backward_kernel(KParams p, const
       if (g == 0.0) continue;
       for (int e = cr.y; e < cr.y + cr.z; ++e) {
         const int2 be = p.bent[e];
-        atomicAdd(&s_g[be.x - root], (double)(uint32_t)be.y * g);
+        const double t = (double)(uint32_t)be.y * g;
+        if (bad)
+          atomicAdd(reinterpret_cast<double *>(&s_g[be.x - root]), t);
+        else
+          atomicAdd(&s_g[be.x - root], (unsigned long long)llrint(ldexp(t, sc)));
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nh; i += BS)
-      if (s_g[i] != 0.0) atomicAdd(&grad_node[root + i], s_g[i]);
+    for (int i = threadIdx.x; i < nh; i += BS) {
+      if (s_g[i] == 0ull) continue;
+      if (bad)
+        atomicAdd(reinterpret_cast<double *>(&grad_node[root + i]), __longlong_as_double((long long)s_g[i]));
+      else
+        atomicAdd(&grad_node[root + i], s_g[i]);
+    }
     __syncthreads();
+  }
+}
+
+// grad_node's int64 fixed-point sums -> fp64 in place (the zero fill is 0 in both)
+__global__ void predictor_bw_fix_kernel(KParams p, int n_nodes, unsigned long long *__restrict__ grad_node) {
+  bool bad;
+  const int sc = pred_bw_scale(p, bad);
+  if (bad) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_nodes; i += gridDim.x * blockDim.x) {
+    const long long v = (long long)grad_node[i];
+    if (v) reinterpret_cast<double *>(grad_node)[i] = ldexp((double)v, -sc);
   }
 }
 
@@ -292,8 +360,14 @@ int rnnl_predictor_backward(void *ws, int32_t nq, int32_t scale, const int32_t *
   p.rl = r->d;
   p.all_r = all_r;
   p.g.E = n_entities;
-  hipLaunchKernelGGL(predictor_backward_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(BS),
-                     (size_t)ld * 8, (hipStream_t)stream, p, grad_score, ld, grad_node);
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned nb = (unsigned)std::min<int64_t>(nq, 4096);
+  RNNL_HIP_CHECK(hipMemsetAsync(static_cast<unsigned char *>(ws) + 4 * H_BW_MAXG, 0, 16, st));
+  hipLaunchKernelGGL(predictor_bw_stats_kernel, dim3(nb), dim3(BS), 0, st, p, grad_score);
+  hipLaunchKernelGGL(predictor_backward_kernel, dim3(nb), dim3(BS), (size_t)ld * 8, st, p, grad_score, ld,
+                     reinterpret_cast<unsigned long long *>(grad_node));
+  hipLaunchKernelGGL(predictor_bw_fix_kernel, dim3((unsigned)std::min<int64_t>((r->d.n_nodes + 255) / 256, 1024)),
+                     dim3(256), 0, st, p, r->d.n_nodes, reinterpret_cast<unsigned long long *>(grad_node));
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -604,7 +604,10 @@ using namespace rnnl;
 // One thread per (entity, dim) for BW_EPT entities (stride 256, coalesced over
 // the transposed entity planes [D][2][ld]); the per-query sums over entities
 // are reduce-scattered over the wave (63 shuffles for 32 queries x 2 parts),
-// then over the block's waves in LDS, then one atomicAdd per (block, q, part).
+// then over the block's waves in LDS, then per (block, q, part) one value:
+// into d_hr_part[block][q][part D + d] (rnnl_rotate_param_grads: summed over
+// the blocks in block order by head_grad_kernel — deterministic) or, without
+// a partial buffer (rnnl_rotate_backward), one atomicAdd into d_hr.
 constexpr int BW_EPT = 4;
 constexpr int BW_BS = 256;
 
@@ -612,6 +615,7 @@ __global__ __launch_bounds__(BW_BS) void rotate_backward_kernel(const float *__r
                                                                 const float *__restrict__ hr,
                                                                 const float *__restrict__ g, int B, int E, int D,
                                                                 float *__restrict__ d_hr,
+                                                                float *__restrict__ d_hr_part,
                                                                 float *__restrict__ d_tail) {
   __shared__ float s_red[BW_BS / 64][64];
   const int d = blockIdx.y;
@@ -670,7 +674,13 @@ __global__ __launch_bounds__(BW_BS) void rotate_backward_kernel(const float *__r
 #pragma unroll
       for (int w2 = 0; w2 < BW_BS / 64; ++w2) t += s_red[w2][lane];
       const int q = q0 + (lane & 31);
-      if (q < B) atomicAdd(&d_hr[(int64_t)q * 2 * D + (lane < 32 ? d : D + d)], -t);
+      const int64_t j = (int64_t)q * 2 * D + (lane < 32 ? d : D + d);
+      if (q < B) {
+        if (d_hr_part)
+          d_hr_part[(int64_t)blockIdx.x * B * 2 * D + j] = -t;
+        else
+          atomicAdd(&d_hr[j], -t);
+      }
     }
     __syncthreads();
   }
@@ -729,7 +739,7 @@ __global__ void tail_rows_kernel(const float *__restrict__ d_tail, int E, int D,
 //   d remb[r][d] += (d s c - d c s) / div
 __global__ void head_grad_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D, float gamma,
                                  const int64_t *__restrict__ all_h, const int64_t *__restrict__ all_r, int nq,
-                                 const float *__restrict__ d_hr, float *__restrict__ d_eemb,
+                                 const float *__restrict__ d_hr_part, int nparts, float *__restrict__ d_eemb,
                                  float *__restrict__ d_remb) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= D) return;
@@ -738,7 +748,13 @@ __global__ void head_grad_kernel(const float *__restrict__ eemb, const float2 *_
     const int64_t h = all_h[q], r = all_r[q];
     const float rh = eemb[h * 2 * D + d], ih = eemb[h * 2 * D + D + d];
     const float2 cs = rtab[r * D + d];
-    const float gre = d_hr[(int64_t)q * 2 * D + d], gim = d_hr[(int64_t)q * 2 * D + D + d];
+    // d(h o r): rotate_backward_kernel's per-block partials, in block order
+    float gre = 0.f, gim = 0.f;
+    for (int b = 0; b < nparts; ++b) {
+      const float *pb = d_hr_part + (int64_t)b * nq * 2 * D + (int64_t)q * 2 * D;
+      gre += pb[d];
+      gim += pb[D + d];
+    }
     if (d_eemb) {
       d_eemb[h * 2 * D + d] += gre * cs.x + gim * cs.y;
       d_eemb[h * 2 * D + D + d] += gim * cs.x - gre * cs.y;
@@ -918,19 +934,21 @@ int rnnl_rotate_backward(const float *planes, int32_t ld, const float *hr, const
   if (nq == 0) return RNNL_OK;
   const unsigned bx = (unsigned)((E + BW_BS * BW_EPT - 1) / (BW_BS * BW_EPT));
   hipLaunchKernelGGL(rotate_backward_kernel, dim3(bx, (unsigned)D), dim3(BW_BS), 0, (hipStream_t)stream, planes, ld,
-                     hr, grad, nq, E, D, d_hr, d_tail);
+                     hr, grad, nq, E, D, d_hr, (float *)nullptr, d_tail);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
 
 static size_t grads_hr_bytes(int64_t nq, int D) { return ((size_t)nq * 2 * D * sizeof(float) + 255) / 256 * 256; }
+static unsigned bw_blocks(int E) { return (unsigned)((E + BW_BS * BW_EPT - 1) / (BW_BS * BW_EPT)); }
 
 int rnnl_rotate_param_grads_scratch(int32_t nq, int32_t E, int32_t D, int32_t with_eemb, size_t *bytes) {
   if (nq < 0 || E <= 0 || D <= 0 || !bytes) {
     set_error("rnnl_rotate_param_grads_scratch: bad arguments");
     return RNNL_ERR_INVALID;
   }
-  *bytes = 2 * grads_hr_bytes(nq, D) + (with_eemb ? (size_t)2 * D * E * sizeof(float) : 0);
+  // hr | the entity blocks' d(h o r) partials | d_tail
+  *bytes = (1 + bw_blocks(E)) * grads_hr_bytes(nq, D) + (with_eemb ? (size_t)2 * D * E * sizeof(float) : 0);
   return RNNL_OK;
 }
 
@@ -953,20 +971,21 @@ int rnnl_rotate_param_grads(const float *eemb, const float *planes, int32_t ld, 
     return RNNL_OK;
   }
   unsigned char *ws = static_cast<unsigned char *>(scratch);
+  const unsigned bx = bw_blocks(E);
   float *hr = reinterpret_cast<float *>(ws);
-  float *d_hr = reinterpret_cast<float *>(ws + grads_hr_bytes(nq, D));
-  float *d_tail = d_eemb ? reinterpret_cast<float *>(ws + 2 * grads_hr_bytes(nq, D)) : nullptr;
+  // per entity block a partial d(h o r) (every entry written: no fill), summed
+  // in block order by head_grad_kernel — no atomics, run-to-run bitwise
+  float *d_hr_part = reinterpret_cast<float *>(ws + grads_hr_bytes(nq, D));
+  float *d_tail = d_eemb ? reinterpret_cast<float *>(ws + (1 + bx) * grads_hr_bytes(nq, D)) : nullptr;
   hipLaunchKernelGGL(hr_rows_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)nq), dim3(256), 0, st, eemb,
                      (const float2 *)rtab, D, all_h, all_r, hr);
-  RNNL_HIP_CHECK(hipMemsetAsync(d_hr, 0, (size_t)nq * 2 * D * sizeof(float), st));
-  const unsigned bx = (unsigned)((E + BW_BS * BW_EPT - 1) / (BW_BS * BW_EPT));
   hipLaunchKernelGGL(rotate_backward_kernel, dim3(bx, (unsigned)D), dim3(BW_BS), 0, st, planes, ld, hr, grad, nq, E, D,
-                     d_hr, d_tail);
+                     (float *)nullptr, d_hr_part, d_tail);
   if (d_eemb)
     hipLaunchKernelGGL(tail_rows_kernel, dim3((unsigned)((D + 31) / 32), (unsigned)((E + 31) / 32)), dim3(256), 0, st,
                        d_tail, E, D, d_eemb);
   hipLaunchKernelGGL(head_grad_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, st, eemb,
-                     (const float2 *)rtab, D, gamma, all_h, all_r, nq, d_hr, d_eemb, d_remb);
+                     (const float2 *)rtab, D, gamma, all_h, all_r, nq, d_hr_part, (int)bx, d_eemb, d_remb);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

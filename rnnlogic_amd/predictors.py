@@ -922,6 +922,15 @@ class _PlusSumTrain(torch.autograd.Function):
             mask8 = torch.empty((nq, E), dtype=torch.uint8, device=device)
         model.check_deferred(keep=1)
         pre = model._prefetched(device, *raw) if raw is not None else None
+        if pre is not None:
+            # the node records' range flag (trailer word 2: a non-finite or
+            # >= 2^30 aggregate), copied behind rnnl_node_weights*: checked
+            # below before the lookahead's scores are used, so that such a
+            # batch takes the one-call path and its RNNL_ERR_RANGE fallback
+            # (the exact COO path) exactly as without the lookahead
+            nflag, nflag_ev = model._node_flag_slot(device)
+            nflag.copy_(node_w[nbytes.value - 64 + 8:nbytes.value - 64 + 12], non_blocking=True)
+            nflag_ev.record()
         if pre is not None:  # grounded ahead (prefetch): the scoring half only
             _, _, _, ws, scale, n_cand_pf, ev, _, hdr = pre
             ev.synchronize()  # that grounding and its header copy, not the later side-stream work
@@ -938,8 +947,14 @@ class _PlusSumTrain(torch.autograd.Function):
                 _native.call("rnnl_predictorplus_score", g, nr.ptr, ctypes.byref(p), all_h.data_ptr(),
                              all_r.data_ptr(), nq, score.data_ptr(), mask8.data_ptr() if mask8 is not None else None,
                              n_cand_pf.data_ptr(), None, ws.data_ptr(), ws.numel(), scale, 0, 0, stream)
-                model._defer_status(device, ws)  # the scoring pass's range flags, read two forwards later
-                n_cand = n_cand_pf
+                nflag_ev.synchronize()  # (the node records only: the scoring pass runs on)
+                if int(nflag.view(torch.int32)[0]) == 0:
+                    # the scoring pass's remaining range flag (a candidate's
+                    # counts past the exact int64 sums), read two forwards later
+                    model._defer_status(device, ws)
+                    n_cand = n_cand_pf
+                else:  # out of the records' range: the one-call path raises RNNL_ERR_RANGE
+                    pre = None
             else:  # overflow (or another failure): the one-call path, with its retry
                 pre = None
         if pre is None:
@@ -987,6 +1002,9 @@ class _PlusSumTrain(torch.autograd.Function):
             ws, scale = model._launch(device, nq, run)
         gs = grad_score.float().contiguous()
         sb = model._backward_scratch(device)
+        nrb = ctypes.c_size_t()
+        _native.call("rnnl_predictorplus_backward_rows_size", nq, ctx.n_total, ctypes.byref(nrb))
+        rows_sb = torch.empty(max(nrb.value, 4), dtype=torch.uint8, device=device)
         outs = [torch.empty_like(emb_d)] + [torch.empty_like(t) for t in ws_]
         gr = _native.SumGrads()
         gr.emb, gr.emb_ld = outs[0].data_ptr(), 16
@@ -994,8 +1012,8 @@ class _PlusSumTrain(torch.autograd.Function):
             [t.data_ptr() for t in outs[1:]]
         _native.call("rnnl_predictorplus_backward", g, nr.ptr, ctypes.byref(p), emb_d.data_ptr(), 16,
                      all_r.data_ptr(), nq, gs.data_ptr(), n_cand.data_ptr(), ctx.n_total, ws.data_ptr(), ws.numel(),
-                     scale,
-                     ctx.head, sb.data_ptr(), sb.numel(), ctypes.byref(gr), stream)
+                     scale, ctx.head, sb.data_ptr(), sb.numel(), rows_sb.data_ptr(), rows_sb.numel(),
+                     ctypes.byref(gr), stream)
         grads = [o if ctx.needs_input_grad[8 + k] else None for k, o in enumerate(outs)]
         return (None,) * 7 + (g_base,) + tuple(grads)
 
@@ -1183,6 +1201,11 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         self._native_rules = {}
         self._node_cache = {}
         self._tok_cache = {}
+        # scratch sized by the old rules' trie (encoder state, backward, the
+        # parameter block) and groundings of the old rules queued ahead
+        self._side = {}
+        self._pf = {}
+        self.__dict__.pop("_src_lists", None)
 
     def encode_rules(self, rule_features):
         """LSTM/GRU/RNN output at each rule's last token (predictors.py:201-208)."""
@@ -1466,6 +1489,8 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                              all_r.data_ptr(), nq, score.data_ptr(), mask8.data_ptr() if mask8 is not None else None,
                              n_cand.data_ptr(), digest.data_ptr() if digest is not None else None, ws.data_ptr(),
                              ws.numel(), scale, 0, 0, stream)
+                # a grounding saved for a training backward in this workspace is now stale
+                self._ws_touch(ws)
             else:
                 scale = self.capacity_scale
                 ws = self._workspace(device, nq, scale)
@@ -1477,6 +1502,7 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                              mask8.data_ptr() if mask8 is not None else None, n_cand.data_ptr(),
                              digest.data_ptr() if digest is not None else None, ws.data_ptr(), ws.numel(), scale,
                              stream)
+                self._ws_touch(ws)
             rec("end")
             rc = self._status(ws, stream)
             if rc == _native.RNNL_ERR_OVERFLOW and self.capacity_scale < 64:
@@ -1624,6 +1650,15 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         _native.call("rnnl_predictorplus_ground", g, nr.ptr, _native.AGG_SUM, h.data_ptr(), r.data_ptr(),
                      etr.data_ptr() if etr is not None else None, nq, n_cand.data_ptr(), ws.data_ptr(), ws.numel(),
                      scale, 0, stream)
+
+    def _node_flag_slot(self, device):
+        """(pinned int32, event): the host copy of a node-record table's range
+        flag for the lookahead training forward (waited on within the call)."""
+        key = ("nflag", self._device_index(device))
+        v = self._side.get(key)
+        if v is None:
+            v = self._side[key] = (torch.zeros(4, dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
+        return v
 
     def _backward_scratch(self, device):
         key = ("bwd", self._device_index(device))

@@ -143,9 +143,11 @@ def test_path_count_above_2_31_matches_oracle(tmp_path, dev, aggregator, m, w5):
                                            ref.Rules(rules, g.relation_size), np.asarray([0]), np.asarray([0]), None)
     assert np.array_equal(mask.cpu().numpy(), wmask)
     np.testing.assert_allclose(score.cpu().numpy(), want, atol=1e-4, rtol=1e-5)
-    # the training path's COO carries the same u32 count (not a negative int32)
+    # the training path's COO carries the same u32 count (not a negative int32):
+    # the rule's one (candidate, node) entry, its w5 paths' counts merged in
+    # phase B into the reference's single rule_count cell (w5 x m^4 < 2^32)
     row, ent, ce, node, count = model.ground_coo(torch.tensor([0], device=dev), torch.tensor([0], device=dev))
-    assert sorted(set(ent.tolist())) == [graph.entity_size - 1] and count.tolist() == [m ** 4] * w5
+    assert sorted(set(ent.tolist())) == [graph.entity_size - 1] and count.tolist() == [w5 * m ** 4]
 
 
 @pytest.mark.parametrize("aggregator", ["sum", "pna"])

@@ -145,3 +145,17 @@ def test_device_eval_batches_tables():
         for k, v in list(lists.items())[::13]:
             i = np.searchsorted(keys, k)
             assert keys[i] == k and list(vals[offs[i]:offs[i + 1]]) == v
+
+
+def test_host_resources_keyed_by_stream_device(tmp_path):
+    """The forward's per-device host resources (pinned header, side streams)
+    are keyed by the device of the call's stream, not the thread's current
+    device, and the current device is restored (csrc/hostside.h, as used by
+    ground.hip's entry points) — with a mock device API, no GPU."""
+    import subprocess
+    exe = str(tmp_path / "hostside_keying")
+    src = os.path.join(REPO, "tests", "native", "hostside_keying.cpp")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(REPO, "rnnlogic_amd", "csrc"), src,
+                    "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr

@@ -49,6 +49,9 @@ nch = chunk.max() + 1
 cmax = np.zeros(nch, dtype=np.int64)
 np.maximum.at(cmax, chunk, nent)
 print("candidates %d, entries %d (%.2f per candidate), chunks %d" % (C, P, P / C, nch))
+nn = max(model.native_rules(dev).n_nodes, 1)
+distinct = len(np.unique(ce.cpu().numpy().astype(np.int64) * nn + node.cpu().numpy()))
+print("distinct (candidate, trie node) pairs %d: entries / distinct = %.4f" % (distinct, P / distinct))
 print("entries per candidate: p50 %d p90 %d p99 %d p99.9 %d max %d" % tuple(
     np.percentile(nent, [50, 90, 99, 99.9]).tolist() + [nent.max()]))
 print("lane-per-candidate walk: sum over chunks of max entries %d (%.1f per chunk; %.1fx the entries / 64)"
