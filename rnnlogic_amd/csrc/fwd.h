@@ -33,7 +33,7 @@ constexpr int MAXE_BITS = 19;   // |E| <= 2^MAXE_BITS
 // consecutive windows fill LDS hash passes (which merge a candidate's
 // duplicate (node, entity) entries) and only a window of more than HB_LOAD
 // contributions takes the dense direct-mapped pass.
-constexpr int SORT_WINS = 1024;
+constexpr int SORT_WINS = 256;
 constexpr int MAX_SBITS = MAXE_BITS - 10;  // 2^MAXE_BITS / SORT_WINS entities per window at most
 static_assert((1 << MAX_SBITS) <= WIN, "a sort window must fit the dense pass's direct map");
 constexpr int HB = WIN;                // phase-B candidate hash slots

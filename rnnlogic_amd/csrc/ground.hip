@@ -69,7 +69,8 @@ struct __align__(16) SmemT {
   };
   int ws[(G / 64) + 1];
   int q, nd, np, ovf, err, root, nocc;
-  int nent;  // bucket entries of the current query written so far (phase B)
+  int nent;   // the query's pool entries used by its passes so far (phase B)
+  int nreal;  // of which bucket entries (a merged short bucket leaves a gap behind it)
   long long qbase;
   unsigned long long t0;
   int whist[SORT_WINS], wbeg[SORT_WINS + 1], wfill[SORT_WINS];
@@ -293,8 +294,12 @@ __device__ __forceinline__ int scan_win(int *a, int *s_ws) {
 
 // One entity window [lo, lo + WIN) whose contributions are w[beg, end):
 // candidate records for it are written at pool indices cbase + [0, nc) and
-// its buckets at pool indices qbase + beg + [0, end - beg).  degree_only (PNA
-// sweep 1) accumulates sum log(degree) instead.  Returns nc.
+// its buckets at pool indices qbase + nent + [0, end - beg).  degree_only
+// (PNA sweep 1) accumulates sum log(degree) instead.  Returns nc.
+// (Duplicate (node, entity) contributions stay separate entries here: a
+// register merge of buckets of up to 4 / 8 entries removed 2.5 M / 7 M of
+// FB15k-237's 26 M duplicates for +0.3 / +0.45 ms on the bias step —
+// tools/sort_ab.py)
 template <int G>
 __device__ int window_pass(const KParams &p, SmemT<G> &S, const Ent *w, int lo, int beg, int end, int64_t cbase,
                            bool degree_only) {
@@ -337,12 +342,8 @@ __device__ int window_pass(const KParams &p, SmemT<G> &S, const Ent *w, int lo, 
   for (int i = tid; i < WIN; i += G) S.u.b.off[i] = S.u.b.cnt[i];
   __syncthreads();
   scan_win<G>(S.u.b.off, S.ws);
-  // candidate records; the pass's entries follow the query's earlier ones
+  // the pass's entries follow the query's earlier ones
   const int64_t qb = S.qbase + S.nent;
-  for (int s2 = tid; s2 < nc; s2 += G) {
-    p.cand[cbase + s2] = make_int4(S.u.b.st[s2], (int32_t)(qb + S.u.b.off[s2]), S.u.b.cnt[s2], 0);
-  }
-  __syncthreads();
   for (int i = tid; i < WIN; i += G) S.u.b.cnt[i] = 0;
   __syncthreads();
   PSTAMP(1);
@@ -352,7 +353,14 @@ __device__ int window_pass(const KParams &p, SmemT<G> &S, const Ent *w, int lo, 
     p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
   }
   __syncthreads();
-  if (tid == 0) S.nent += end - beg;
+  // candidate records (bucket sizes: the fill counters)
+  for (int s2 = tid; s2 < nc; s2 += G)
+    p.cand[cbase + s2] = make_int4(S.u.b.st[s2], (int32_t)(qb + S.u.b.off[s2]), S.u.b.cnt[s2], 0);
+  __syncthreads();
+  if (tid == 0) {
+    S.nent += end - beg;
+    S.nreal += end - beg;
+  }
   __syncthreads();
   PSTAMP(2);
   return nc;
@@ -512,7 +520,10 @@ __device__ int hash_pass(const KParams &p, SmemT<G> &S, const Ent *w, int beg, i
     p.bent[pos] = make_int2(S.root + (int)(w[i].k >> p.ebits), (int)w[i].c);
   }
   __syncthreads();
-  if (tid == 0) S.nent += end - beg;
+  if (tid == 0) {
+    S.nent += end - beg;
+    S.nreal += end - beg;
+  }
   __syncthreads();
   return nc;
 }
@@ -624,7 +635,10 @@ __device__ int hash_pass_merged(const KParams &p, SmemT<G> &S, const Ent *w, int
     }
   }
   __syncthreads();
-  if (tid == 0) S.nent += nd;
+  if (tid == 0) {
+    S.nent += nd;
+    S.nreal += nd;
+  }
   __syncthreads();
   return nc;
 }
@@ -642,6 +656,9 @@ __device__ int candidates_phase(const KParams &p, SmemT<G> &S, const Slot &sl, i
   if (P <= HB_LOAD) return P > 0 ? hash_pass(p, S, sl.ct, 0, P, S.qbase, degree_only, 0, p.g.E) : 0;
   const int sb = p.sbits;
   const int nwin = (p.g.E + (1 << sb) - 1) >> sb;
+  // a graph of at most one window (kinship, UMLS): the dense pass over the
+  // raw list, without the window-sorted copy
+  if (nwin == 1) return window_pass(p, S, sl.ct, 0, 0, P, S.qbase, degree_only);
   if (!sorted) {
     for (int i = tid; i < nwin; i += G) S.whist[i] = 0;
     __syncthreads();
@@ -705,7 +722,8 @@ __device__ __forceinline__ void flag_error(const KParams &p, unsigned int *hdr, 
 }
 
 template <int AGG, int G>
-__global__ __launch_bounds__(G) void ground_kernel(KParams p) {
+// (512 / 1024 lanes: 4 waves per SIMD, two / one workgroups per CU: <= 128 VGPRs)
+__global__ __launch_bounds__(G, G >= 512 ? 4 : 1) void ground_kernel(KParams p) {
   __shared__ SmemT<G> S;
   const int tid = threadIdx.x;
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
@@ -756,6 +774,7 @@ __global__ __launch_bounds__(G) void ground_kernel(KParams p) {
       S.nocc = 0;
       S.ovf = 0;
       S.nent = 0;
+      S.nreal = 0;
       S.sumlog = 0ull;
     }
     __syncthreads();
@@ -802,7 +821,7 @@ __global__ __launch_bounds__(G) void ground_kernel(KParams p) {
     } else if (tid == 0) {
       p.n_cand[q] = ncand;
       atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_NCAND), (unsigned long long)ncand);
-      atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_NENT), (unsigned long long)S.nent);
+      atomicAdd(reinterpret_cast<unsigned long long *>(hdr + H_NENT), (unsigned long long)S.nreal);
       p.q_base[q] = S.qbase;
       if (p.prof) {
         pr[2] += __builtin_amdgcn_s_memtime() - t_a;
@@ -1055,15 +1074,30 @@ __global__ void export_candidates_kernel(KParams p, const int64_t *__restrict__ 
   }
 }
 
-__global__ void export_entries_kernel(KParams p, const int64_t *__restrict__ ent_off, int32_t *__restrict__ out_node,
-                                      int32_t *__restrict__ out_count) {
+// per query a block: its candidates' buckets in candidate order (a merged
+// short bucket leaves a gap behind it in the pool), output offsets by a block
+// scan of the bucket lengths
+constexpr int EXP_BS = 256;
+__global__ __launch_bounds__(EXP_BS) void export_entries_kernel(KParams p, const int64_t *__restrict__ ent_off,
+                                                                int32_t *__restrict__ out_node,
+                                                                int32_t *__restrict__ out_count) {
+  __shared__ int s_ws[EXP_BS / 64 + 1];
   for (int q = blockIdx.x; q < p.nq; q += gridDim.x) {
-    if (p.n_cand[q] <= 0) continue;
-    const int64_t qb = p.q_base[q], o = ent_off[q], n = ent_off[q + 1] - o;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const int2 be = p.bent[qb + i];
-      out_node[o + i] = be.x;
-      out_count[o + i] = be.y;
+    const int nc = p.n_cand[q];  // block-uniform
+    if (nc <= 0) continue;
+    const int64_t qb = p.q_base[q];
+    int64_t o = ent_off[q];
+    for (int base = 0; base < nc; base += EXP_BS) {
+      const int s = base + (int)threadIdx.x;
+      const int4 cr = s < nc ? p.cand[qb + s] : make_int4(0, 0, 0, 0);
+      int total;
+      const int at = block_scan<EXP_BS>(cr.z, s_ws, total);
+      for (int i = 0; i < cr.z; ++i) {
+        const int2 be = p.bent[cr.y + i];
+        out_node[o + at + i] = be.x;
+        out_count[o + at + i] = be.y;
+      }
+      o += total;
     }
   }
 }
@@ -1126,9 +1160,13 @@ int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all
   p.g = g->d;
   p.ebits = ebits;
   p.emask = (uint32_t)((1u << ebits) - 1u);
-  p.sbits = 0;
-  while (((int64_t)g->d.E + (1ll << p.sbits) - 1) >> p.sbits > SORT_WINS) ++p.sbits;
-  if (g_sort_bits >= p.sbits && g_sort_bits <= WBITS) p.sbits = g_sort_bits;
+  // phase B's sort windows: WIN entities (finer windows merge more duplicate
+  // entries in hash passes but cost more passes: FB15k-237 bias step 9.2 ms at
+  // 2048 entities, 9.8 at 256, 11.1 at 16 — tools/sort_ab.py)
+  int min_bits = 0;
+  while (((int64_t)g->d.E + (1ll << min_bits) - 1) >> min_bits > SORT_WINS) ++min_bits;
+  p.sbits = std::max(min_bits, WBITS);
+  if (g_sort_bits >= min_bits && g_sort_bits <= WBITS) p.sbits = g_sort_bits;
   p.rl = r->d;
   p.all_h = all_h;
   p.all_r = all_r;
@@ -1408,7 +1446,7 @@ int rnnl_ground_export_entries(void *ws, int32_t nq, int32_t scale, const int32_
   }
   if (nq == 0) return RNNL_OK;
   const KParams p = export_params(ws, nq, scale, n_cand);
-  hipLaunchKernelGGL(export_entries_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0,
+  hipLaunchKernelGGL(export_entries_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(EXP_BS), 0,
                      (hipStream_t)stream, p, ent_off, out_node, out_count);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Builds compile-flag variants of one kernel source (ground.hip or rotate.hip)
 # into rnnlogic_amd/_build/variants/<name>.so, for A/B runs through
-# tools/ab_run.py (e.g. VAR=LIB VALS="rnnlogic_amd/_build/variants/a.so ..."
-# bash tools/env_ab.sh).
+# tools/ab_run.py (python tools/ab_run.py rnnlogic_amd/_build/variants/a.so
+# tools/sort_ab.py ...: the same script against each build in one GPU call).
 # Usage: tools/build_variants.sh <source>.hip name "flags" [name "flags" ...]
 set -e
 src=$1
