@@ -453,6 +453,42 @@ def train_step_line(model, solver, dev, n_steps=10, warmup=2):
                     "Adam): forward + loss + backward + step, each step synchronised"}
 
 
+def wn18rr_train_line(dev, n_steps=10, warmup=3):
+    """Config 3's training step: TrainerPredictor.train_step on WN18RR train
+    batches (B = 32, edge removal, Adam) for PredictorPlus(emb, 3, 16, pna) +
+    RotatE(D = 500) — FuncToNode's statistics and their backward on the HIP
+    path (predictors._PnaStats, csrc/pna_grad.hip), beside the same steps
+    through torch autograd over the exported grounding COO (the round-5 path)."""
+    from rnnlogic_amd.trainer import TrainerPredictor
+    path = datasets.materialize("wn18rr", with_rotate=True)
+    random.seed(1)
+    np.random.seed(1)
+    torch.manual_seed(1)
+    with contextlib.redirect_stdout(sys.stderr):
+        graph = KnowledgeGraph(path)
+        train_set = TrainDataset(graph, 32)
+        ValidDataset(graph, 32)
+        test_set = TestDataset(graph, 32)
+        model = PredictorPlus(graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="RotatE",
+                              aggregator="pna", embedding_path=datasets.rotate_path("wn18rr"))
+        model.set_rules(datasets.rule_file("wn18rr"))
+    model = model.to(dev)
+    model.train_set = train_set
+    solver = TrainerPredictor(model, train_set, None, test_set, None, gpus=[dev.index or 0])
+    # a first pass over the batches: the dense layers' GEMM shapes (one per
+    # candidate count) are selected on first use, for both paths alike
+    train_step_line(model, solver, dev, n_steps=n_steps, warmup=warmup)
+    model.fused_backward = False
+    coo = train_step_line(model, solver, dev, n_steps=n_steps, warmup=warmup)
+    model.fused_backward = True
+    out = train_step_line(model, solver, dev, n_steps=n_steps, warmup=warmup)
+    out["autograd_coo_ms_per_batch"] = coo["ms_per_batch"]
+    out["note"] = ("TrainerPredictor.train_step on WN18RR train batches (B=32, edge removal, RotatE D=500 trainable, "
+                   "Adam), each step synchronised: PNA statistics + backward in HIP (csrc/pna_grad.hip); "
+                   "autograd_coo_ms_per_batch: the same steps through torch autograd over the grounding COO")
+    return out
+
+
 def recorded_em_full(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                         "r05_em_full_fb.json")):
     """Config 5 end to end (tools/em_full_fb.py: the whole run_rnnlogic.py flow
@@ -811,6 +847,7 @@ def main():
         if args.feature == "RotatE":
             extra["shard_balance"] = shard_balance_line(model, test_set, dev, elapsed / args.steps * 1e3)
         extra["wn18rr_forward"] = wn18rr_line(dev)
+        extra["wn18rr_train_step"] = wn18rr_train_line(dev)
         extra["kinship_forward"] = kinship_line(dev)
         # end-to-end evaluate('test') (trainer.py:145-248): device rows + filter
         # flags, one forward over the split, device ranks, host metrics

@@ -604,6 +604,38 @@ int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor
                                 int32_t capacity_scale, int32_t head, void *scratch, size_t scratch_bytes,
                                 void *rows_scratch, size_t rows_bytes, const rnnl_sum_grads *grads, void *stream);
 
+/* PNA (FuncToNode) training path (reference src/layers.py:89-101 under
+ * autograd): the per-candidate statistics of the grounding in `workspace`
+ * (after rnnl_ground / rnnl_predictorplus_ground), candidates in row-major
+ * order at cand_off[q] = exclusive prefix of n_cand (n_queries + 1):
+ *   wsum / wsq (C x 16) = sum over the candidate's (node, count) entries of
+ *     count x (sum over the node's rules of x / of x^2) — exact, one rounding,
+ *   mn / mx (C x 16) = min / max of x over the rules reaching it,
+ *   deg (C) = 1 + sum of count x rules, row / ent (C) its row and entity,
+ *   row_scale (n_queries) = the row's mean log(deg) over its candidates
+ *     (layers.py:108-114, one order-free fixed-point sum; 0 without any).
+ * node_w: rnnl_node_weights(..., RNNL_AGG_PNA, ...) of the same embeddings.
+ * A table the fixed-point records cannot hold, or a candidate past 2^33
+ * paths, sets the workspace header's range bits (rnnl_forward_status:
+ * RNNL_ERR_RANGE).
+ * rnnl_pna_features_backward: d_x (n_rules x 16, written whole) from the
+ * gradients of the four statistics — per node sum count x gradient, min / max
+ * split evenly among tied entries then tied rules (torch scatter_reduce amin /
+ * amax), int64 fixed point at one scale per launch: run-to-run bitwise.
+ * head >= 0: every row is of that relation (only its trie is touched), -1:
+ * any rows.  scratch: rnnl_pna_features_backward_scratch bytes. */
+int rnnl_pna_features(rnnl_rules r, const void *node_w, void *workspace, int32_t n_queries, int32_t capacity_scale,
+                      const int32_t *n_cand, const int64_t *cand_off, int64_t n_cand_total, float *wsum, float *wsq,
+                      float *mn, float *mx, float *deg, int64_t *row, int64_t *ent, float *row_scale,
+                      void *row_scratch /* n_queries x 8 bytes */, void *stream);
+int rnnl_pna_features_backward_scratch(rnnl_rules r, size_t *bytes);
+int rnnl_pna_features_backward(rnnl_rules r, const void *node_w, const float *x, int32_t ld, void *workspace,
+                               int32_t n_queries, int32_t capacity_scale, const int64_t *all_r, const int32_t *n_cand,
+                               const int64_t *cand_off, int64_t n_cand_total, const float *mn, const float *mx,
+                               const float *d_wsum,
+                               const float *d_wsq, const float *d_mn, const float *d_mx, int32_t head, void *scratch,
+                               size_t scratch_bytes, float *d_x, void *stream);
+
 /* ------------------------------------------------ 64-bit path counts --
  * Rows whose path counts (or PNA degree) reach 2^32 fail the forward with
  * RNNL_ERR_RANGE (the grounding kernel sums u32) and n_cand = -2; the

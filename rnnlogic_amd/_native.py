@@ -117,6 +117,12 @@ SIGNATURES = [
     ("rnnl_forward_error_bits", ctypes.c_int, [_P, _P, _P]),
     ("rnnl_predictorplus_backward_size", ctypes.c_int, [_P, _I32, _P]),
     ("rnnl_predictorplus_backward_rows_size", ctypes.c_int, [_I32, _I64, _P]),
+    ("rnnl_pna_features", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                         _P]),
+    ("rnnl_pna_features_backward_scratch", ctypes.c_int, [_P, _P]),
+    ("rnnl_pna_features_backward", ctypes.c_int,
+     [_P, _P, _P, _I32, _P, _I32, _I32, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _I32, _P, ctypes.c_size_t, _P,
+      _P]),
     ("rnnl_predictorplus_backward", ctypes.c_int,
      [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I64, _P, ctypes.c_size_t, _I32, _I32, _P, ctypes.c_size_t, _P,
       ctypes.c_size_t, _P, _P]),

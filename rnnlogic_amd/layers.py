@@ -82,11 +82,13 @@ class FuncToNode(nn.Module):
         mx = torch.where(active, xb, torch.full_like(xb, float("-inf"))).max(1)[0]
         return self.finish(At.matmul(x_f), At.matmul(x_f * x_f), mn, mx, deg, b_n, int(b_n.max().item()) + 1)
 
-    def finish(self, wsum, wsq, mn, mx, deg, b_n, n_batch):
+    def finish(self, wsum, wsq, mn, mx, deg, b_n, n_batch, row_scale=None):
         """The PNA block from its sufficient statistics per candidate:
         count-weighted sums of x and x^2 (C, H), unweighted min/max over the
         candidate's rules (C, H), degree = 1 + sum of counts (C,), and the
-        candidate's batch row b_n (C,)."""
+        candidate's batch row b_n (C,).  row_scale (n_batch,): the rows' mean
+        log-degree when the caller has it (the HIP statistics' order-free sum;
+        else the per-row index_add below)."""
         eps = self.eps
         deg = deg.unsqueeze(-1)
         mean = wsum / deg.clamp(min=eps)
@@ -94,9 +96,12 @@ class FuncToNode(nn.Module):
         std = (sq_mean - mean * mean).clamp(min=eps).sqrt()
         feats = torch.cat([mean, mn, mx, std], -1)     # (C, 4H)
         s = deg.log()
-        s_sum = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add(0, b_n, s.squeeze(-1))
-        s_cnt = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add(0, b_n, torch.ones_like(s.squeeze(-1)))
-        s = s / (s_sum / s_cnt.clamp(min=eps))[b_n].unsqueeze(-1).clamp(min=eps)
+        if row_scale is None:
+            s_sum = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add(0, b_n, s.squeeze(-1))
+            s_cnt = torch.zeros(n_batch, device=s.device, dtype=s.dtype).index_add(
+                0, b_n, torch.ones_like(s.squeeze(-1)))
+            row_scale = s_sum / s_cnt.clamp(min=eps)
+        s = s / row_scale[b_n].unsqueeze(-1).clamp(min=eps)
         scales = torch.cat([torch.ones_like(s), s, 1 / s.clamp(min=eps)], -1)  # (C, 3)
         upd = (feats.unsqueeze(-1) * scales.unsqueeze(-2)).flatten(-2)
         return torch.relu(self.layer_norm(self.add_model(upd)))

@@ -1018,6 +1018,81 @@ class _PlusSumTrain(torch.autograd.Function):
         return (None,) * 7 + (g_base,) + tuple(grads)
 
 
+class _PnaStats(torch.autograd.Function):
+    """FuncToNode's sufficient statistics (layers.py:89-101) on the HIP
+    grounding, under autograd: per candidate (row-major order) the
+    count-weighted sums of x and x^2, the min / max of x over the rules
+    reaching it, and (not differentiable) its degree, row and entity —
+    rnnl_pna_features after rnnl_node_weights(PNA) of the embedding table
+    `emb` (num_rules x 16) and rnnl_ground.  Backward:
+    rnnl_pna_features_backward (per node count x gradient sums, min / max as
+    torch's scatter_reduce amin / amax backward; int64 fixed point, run-to-run
+    bitwise).  The grounding stays in the model's workspace between the two;
+    if another launch has reused it by then, the rows are grounded again."""
+
+    @staticmethod
+    def forward(ctx, model, emb, all_h, all_r, etr, head):
+        device = all_h.device
+        nq = all_h.numel()
+        nr = model.native_rules(device)
+        emb_d = emb.detach().float().contiguous()
+        nbytes = ctypes.c_size_t()
+        _native.call("rnnl_node_weights_size", nr.ptr, _native.AGG_PNA, ctypes.byref(nbytes))
+        node_w = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if head >= 0:  # a one-relation batch: that head's trie only
+            _native.call("rnnl_node_weights_head", nr.ptr, head, emb_d.data_ptr(), 16, _native.AGG_PNA, None,
+                         node_w.data_ptr(), stream)
+        else:
+            _native.call("rnnl_node_weights", nr.ptr, emb_d.data_ptr(), 16, _native.AGG_PNA, None, node_w.data_ptr(),
+                         stream)
+        totals = np.zeros(2, dtype=np.int64)
+        ws, scale, n_cand = model.ground(all_h, all_r, etr, totals)
+        C = int(totals[0])
+        cand_off = torch.zeros(nq + 1, dtype=torch.int64, device=device)
+        torch.cumsum(n_cand.to(torch.int64), 0, out=cand_off[1:])
+        f32 = dict(dtype=torch.float32, device=device)
+        wsum, wsq, mn, mx = [torch.empty((C, 16), **f32) for _ in range(4)]
+        deg = torch.empty(C, **f32)
+        row = torch.empty(C, dtype=torch.int64, device=device)
+        ent = torch.empty(C, dtype=torch.int64, device=device)
+        row_scale = torch.zeros(nq, **f32)
+        if C:
+            lsum = torch.empty(nq, dtype=torch.int64, device=device)
+            _native.call("rnnl_pna_features", nr.ptr, node_w.data_ptr(), ws.data_ptr(), nq, scale, n_cand.data_ptr(),
+                         cand_off.data_ptr(), C, wsum.data_ptr(), wsq.data_ptr(), mn.data_ptr(), mx.data_ptr(),
+                         deg.data_ptr(), row.data_ptr(), ent.data_ptr(), row_scale.data_ptr(), lsum.data_ptr(), stream)
+            # the records' / sums' range bits: RNNL_ERR_RANGE -> the caller's COO path
+            _native.check(_native.lib().rnnl_forward_status(ws.data_ptr(), stream))
+        ctx.model, ctx.head, ctx.C = model, head, C
+        ctx.launch = (ws, scale, n_cand, cand_off, model._ws_uses.get(ws.data_ptr()), node_w, emb_d)
+        ctx.rows = (all_h, all_r, etr)
+        ctx.save_for_backward(mn, mx)
+        ctx.mark_non_differentiable(deg, row, ent, row_scale)
+        return wsum, wsq, mn, mx, deg, row, ent, row_scale
+
+    @staticmethod
+    def backward(ctx, g_wsum, g_wsq, g_mn, g_mx, *_):  # (deg, row, ent, row_scale: no gradient)
+        if ctx.C == 0 or not ctx.needs_input_grad[1]:
+            return (None,) * 6
+        model = ctx.model
+        mn, mx = ctx.saved_tensors
+        ws, scale, n_cand, cand_off, gen, node_w, emb_d = ctx.launch
+        all_h, all_r, etr = ctx.rows
+        device = all_h.device
+        if model._ws_uses.get(ws.data_ptr()) != gen:  # the workspace was reused: ground again (same COO)
+            ws, scale, n_cand = model.ground(all_h, all_r, etr)
+        grads = [g.float().contiguous() if g is not None else torch.zeros_like(mn) for g in (g_wsum, g_wsq, g_mn, g_mx)]
+        nr = model.native_rules(device)
+        d_x = torch.empty((model.num_rules, 16), dtype=torch.float32, device=device)
+        sb = model._pna_scratch(device)
+        _native.call("rnnl_pna_features_backward", nr.ptr, node_w.data_ptr(), emb_d.data_ptr(), 16, ws.data_ptr(),
+                     all_h.numel(), scale, all_r.data_ptr(), n_cand.data_ptr(), cand_off.data_ptr(), ctx.C, mn.data_ptr(),
+                     mx.data_ptr(), *[g.data_ptr() for g in grads], ctx.head, sb.data_ptr(), sb.numel(),
+                     d_x.data_ptr(), torch.cuda.current_stream(device).cuda_stream)
+        return None, d_x, None, None, None, None
+
+
 class _LstmRules(torch.autograd.Function):
     """PredictorPlus.encode_rules (predictors.py:201-208) for type 'lstm' under
     autograd: the top layer's output at each rule's last token for the rules
@@ -1600,6 +1675,12 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                 if e.code != _native.RNNL_ERR_RANGE:
                     raise
                 # past the fused kernels' integer ranges: the autograd COO path below
+        if self.fused and self.aggregator == "pna" and self.fused_backward and device.type == "cuda":
+            try:
+                return self._forward_pna_train(all_h, all_r, edges_to_remove, query_r)
+            except _native.NativeError as e:
+                if e.code != _native.RNNL_ERR_RANGE:
+                    raise
         row, ent, ce, node, count = self.ground_coo(all_h, all_r, edges_to_remove)
         if ent.numel() == 0:
             # predictors.py:230-237 early return
@@ -1640,6 +1721,45 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
                                    rte.add_model.layers[0].bias, rte.layer_norm.weight, rte.layer_norm.bias,
                                    sm.layers[0].weight, sm.layers[0].bias, sm.layers[1].weight, sm.layers[1].bias,
                                    self.relation_emb.weight)
+
+    @_native.on_input_device
+    def _forward_pna_train(self, all_h, all_r, edges_to_remove, query_r):
+        """forward_autograd for the PNA aggregator: FuncToNode's statistics
+        on the HIP grounding (_PnaStats: one kernel forward, one backward)
+        and its dense rest (layers.FuncToNode.finish) and score_model as
+        torch layers."""
+        device = all_h.device
+        nq, E = all_h.numel(), self.num_entities
+        etr = edges_to_remove.to(device, torch.int64).contiguous() if edges_to_remove is not None else None
+        all_h, all_r = all_h.contiguous(), all_r.contiguous()
+        head = int(query_r) if isinstance(query_r, int) else -1
+        if self.type == "emb":
+            emb = self.rule_emb
+        else:
+            rels = [head] if head >= 0 else torch.unique(all_r).tolist()
+            ridx = self._rule_ids(rels, device)
+            x_f = self._encode_rules_padded(ridx, device, rels)
+            emb = torch.zeros((self.num_rules, self.hidden_dim), dtype=x_f.dtype, device=device).index_copy(
+                0, ridx, x_f)
+        wsum, wsq, mn, mx, deg, row, ent, row_scale = _PnaStats.apply(self, emb, all_h, all_r, etr, head)
+        if ent.numel() == 0:  # predictors.py:230-237 early return
+            zero = torch.zeros((nq, E), device=device)
+            if self.entity_feature == "bias":
+                return zero + self.bias.unsqueeze(0), torch.ones((nq, E), dtype=torch.bool, device=device)
+            if self.entity_feature == "RotatE":
+                return zero + self.RotatE(all_h, all_r), torch.ones((nq, E), dtype=torch.bool, device=device)
+            return zero - float("-inf"), torch.zeros((nq, E), dtype=torch.bool, device=device)
+        out = self.rule_to_entity.finish(wsum, wsq, mn, mx, deg, row, nq, row_scale=row_scale)
+        return self._score_tail(all_h, all_r, row, ent, out, head=head)
+
+    def _pna_scratch(self, device):
+        key = ("pna_bwd", self._device_index(device))
+        sb = self._side.get(key)
+        if sb is None:
+            n = ctypes.c_size_t()
+            _native.call("rnnl_pna_features_backward_scratch", self.native_rules(device).ptr, ctypes.byref(n))
+            sb = self._side[key] = torch.empty(n.value, dtype=torch.uint8, device=device)
+        return sb
 
     def _prefetch_enabled(self):
         """The lookahead serves the fused SUM training forward only."""
@@ -1743,7 +1863,20 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
             mx = torch.full((C, H), float("-inf"), device=device, dtype=x_f.dtype).scatter_reduce(
                 0, idx_c, node_max.index_select(0, node), "amax", include_self=True)
             out = self.rule_to_entity.finish(wsum, wsq, mn, mx, deg, row, nq)
-        rel = self.relation_emb(all_r).index_select(0, row)  # per row, then per candidate
+        return self._score_tail(all_h, all_r, row, ent, out)
+
+    def _score_tail(self, all_h, all_r, row, ent, out, head=-1):
+        """predictors.py:251-271 from rule_to_entity's output (C, H) of the
+        candidates (row, ent): score_model, the scatter into (B, |E|) and the
+        entity feature / mask.  head >= 0: every row is of that relation (its
+        embedding broadcast: the gradient is a plain sum over the candidates,
+        not an index_add's atomics)."""
+        device = all_h.device
+        nq, E = all_h.numel(), self.num_entities
+        if head >= 0:
+            rel = self.relation_emb.weight[head].unsqueeze(0).expand(row.numel(), -1)
+        else:
+            rel = self.relation_emb(all_r).index_select(0, row)  # per row, then per candidate
         output = self.score_model(torch.cat([out, rel], dim=-1)).squeeze(-1)
         score = torch.zeros(nq * E, device=device, dtype=output.dtype).scatter(0, row * E + ent, output).view(nq, E)
         if self.entity_feature == "bias":

@@ -10,7 +10,8 @@ block in block order (rotate.hip head_grad_kernel), the SUM rule part's
 per-node gradients and the EM Predictor's are int64 fixed-point sums at
 one scale per launch (backward.hip node_accum_kernel, predictor.hip
 predictor_backward_kernel), and relation_emb's gradient of a one-relation
-batch is W0[:, 16:]^T dL/db0 in a fixed order (rel_grad_kernel).
+batch is W0[:, 16:]^T dL/db0 in a fixed order (rel_grad_kernel); the PNA
+statistics' backward sums in int64 fixed point too (pna_grad.hip).
 """
 import pytest
 import torch
@@ -83,3 +84,45 @@ def test_training_is_bitwise_repeatable(case, dev):
     assert a.keys() == b.keys()
     differ = [k for k in a if not torch.equal(a[k], b[k])]
     assert not differ, "%s: parameters differ between two identical runs: %s" % (case, differ)
+
+
+def test_pna_statistics_backward_is_bitwise_repeatable(dev):
+    """The PNA path (config 3) trains its dense layers (Linear(192, 16),
+    score_model) through torch GEMMs whose weight gradients reduce over every
+    candidate — the BLAS library may split that reduction with atomics, so
+    end-to-end training is not bitwise repeatable there.  The package's own
+    part is: the statistics' forward and backward (csrc/pna_grad.hip, int64
+    fixed-point node sums) give bitwise-equal rule-embedding gradients for the
+    same incoming gradients, over WN18RR training batches (edge removal)."""
+    import contextlib
+    import io
+
+    from rnnlogic_amd import datasets
+    from rnnlogic_amd.data import KnowledgeGraph, TrainDataset
+    from rnnlogic_amd.predictors import PredictorPlus, _PnaStats
+    torch.manual_seed(3)
+    with contextlib.redirect_stdout(io.StringIO()):
+        graph = KnowledgeGraph(datasets.materialize("wn18rr"))
+        ts = TrainDataset(graph, 32)
+        model = PredictorPlus(graph, type="emb", num_layers=3, hidden_dim=16, entity_feature="bias", aggregator="pna")
+        model.set_rules(datasets.rule_file("wn18rr"))
+    model = model.to(dev).train()
+    n_checked = 0
+    for i in range(0, len(ts), max(len(ts) // 8, 1)):
+        all_h, all_r, _, _, etr = [x.to(dev) for x in ts[i]]
+        head = int(all_r[0])
+        grads = []
+        for _ in range(2):
+            emb = model.rule_emb.detach().clone().requires_grad_()
+            wsum, wsq, mn, mx = _PnaStats.apply(model, emb, all_h, all_r, etr, head)[:4]
+            if wsum.numel() == 0:
+                break
+            g = torch.Generator(device=dev).manual_seed(i)
+            loss = sum((t * torch.randn(t.shape, generator=g, device=dev)).sum() for t in (wsum, wsq, mn, mx))
+            loss.backward()
+            grads.append(emb.grad.detach().cpu().view(torch.int32))
+        if len(grads) == 2:
+            assert torch.equal(grads[0], grads[1]), "batch %d: rule-embedding gradients differ between runs" % i
+            assert bool(grads[0].ne(0).any())
+            n_checked += 1
+    assert n_checked >= 4

@@ -7,7 +7,9 @@ reference's own values (tests/golden/train_*.npz, tools/make_golden_train.py).
 The grounding runs in HIP.  The SUM aggregator's rule part runs the fused
 HIP forward and backward (csrc/backward.hip, `fused_backward`), and, as a
 second parametrisation, torch autograd over the exported grounding COO; PNA
-runs the latter; RotatE its HIP forward / backward.
+takes its statistics from csrc/pna_grad.hip (forward and backward) with the
+dense layers in torch, or the same COO path; RotatE its HIP forward /
+backward.
 """
 import numpy as np
 import pytest
@@ -127,8 +129,6 @@ def test_train_steps_match_reference(case, fused, dev):
     model = PredictorPlus(graph, num_layers=3, hidden_dim=16,
                           embedding_path=datasets.rotate_path(data, dim) if dim else None, **kw)
     model.set_rules(datasets.rule_file(data))
-    if not fused and kw.get("aggregator", "sum") != "sum":
-        pytest.skip("the PNA aggregator trains through the autograd COO path only")
     model.fused_backward = fused
     sd = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd/")}
     missing, unexpected = model.load_state_dict(sd, strict=False)
@@ -268,10 +268,16 @@ def test_device_train_batches_match_dataset(data, dev):
         ts.make_batches()
 
 
-@pytest.mark.parametrize("data", ["FB15k-237", "umls"])
-@pytest.mark.parametrize("type_,feature", [("emb", "bias"), ("lstm", "RotatE"), ("lstm", "none"), ("emb", "none")])
-def test_fused_sum_backward_matches_autograd(data, type_, feature, dev):
-    """The fused SUM backward (rnnl_predictorplus_backward) against torch
+BACKWARD_CASES = [(d, t, f, "sum") for d in ("FB15k-237", "umls")
+                  for t, f in (("emb", "bias"), ("lstm", "RotatE"), ("lstm", "none"), ("emb", "none"))] + [
+    ("wn18rr", "emb", "RotatE", "pna"), ("wn18rr", "lstm", "bias", "pna"), ("kinship", "emb", "bias", "pna"),
+    ("umls", "lstm", "none", "pna")]
+
+
+@pytest.mark.parametrize("data,type_,feature,agg", BACKWARD_CASES)
+def test_fused_backward_matches_autograd(data, type_, feature, agg, dev):
+    """The fused backward — SUM: rnnl_predictorplus_backward; PNA: the
+    statistics of rnnl_pna_features and their backward — against torch
     autograd over the grounding COO (predictors.py:238-271 restated as torch
     ops) on the same seeded model and training batches (edge removal): the
     loss and every parameter gradient, four batches of distinct relations."""
@@ -281,7 +287,7 @@ def test_fused_sum_backward_matches_autograd(data, type_, feature, dev):
     torch.manual_seed(5)
     graph = KnowledgeGraph(datasets.materialize(data))
     ts = TrainDataset(graph, 32)
-    model = PredictorPlus(graph, type=type_, num_layers=3, hidden_dim=16, entity_feature=feature, aggregator="sum",
+    model = PredictorPlus(graph, type=type_, num_layers=3, hidden_dim=16, entity_feature=feature, aggregator=agg,
                           embedding_path=datasets.rotate_path(data) if feature == "RotatE" else None)
     model.set_rules(datasets.rule_file(data))
     with torch.no_grad():

@@ -14,7 +14,7 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 B="--offload-arch=gfx950 -O3 -fPIC -std=c++17"
 [ "$src" = rotate.hip ] && B="$B -mllvm -amdgpu-mfma-vgpr-form"
 others=""
-for f in graph.cpp ground.hip score.hip predictor.hip rotate.hip encode.hip batch.hip mine.hip loss.hip backward.hip wide.hip; do
+for f in graph.cpp ground.hip score.hip predictor.hip rotate.hip encode.hip batch.hip mine.hip loss.hip backward.hip wide.hip pna_grad.hip; do
   [ "$f" = "$src" ] || others="$others ../_build/$f.o"
 done
 make -s -C . $others
