@@ -54,7 +54,12 @@ __device__ __forceinline__ int cand_row(const int64_t *__restrict__ cand_off, in
   return lo;
 }
 
-// One lane per candidate over the launch's C candidates (row-major order).
+// One wave per candidate (grid-stride over the launch's C candidates,
+// row-major order), lane = (entry slot j = lane >> 4, dim d = lane & 15): the
+// wave takes the candidate's bucket entries four at a time, each lane one
+// (entry, dim) pair of the node records — no per-lane entry loops, so a few
+// registers and every wave busy whatever the lists' lengths — then sums /
+// min / max over the four slots by two xor shuffles.
 __global__ __launch_bounds__(PG_BS) void pna_features_kernel(KParams p, const unsigned char *__restrict__ node_w,
                                                               const int64_t *__restrict__ cand_off, int64_t C,
                                                               float *__restrict__ wsum, float *__restrict__ wsq,
@@ -69,48 +74,52 @@ __global__ __launch_bounds__(PG_BS) void pna_features_kernel(KParams p, const un
     atomicOr(&hdr[H_STATUS], 2u);
   }
   const double inv1 = ldexp(1.0, -(int)tr[1]), inv2 = ldexp(1.0, -(int)tr[4]);
-  for (int64_t c = (int64_t)blockIdx.x * PG_BS + threadIdx.x; c < C; c += (int64_t)gridDim.x * PG_BS) {
+  const int lane = threadIdx.x & 63, d = lane & 15, j = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * (PG_BS / 64);
+  for (int64_t c = (int64_t)blockIdx.x * (PG_BS / 64) + (threadIdx.x >> 6); c < C; c += nw) {
     const int q = cand_row(cand_off, p.nq, c);
     const int4 cr = p.cand[p.q_base[q] + (c - cand_off[q])];
-    long long a1[16], a2[16];
-    float m1[16], m2[16];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a1[d] = a2[d] = 0;
-      m1[d] = __builtin_huge_valf();
-      m2[d] = -__builtin_huge_valf();
-    }
+    long long a1 = 0, a2 = 0;
+    float m1 = __builtin_huge_valf(), m2 = -__builtin_huge_valf();
     unsigned long long dsum = 0, csum = 0;
 #pragma unroll 1
-    for (int e = cr.y; e < cr.y + cr.z; ++e) {
+    for (int e = cr.y + j; e < cr.y + cr.z; e += 4) {
       const int2 be = p.bent[e];
       const long long k = (uint32_t)be.y;
       const int *rec = reinterpret_cast<const int *>(node_w + (uint32_t)be.x * (uint32_t)kStridePna);
-      const float *fr = reinterpret_cast<const float *>(rec + 32);
-#pragma unroll
-      for (int d = 0; d < 16; ++d) {
-        a1[d] += k * rec[d];
-        a2[d] += k * rec[16 + d];
-        m1[d] = fminf(m1[d], fr[d]);
-        m2[d] = fmaxf(m2[d], fr[16 + d]);
+      a1 += k * rec[d];
+      a2 += k * rec[16 + d];
+      m1 = fminf(m1, __int_as_float(rec[32 + d]));
+      m2 = fmaxf(m2, __int_as_float(rec[48 + d]));
+      if (d == 0) {
+        dsum += (unsigned long long)k * (unsigned)p.rl.node_nrules[be.x];
+        csum += (unsigned long long)k;
       }
-      dsum += (unsigned long long)k * (unsigned)p.rl.node_nrules[be.x];
-      csum += (unsigned long long)k;
     }
-    if (csum >> 33) flag_acc_range(p);  // |record| < 2^30: the int64 sums are exact below 2^33 paths
 #pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      wsum[c * 16 + d] = (float)((double)a1[d] * inv1);
-      wsq[c * 16 + d] = (float)((double)a2[d] * inv2);
-      mn[c * 16 + d] = m1[d];
-      mx[c * 16 + d] = m2[d];
+    for (int o = 16; o <= 32; o <<= 1) {  // over the four entry slots
+      a1 += __shfl_xor(a1, o, 64);
+      a2 += __shfl_xor(a2, o, 64);
+      m1 = fminf(m1, __shfl_xor(m1, o, 64));
+      m2 = fmaxf(m2, __shfl_xor(m2, o, 64));
+      dsum += __shfl_xor(dsum, o, 64);
+      csum += __shfl_xor(csum, o, 64);
     }
-    const float degf = (float)(dsum + 1);
-    deg[c] = degf;  // layers.py:92: A_fn.sum(0) + 1
-    row[c] = q;
-    ent[c] = cr.x;
-    // the row's sum of log(degree) in 2^32 fixed point (integer adds: order-free)
-    atomicAdd(&lsum[q], (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
+    if (lane < 16) {
+      wsum[c * 16 + d] = (float)((double)a1 * inv1);
+      wsq[c * 16 + d] = (float)((double)a2 * inv2);
+      mn[c * 16 + d] = m1;
+      mx[c * 16 + d] = m2;
+    }
+    if (lane == 0) {
+      if (csum >> 33) flag_acc_range(p);  // |record| < 2^30: the int64 sums are exact below 2^33 paths
+      const float degf = (float)(dsum + 1);
+      deg[c] = degf;  // layers.py:92: A_fn.sum(0) + 1
+      row[c] = q;
+      ent[c] = cr.x;
+      // the row's sum of log(degree) in 2^32 fixed point (integer adds: order-free)
+      atomicAdd(&lsum[q], (unsigned long long)(long long)llrint((double)logf(degf) * 4294967296.0));
+    }
   }
 }
 
@@ -175,15 +184,17 @@ __device__ __forceinline__ unsigned long long pg_fix(double v, int sc) {
   return (unsigned long long)llrint(ldexp(v, sc));
 }
 
-// One lane per candidate (grid-stride over the C candidates): per bucket
-// entry (node n, count k) G1[n] += k dL/dwsum, G2[n] += k dL/dwsq, and the
-// candidate's min / max gradient to its entries tied at the min / max
-// (scatter_reduce amin / amax split it evenly among them): Gmin[n] +=
-// dL/dmn / ties.  Four int64 tables at the launch's scale; the first nl
-// nodes from `lo` (a one-relation launch's head trie) summed in LDS and
-// written as this workgroup's partial rows (summed by pna_grad_rules_kernel:
-// per-entry global atomics on the few shared nodes would serialise), the
-// rest by int64 HBM atomics.
+// One wave per candidate (grid-stride over the C candidates), lane = (entry
+// slot j, dim d) as pna_features_kernel: per bucket entry (node n, count k)
+// G1[n] += k dL/dwsum, G2[n] += k dL/dwsq, and the candidate's min / max
+// gradient to its entries tied at the min / max (scatter_reduce amin / amax
+// split it evenly among them): Gmin[n] += dL/dmn / ties.  A wave's adds go to
+// 64 distinct (entry, dim) words (a lane per candidate had every lane of a
+// wave add into the same few shared nodes: 2.2 ms per WN18RR batch).  Four
+// int64 tables at the launch's scale; the first nl nodes from `lo` (a
+// one-relation launch's head trie) summed in LDS and written as this
+// workgroup's partial rows (summed by pna_grad_rules_kernel), the rest by
+// int64 HBM atomics.
 __global__ __launch_bounds__(PG_BS) void pna_grad_nodes_kernel(
     KParams p, const unsigned char *__restrict__ node_w, const int64_t *__restrict__ cand_off, int64_t C,
     const float *__restrict__ mn, const float *__restrict__ mx, const float *__restrict__ d_wsum,
@@ -202,50 +213,39 @@ __global__ __launch_bounds__(PG_BS) void pna_grad_nodes_kernel(
     else
       atomicAdd(&G[k * tab + (int64_t)n * 16 + d], v);
   };
+  const int lane = threadIdx.x & 63, d = lane & 15, j = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * (PG_BS / 64);
   if (!bad)  // (a non-finite gradient: pna_grad_rules_kernel writes NaN)
-    for (int64_t c = (int64_t)blockIdx.x * PG_BS + threadIdx.x; c < C; c += (int64_t)gridDim.x * PG_BS) {
+    for (int64_t c = (int64_t)blockIdx.x * (PG_BS / 64) + (threadIdx.x >> 6); c < C; c += nw) {
       const int q = cand_row(cand_off, p.nq, c);
       const int4 cr = p.cand[p.q_base[q] + (c - cand_off[q])];
-      float g1[16], g2[16], vmn[16], vmx[16];
-#pragma unroll
-      for (int d = 0; d < 16; ++d) {
-        g1[d] = d_wsum[c * 16 + d];
-        g2[d] = d_wsq[c * 16 + d];
-        vmn[d] = mn[c * 16 + d];
-        vmx[d] = mx[c * 16 + d];
-      }
-      int tmn[16], tmx[16];  // the candidate's entries tied at its min / max, per dim
-#pragma unroll
-      for (int d = 0; d < 16; ++d) tmn[d] = tmx[d] = 0;
+      const float g1 = d_wsum[c * 16 + d], g2 = d_wsq[c * 16 + d];
+      const float vmn = mn[c * 16 + d], vmx = mx[c * 16 + d];
+      int tmn = 0, tmx = 0;  // the candidate's entries tied at its min / max (dim d)
 #pragma unroll 1
-      for (int e = cr.y; e < cr.y + cr.z; ++e) {
+      for (int e = cr.y + j; e < cr.y + cr.z; e += 4) {
         const int2 be = p.bent[e];
         const float *fr = reinterpret_cast<const float *>(node_w + (uint32_t)be.x * (uint32_t)kStridePna) + 32;
         const double k = (double)(uint32_t)be.y;
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-          tmn[d] += fr[d] == vmn[d];
-          tmx[d] += fr[16 + d] == vmx[d];
-          if (g1[d] != 0.f) add(0, be.x, d, pg_fix(k * (double)g1[d], sc));
-          if (g2[d] != 0.f) add(1, be.x, d, pg_fix(k * (double)g2[d], sc));
-        }
+        tmn += fr[d] == vmn;
+        tmx += fr[16 + d] == vmx;
+        if (g1 != 0.f) add(0, be.x, d, pg_fix(k * (double)g1, sc));
+        if (g2 != 0.f) add(1, be.x, d, pg_fix(k * (double)g2, sc));
       }
-      float gmn[16], gmx[16];
-#pragma unroll
-      for (int d = 0; d < 16; ++d) {
-        gmn[d] = tmn[d] ? d_mn[c * 16 + d] / (float)tmn[d] : 0.f;
-        gmx[d] = tmx[d] ? d_mx[c * 16 + d] / (float)tmx[d] : 0.f;
-      }
+      tmn += __shfl_xor(tmn, 16, 64);
+      tmn += __shfl_xor(tmn, 32, 64);
+      tmx += __shfl_xor(tmx, 16, 64);
+      tmx += __shfl_xor(tmx, 32, 64);
+      const float gmn = tmn ? d_mn[c * 16 + d] / (float)tmn : 0.f;
+      const float gmx = tmx ? d_mx[c * 16 + d] / (float)tmx : 0.f;
+      if (__ballot(gmn != 0.f || gmx != 0.f))
 #pragma unroll 1
-      for (int e = cr.y; e < cr.y + cr.z; ++e) {
-        const int n = p.bent[e].x;
-        const float *fr = reinterpret_cast<const float *>(node_w + (uint32_t)n * (uint32_t)kStridePna) + 32;
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-          if (gmn[d] != 0.f && fr[d] == vmn[d]) add(2, n, d, pg_fix((double)gmn[d], sc));
-          if (gmx[d] != 0.f && fr[16 + d] == vmx[d]) add(3, n, d, pg_fix((double)gmx[d], sc));
+        for (int e = cr.y + j; e < cr.y + cr.z; e += 4) {
+          const int n = p.bent[e].x;
+          const float *fr = reinterpret_cast<const float *>(node_w + (uint32_t)n * (uint32_t)kStridePna) + 32;
+          if (gmn != 0.f && fr[d] == vmn) add(2, n, d, pg_fix((double)gmn, sc));
+          if (gmx != 0.f && fr[16 + d] == vmx) add(3, n, d, pg_fix((double)gmx, sc));
         }
-      }
     }
   __syncthreads();
   long long *row = gpart + (int64_t)blockIdx.x * 4 * nl * 16;
@@ -338,7 +338,7 @@ int rnnl_pna_features(rnnl_rules r, const void *node_w, void *ws, int32_t nq, in
   KParams p = export_params(ws, nq, scale, n_cand);
   p.rl = r->d;
   if (n_cand_total > 0)
-    hipLaunchKernelGGL(pna_features_kernel, dim3((unsigned)std::min<int64_t>((n_cand_total + PG_BS - 1) / PG_BS, 8192)),
+    hipLaunchKernelGGL(pna_features_kernel, dim3((unsigned)std::min<int64_t>((n_cand_total + 3) / 4, 8192)),
                        dim3(PG_BS), 0, st, p, static_cast<const unsigned char *>(node_w), cand_off, n_cand_total, wsum,
                        wsq, mn, mx, deg, row, ent, lsum);
   hipLaunchKernelGGL(pna_rowscale_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, n_cand, nq,
@@ -389,7 +389,7 @@ int rnnl_pna_features_backward(rnnl_rules r, const void *node_w, const float *x,
   p.rl = r->d;
   p.all_r = all_r;
   const unsigned nb = (unsigned)std::min<int64_t>((n_cand_total + PG_BS - 1) / PG_BS, 4096);
-  const unsigned na = std::min<unsigned>(nb, PG_GRID);
+  const unsigned na = (unsigned)std::min<int64_t>((n_cand_total + 3) / 4, PG_GRID);
   const auto *nw = static_cast<const unsigned char *>(node_w);
   hipLaunchKernelGGL(pna_grad_stats_kernel, dim3(nb), dim3(PG_BS), 0, st, p, cand_off, n_cand_total, d_wsum, d_wsq,
                      d_mn, d_mx, stats);

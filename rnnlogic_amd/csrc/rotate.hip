@@ -708,6 +708,17 @@ __global__ void hr_rows_kernel(const float *__restrict__ eemb, const float2 *__r
   hr[(int64_t)q * 2 * D + D + d] = im;
 }
 
+// d(h o r) = the sum of rotate_backward_kernel's per-entity-block partials,
+// in block order (one thread per (row, part, dim); the partial rows are
+// coalesced along the dims)
+__global__ void hr_fold_kernel(const float *__restrict__ parts, int nparts, int64_t n, float *__restrict__ d_hr) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float t = 0.f;
+    for (int b = 0; b < nparts; ++b) t += parts[(int64_t)b * n + i];
+    d_hr[i] = t;
+  }
+}
+
 // d_eemb[e][part D + d] = d_tail[2 d + part][e]: 32 x 32 tiles through LDS
 // (the transposing copy torch's permute().reshape() made at ~1 TB/s)
 __global__ void tail_rows_kernel(const float *__restrict__ d_tail, int E, int D, float *__restrict__ d_eemb) {
@@ -739,7 +750,7 @@ __global__ void tail_rows_kernel(const float *__restrict__ d_tail, int E, int D,
 //   d remb[r][d] += (d s c - d c s) / div
 __global__ void head_grad_kernel(const float *__restrict__ eemb, const float2 *__restrict__ rtab, int D, float gamma,
                                  const int64_t *__restrict__ all_h, const int64_t *__restrict__ all_r, int nq,
-                                 const float *__restrict__ d_hr_part, int nparts, float *__restrict__ d_eemb,
+                                 const float *__restrict__ d_hr, float *__restrict__ d_eemb,
                                  float *__restrict__ d_remb) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= D) return;
@@ -748,13 +759,7 @@ __global__ void head_grad_kernel(const float *__restrict__ eemb, const float2 *_
     const int64_t h = all_h[q], r = all_r[q];
     const float rh = eemb[h * 2 * D + d], ih = eemb[h * 2 * D + D + d];
     const float2 cs = rtab[r * D + d];
-    // d(h o r): rotate_backward_kernel's per-block partials, in block order
-    float gre = 0.f, gim = 0.f;
-    for (int b = 0; b < nparts; ++b) {
-      const float *pb = d_hr_part + (int64_t)b * nq * 2 * D + (int64_t)q * 2 * D;
-      gre += pb[d];
-      gim += pb[D + d];
-    }
+    const float gre = d_hr[(int64_t)q * 2 * D + d], gim = d_hr[(int64_t)q * 2 * D + D + d];
     if (d_eemb) {
       d_eemb[h * 2 * D + d] += gre * cs.x + gim * cs.y;
       d_eemb[h * 2 * D + D + d] += gim * cs.x - gre * cs.y;
@@ -947,8 +952,8 @@ int rnnl_rotate_param_grads_scratch(int32_t nq, int32_t E, int32_t D, int32_t wi
     set_error("rnnl_rotate_param_grads_scratch: bad arguments");
     return RNNL_ERR_INVALID;
   }
-  // hr | the entity blocks' d(h o r) partials | d_tail
-  *bytes = (1 + bw_blocks(E)) * grads_hr_bytes(nq, D) + (with_eemb ? (size_t)2 * D * E * sizeof(float) : 0);
+  // hr | d(h o r) | the entity blocks' d(h o r) partials | d_tail
+  *bytes = (2 + bw_blocks(E)) * grads_hr_bytes(nq, D) + (with_eemb ? (size_t)2 * D * E * sizeof(float) : 0);
   return RNNL_OK;
 }
 
@@ -975,17 +980,21 @@ int rnnl_rotate_param_grads(const float *eemb, const float *planes, int32_t ld, 
   float *hr = reinterpret_cast<float *>(ws);
   // per entity block a partial d(h o r) (every entry written: no fill), summed
   // in block order by head_grad_kernel — no atomics, run-to-run bitwise
-  float *d_hr_part = reinterpret_cast<float *>(ws + grads_hr_bytes(nq, D));
-  float *d_tail = d_eemb ? reinterpret_cast<float *>(ws + (1 + bx) * grads_hr_bytes(nq, D)) : nullptr;
+  float *d_hr = reinterpret_cast<float *>(ws + grads_hr_bytes(nq, D));
+  float *d_hr_part = reinterpret_cast<float *>(ws + 2 * grads_hr_bytes(nq, D));
+  float *d_tail = d_eemb ? reinterpret_cast<float *>(ws + (2 + bx) * grads_hr_bytes(nq, D)) : nullptr;
   hipLaunchKernelGGL(hr_rows_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)nq), dim3(256), 0, st, eemb,
                      (const float2 *)rtab, D, all_h, all_r, hr);
   hipLaunchKernelGGL(rotate_backward_kernel, dim3(bx, (unsigned)D), dim3(BW_BS), 0, st, planes, ld, hr, grad, nq, E, D,
                      (float *)nullptr, d_hr_part, d_tail);
+  const int64_t nhr = (int64_t)nq * 2 * D;
+  hipLaunchKernelGGL(hr_fold_kernel, dim3(grid_for(nhr)), dim3(256), 0, st, (const float *)d_hr_part, (int)bx, nhr,
+                     d_hr);
   if (d_eemb)
     hipLaunchKernelGGL(tail_rows_kernel, dim3((unsigned)((D + 31) / 32), (unsigned)((E + 31) / 32)), dim3(256), 0, st,
                        d_tail, E, D, d_eemb);
   hipLaunchKernelGGL(head_grad_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, st, eemb,
-                     (const float2 *)rtab, D, gamma, all_h, all_r, nq, d_hr_part, (int)bx, d_eemb, d_remb);
+                     (const float2 *)rtab, D, gamma, all_h, all_r, nq, (const float *)d_hr, d_eemb, d_remb);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }
