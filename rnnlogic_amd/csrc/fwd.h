@@ -170,6 +170,11 @@ __device__ inline Slot make_slot(unsigned char *base, int slot, int64_t fcap, in
   return s;
 }
 
+#ifndef RNNL_PTAB_MIN_BITS  // compile-time knob for A/B builds (tools/build_variants.sh)
+#define RNNL_PTAB_MIN_BITS 12
+#endif
+constexpr int PTAB_MIN_BITS = RNNL_PTAB_MIN_BITS;
+
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
@@ -208,8 +213,10 @@ inline Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   o += 8 * L.chunk_cap + 4 * (std::max<int64_t>(nq, 1) / 256 + 1);  // list | per-block chunk totals
   L.off_memo = o = align256(o);
   o += 4 * n_nodes;
-  // pair memo (SUM): 2^ptab_bits 8-B slots, ~128 per row, 2^16 .. 2^23
-  L.ptab_bits = 16;
+  // pair memo (SUM): 2^ptab_bits 8-B slots, ~128 per row, 2^PTAB_MIN_BITS .. 2^23
+  // (a 32-row reference batch: 2^12, 32 KB, zeroed by one block of the
+  // chunk-list kernel on the call's critical path)
+  L.ptab_bits = PTAB_MIN_BITS;
   while (L.ptab_bits < 23 && (1ll << L.ptab_bits) < 128 * std::max<int64_t>(nq, 1)) ++L.ptab_bits;
   L.off_ptab = o = align256(o);
   if (n_nodes > 0) o += 8ll << L.ptab_bits;
