@@ -170,6 +170,16 @@ int rnnl_lstm_train_backward(const float *vocab, const float *const *w_ih, const
                              const float *act, const float *d_out, float *da, float *xh, float *dvx,
                              const int32_t *tok_id, const int32_t *tok_ptr, const int32_t *tok_pos, int32_t n_tok,
                              float *d_vocab, int32_t vocab_rows, void *stream);
+/* The weight gradients of the same backward (torch.nn.LSTM's dW_ih, dW_hh,
+ * db): dW_l = da_l^T xh_l over the `rows` = n seq_len rows of da / xh as
+ * filled above, db_l = column sums of da_l, summed in a fixed order (per
+ * 128-row segment, then over segments in order) so that they are bitwise
+ * repeatable — a library GEMM with K = n seq_len may split K with atomics.
+ * out (floats): [layers][64][16] dW_ih | [layers][64][16] dW_hh |
+ * [layers][64] db.  part: rnnl_lstm_weight_grads_scratch floats. */
+int rnnl_lstm_weight_grads_scratch(int32_t layers, int64_t rows, size_t *part_floats);
+int rnnl_lstm_weight_grads(const float *da, const float *xh, int32_t layers, int64_t rows, float *part,
+                           size_t part_floats, float *out, void *stream);
 
 /* ------------------------------------------------------------- forward --
  * Replaces the body of PredictorPlus.forward (reference

@@ -44,6 +44,8 @@ SIGNATURES = [
     ("rnnl_lstm_train_forward", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P]),
     ("rnnl_lstm_train_backward", ctypes.c_int,
      [_P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _I32, _P]),
+    ("rnnl_lstm_weight_grads_scratch", ctypes.c_int, [_I32, ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]),
+    ("rnnl_lstm_weight_grads", ctypes.c_int, [_P, _P, _I32, ctypes.c_int64, _P, ctypes.c_size_t, _P, _P]),
     ("rnnl_lstm_encode_trie_scratch", ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_size_t)]),
     ("rnnl_lstm_encode_trie", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _P, ctypes.c_size_t, _P]),
     ("rnnl_lstm_encode_trie_sum", ctypes.c_int,

@@ -439,6 +439,62 @@ __global__ void vocab_grad_kernel(const float *__restrict__ dvx, const int32_t *
   d_vocab[(int64_t)tok_id[u] * LH + k] = s;
 }
 
+// Weight gradients dW_l = da_l^T [x | h_prev], db_l = column sums of da_l
+// (torch.nn.LSTM's, summed over every rule and step) in a fixed order: block
+// (segment, layer) sums its WG_SEG rows in row order into part, then
+// lstm_wgrad_fold_kernel sums the segments in segment order.  Column
+// WG_COLS - 1 is the bias (an all-ones input column).
+constexpr int WG_SEG = 128;
+constexpr int WG_COLS = 2 * LH + 1;
+constexpr int WG_PER = (WG_COLS + 3) / 4;  // columns per thread (4 column groups)
+
+static inline int64_t wg_segments(int64_t rows) { return (rows + WG_SEG - 1) / WG_SEG; }
+
+__global__ void __launch_bounds__(256) lstm_wgrad_part_kernel(const float *__restrict__ da,
+                                                              const float *__restrict__ xh, int64_t rows,
+                                                              float *__restrict__ part) {
+  const int g = threadIdx.x & (LG - 1), cg = threadIdx.x >> 6;
+  const int l = blockIdx.y, L = gridDim.y;
+  const int64_t seg = blockIdx.x, r0 = seg * WG_SEG, r1 = r0 + WG_SEG < rows ? r0 + WG_SEG : rows;
+  float acc[WG_PER];
+#pragma unroll
+  for (int j = 0; j < WG_PER; ++j) acc[j] = 0.f;
+  const float *dal = da + (int64_t)l * rows * LG;
+  const float *xhl = xh + (int64_t)l * rows * 2 * LH;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float a = dal[r * LG + g];
+    const float *x = xhl + r * 2 * LH;
+#pragma unroll
+    for (int j = 0; j < WG_PER; ++j) {
+      const int c = cg + 4 * j;
+      if (c < 2 * LH)
+        acc[j] = fmaf(a, x[c], acc[j]);
+      else if (c == 2 * LH)
+        acc[j] += a;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < WG_PER; ++j) {
+    const int c = cg + 4 * j;
+    if (c < WG_COLS) part[((seg * L + l) * WG_COLS + c) * LG + g] = acc[j];
+  }
+}
+
+__global__ void lstm_wgrad_fold_kernel(const float *__restrict__ part, int L, int64_t nseg, float *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L * WG_COLS * LG) return;
+  const int g = i % LG, c = (i / LG) % WG_COLS, l = i / (LG * WG_COLS);
+  float s = 0.f;
+  for (int64_t seg = 0; seg < nseg; ++seg) s += part[((seg * L + l) * WG_COLS + c) * LG + g];
+  const int64_t wsz = (int64_t)L * LG * LH;
+  if (c < LH)
+    out[((int64_t)l * LG + g) * LH + c] = s;
+  else if (c < 2 * LH)
+    out[wsz + ((int64_t)l * LG + g) * LH + (c - LH)] = s;
+  else
+    out[2 * wsz + (int64_t)l * LG + g] = s;
+}
+
 }  // namespace rnnl
 
 using namespace rnnl;
@@ -601,6 +657,34 @@ int rnnl_lstm_train_backward(const float *vocab, const float *const *w_ih, const
   if (n_tok > 0)
     hipLaunchKernelGGL(vocab_grad_kernel, dim3((unsigned)((n_tok * LH + 255) / 256)), dim3(256), 0, st, dvx, tok_id,
                        tok_ptr, tok_pos, n_tok, d_vocab);
+  RNNL_HIP_CHECK(hipGetLastError());
+  return RNNL_OK;
+}
+
+int rnnl_lstm_weight_grads_scratch(int32_t layers, int64_t rows, size_t *part_floats) {
+  if (layers < 1 || layers > LMAXL || rows < 0 || !part_floats) {
+    set_error("rnnl_lstm_weight_grads_scratch: bad arguments");
+    return RNNL_ERR_INVALID;
+  }
+  *part_floats = (size_t)wg_segments(rows) * layers * WG_COLS * LG;
+  return RNNL_OK;
+}
+
+int rnnl_lstm_weight_grads(const float *da, const float *xh, int32_t layers, int64_t rows, float *part,
+                           size_t part_floats, float *out, void *stream) {
+  size_t need = 0;
+  if (!da || !xh || !part || !out || rnnl_lstm_weight_grads_scratch(layers, rows, &need) != RNNL_OK ||
+      part_floats < need || rows <= 0) {
+    set_error("rnnl_lstm_weight_grads: bad arguments (rows >= 1, part: rnnl_lstm_weight_grads_scratch floats)");
+    return RNNL_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nseg = wg_segments(rows);
+  hipLaunchKernelGGL(lstm_wgrad_part_kernel, dim3((unsigned)nseg, (unsigned)layers), dim3(256), 0, st, da, xh, rows,
+                     part);
+  const int total = layers * WG_COLS * LG;
+  hipLaunchKernelGGL(lstm_wgrad_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, layers,
+                     nseg, out);
   RNNL_HIP_CHECK(hipGetLastError());
   return RNNL_OK;
 }

@@ -1099,7 +1099,9 @@ class _LstmRules(torch.autograd.Function):
     ridx, by rnnl_lstm_train_forward (the inference encoder's recurrence, each
     step's gates and states saved), and its backward through time by
     rnnl_lstm_train_backward — the gate-gradient and layer-input rows, then
-    dW = da^T [x | h_prev] and db = sum(da) as batched GEMMs, and the vocab
+    dW = da^T [x | h_prev] and db = sum(da) in a fixed order by
+    rnnl_lstm_weight_grads (a library GEMM over K = n T may split K with
+    atomics, which made training not bitwise repeatable), and the vocab
     rows' gradient summed per token in position order.  Replaces the library
     LSTM's per-layer / per-step kernels and its host work (~1.6 ms per step)."""
 
@@ -1143,11 +1145,16 @@ class _LstmRules(torch.autograd.Function):
                      T, m.padding_index, ridx.data_ptr(), n, act.data_ptr(), d_out.data_ptr(), da.data_ptr(),
                      xh.data_ptr(), dvx.data_ptr(), tok_id.data_ptr(), ptr.data_ptr(), pos.data_ptr(), n_tok,
                      d_vocab.data_ptr(), vocab.size(0), torch.cuda.current_stream(dev).cuda_stream)
-        da_t = da.view(L, n * T, 64).transpose(1, 2)
-        xh = xh.view(L, n * T, 32)
-        d_wih = torch.bmm(da_t, xh[:, :, :16])
-        d_whh = torch.bmm(da_t, xh[:, :, 16:])
-        d_b = da_t.sum(2)
+        rows = n * T
+        n_part = ctypes.c_size_t()
+        _native.call("rnnl_lstm_weight_grads_scratch", L, rows, ctypes.byref(n_part))
+        part = torch.empty(n_part.value, dtype=torch.float32, device=dev)
+        wg = torch.empty(L * 64 * 33, dtype=torch.float32, device=dev)
+        _native.call("rnnl_lstm_weight_grads", da.data_ptr(), xh.data_ptr(), L, rows, part.data_ptr(), n_part.value,
+                     wg.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        d_wih = wg[:L * 1024].view(L, 64, 16)
+        d_whh = wg[L * 1024:L * 2048].view(L, 64, 16)
+        d_b = wg[L * 2048:].view(L, 64)
         grads = []
         for k in range(L):
             grads += [d_wih[k], d_whh[k], d_b[k], d_b[k].clone()]
