@@ -23,22 +23,6 @@ namespace rnnl {
 // count), so the loads take the scalar-base + 32-bit-offset form
 __device__ __forceinline__ uint32_t rec_off(int n, int stride) { return (uint32_t)n * (uint32_t)stride; }
 
-// Exact int64 sums of count x record word (off + d) over a candidate's bucket
-// entries, one dim at a time (few registers), as a double: the fallback of
-// pna_hidden_2walk's fp64 sums past a total count of 2^23.
-__device__ __forceinline__ void exact_sums(const KParams &p, int beg, int cnt, int off, double (&a)[16]) {
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    long long acc = 0;
-#pragma unroll 1
-    for (int e = beg; e < beg + cnt; ++e) {
-      const int2 be = p.bent[e];
-      acc += (long long)(uint32_t)be.y * reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna))[off + d];
-    }
-    a[d] = (double)acc;
-  }
-}
-
 // score_model's weights as the scoring kernels keep them in LDS: layer 0's
 // candidate half (128 x 16) as the A fragments of v_mfma_f32_16x16x16_f16,
 // each weight split into two fp16 parts, and the last layer as floats.
@@ -163,27 +147,28 @@ __device__ __forceinline__ float relation_bias(const KParams &p, int r, int o) {
 
 // ---------------------------------------------------------------- PNA scoring over chunks
 // FuncToNode (pna, layers.py:79-126) + score_model for one wave x one chunk of
-// <= 64 consecutive candidates of one query (lane = candidate),
-// p.chunks[0 .. hdr[H_CHUNKS]).  Waves dequeue chunks independently, so a
-// query with 17k candidates (WN18RR) is spread over ~280 waves instead of
-// holding one workgroup while the rest of the grid drains; no workgroup
-// barrier per query.
+// <= 64 consecutive candidates of one query, p.chunks[0 .. hdr[H_CHUNKS]).
+// Waves dequeue chunks independently, so a query with 17k candidates (WN18RR)
+// is spread over ~280 waves instead of holding one workgroup while the rest
+// of the grid drains; no workgroup barrier per query.
 //
-// Per candidate, two walks over its bucket entries (pna_walk: sums of
-// count x record in exact fp64 and the min / max), one per half of the node
-// records, give the 64 features [mean, min, max, std] (16 dims each); the
-// degree scalers {1, s, 1/s} make 192 inputs of add_model, Linear(192, 16).
-// That layer runs on the matrix cores as D1 = W . U^T for 16 candidates at a
-// time: U[c][(f, s3)] = feature f x scaler s3 (the reference's fp32 product)
-// split into two fp16 parts (features are means, minima, maxima and standard
+// Per 16-candidate tile, one walk over each candidate's bucket entries (four
+// lanes per candidate, below) gives the 64 features [mean, min, max, std]
+// (16 dims each); the degree scalers {1, s, 1/s} make 192 inputs of
+// add_model, Linear(192, 16).  That layer runs on the matrix cores as
+// D1 = W . U^T for the tile: U[c][(f, s3)] = feature f x scaler s3, the
+// features split into two fp16 parts (means, minima, maxima and standard
 // deviations of rule embeddings: bounded), W (16 x 192) the A fragments per
-// (feature block, scaler), three part products per 16-wide K step.  D1's
-// lane (k, i16) holds outputs 4k .. 4k + 3 of candidate i16, so LayerNorm's
-// mean and variance are two xor shuffles away, and after ReLU the lane holds
-// exactly score_model's B fragment (hidden 4k .. 4k + 3 of candidate i16):
-// mlp0_tile runs on it with no second staging.  On the VALU the Linear was
-// 3,072 FMAs per candidate, most of the pass's VALU instructions — which
-// take RotatE's issue slots beside it.
+// (feature block, scaler), three part products per 16-wide K step; the
+// scalers are per candidate, so they factor out of the Linear (D_s
+// accumulates W_s . x and the output is D_1 + s D_s + D_{1/s} / s: one split
+// per feature block instead of one per (block, scaler)).  D1's lane (k, i16)
+// holds outputs 4k .. 4k + 3 of candidate i16, so LayerNorm's mean and
+// variance are two xor shuffles away, and after ReLU the lane holds exactly
+// score_model's B fragment (hidden 4k .. 4k + 3 of candidate i16): mlp0_tile
+// runs on it with no second staging.  On the VALU the Linear was 3,072 FMAs
+// per candidate, most of the pass's VALU instructions — which take RotatE's
+// issue slots beside it.
 
 // LDS image of the PNA weights: add_model as A fragments per (feature block
 // b, scaler s3): lane (k, i16) holds W[i16][(16 b + 4k + j) 3 + s3], j < 4;
@@ -216,159 +201,143 @@ __device__ __forceinline__ void load_pna_weights(PnaLds &w, const float *__restr
   load_mlp0(w.m, W);
 }
 
-// One walk over a candidate's bucket entries for one half of the node records
-// (HALF 0: sum x and min; 1: sum x^2 and max): the exact sums of count x
-// record word (fp64 is exact below a total count of 2^23; past it the int64
-// sums of exact_sums) as floats at the column's scale, and the min / max.
-// STATS (walk 1): the degree, count total and digest fingerprint too.
-template <int HALF, bool STATS>
-__device__ __forceinline__ void pna_walk(const KParams &p, int beg, int cnt, uint64_t &csum, long long &deg,
-                                         uint64_t &fp, bool want_fp, float (&sum)[16], float (&mm)[16]) {
-  double a[16];
+// ---- lane = (candidate, dim quad) walks
+// The features are walked with four lanes per candidate: a round takes the 16
+// candidates of a tile (lane 4 c + dq: candidate c, dims 4 dq .. 4 dq + 3,
+// 16-byte record loads), each lane accumulating its dims' sums and sums of
+// squares (exact fp64, int64 past a total count of 2^23), minima and maxima
+// over the candidate's entries in ONE walk.  A per-candidate lane walk
+// carries 16 dims x 4 statistics in registers (233 VGPRs + AGPRs: two waves
+// per SIMD, holding RotatE to three beside it) and its wave waits for the
+// longest of 64 lists, twice; here a round waits for the longest of 16, a
+// lane holds 4 dims, and the features go straight into the tile's LDS stage
+// for add_model's MFMA steps (WN18RR ground + PNA alone 5.05-5.2 -> 4.73-4.8
+// ms).  Every sum is exact and min / max are order-free: the walk order does
+// not change a feature.
+struct PnaAcc {
+  double s[4], q[4];  // sum of count x record (sums half, squares half), this lane's dims
+  float mn[4], mx[4];
+  uint64_t csum;      // count total
+  long long deg;      // degree term: sum of count x rules at the node
+  uint64_t fp;        // digest fingerprint term
+};
+
+__device__ __forceinline__ void pna_acc_init(PnaAcc &A) {
 #pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    a[d] = 0;
-    mm[d] = HALF == 0 ? __builtin_huge_valf() : -__builtin_huge_valf();
+  for (int j = 0; j < 4; ++j) {
+    A.s[j] = 0;
+    A.q[j] = 0;
+    A.mn[j] = __builtin_huge_valf();
+    A.mx[j] = -__builtin_huge_valf();
   }
-  // as gather_sum: the next entry loaded beside this entry's record (WN18RR
-  // step 18.35-18.56 -> 18.33-18.38 ms)
-  int2 nx = cnt > 0 ? p.bent[beg] : make_int2(0, 0);
+  A.csum = 0;
+  A.deg = 0;
+  A.fp = 0;
+}
+
+// entries e0, e0 + step, ... < e1, dims 4 dq .. 4 dq + 3, into A
+__device__ __forceinline__ void pna_lane_walk(const KParams &p, int e0, int e1, int step, int dq, bool want_fp,
+                                              PnaAcc &A) {
+  int2 nx = e0 < e1 ? p.bent[e0] : make_int2(0, 0);
 #pragma unroll 1
-  for (int e = beg; e < beg + cnt; ++e) {
+  for (int e = e0; e < e1; e += step) {
     const int2 be = nx;
-    if (e + 1 < beg + cnt) nx = p.bent[e + 1];
-    const double cd = (double)(uint32_t)be.y;
-    if constexpr (STATS) {
-      const long long c = (uint32_t)be.y;
-      csum += (uint64_t)c;
-      deg += c * p.rl.node_nrules[be.x];
-      if (want_fp) fp += (uint64_t)c * p.rl.node_fp[be.x];
-    }
-    const int *rec = reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna)) + HALF * 16;
-    const float *fr = reinterpret_cast<const float *>(rec + 32);
+    if (e + step < e1) nx = p.bent[e + step];
+    const uint32_t c = (uint32_t)be.y;
+    A.csum += c;
+    A.deg += (long long)c * p.rl.node_nrules[be.x];
+    if (want_fp) A.fp += (uint64_t)c * p.rl.node_fp[be.x];
+    const int4 *rec = reinterpret_cast<const int4 *>(p.node_w + rec_off(be.x, kStridePna));
+    const int4 rs = rec[dq], rq = rec[4 + dq];
+    const float4 fmn = reinterpret_cast<const float4 *>(rec)[8 + dq], fmx = reinterpret_cast<const float4 *>(rec)[12 + dq];
+    const int xs[4] = {rs.x, rs.y, rs.z, rs.w}, xq[4] = {rq.x, rq.y, rq.z, rq.w};
+    const float vn[4] = {fmn.x, fmn.y, fmn.z, fmn.w}, vx[4] = {fmx.x, fmx.y, fmx.z, fmx.w};
+    const double cd = (double)c;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a[d] = fma(cd, (double)rec[d], a[d]);
-      mm[d] = __builtin_amdgcn_fmed3f(mm[d], fr[d], HALF == 0 ? -__builtin_huge_valf() : __builtin_huge_valf());  // min / max
+    for (int j = 0; j < 4; ++j) {
+      A.s[j] = fma(cd, (double)xs[j], A.s[j]);
+      A.q[j] = fma(cd, (double)xq[j], A.q[j]);
+      A.mn[j] = __builtin_amdgcn_fmed3f(A.mn[j], vn[j], -__builtin_huge_valf());
+      A.mx[j] = __builtin_amdgcn_fmed3f(A.mx[j], vx[j], __builtin_huge_valf());
     }
   }
-  if (csum >> 23) exact_sums(p, beg, cnt, HALF * 16, a);
-  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
-  const double inv = ldexp(1.0, -(int)trailer[HALF == 0 ? 1 : 4]);
-#pragma unroll
-  for (int d = 0; d < 16; ++d) sum[d] = (float)(a[d] * inv);
 }
 
-// One feature block (16 features of each of the wave's 64 candidates) into
-// the four tiles' add_model accumulators: staged, then per tile one split of
-// the features into fp16 parts and per scaler one 16-wide K step (three part
-// products).  The scalers are per candidate, so they factor out of the
-// Linear: Ds accumulates W_s . x, and the tile's output is D0 + s D1 + D2 / s
-// (pna_combine) — one split per tile instead of one per (tile, scaler).
-__device__ __forceinline__ void pna_block(const PnaLds &w, int b, const float (&v)[16], float *stage,
-                                          f32x4 (&D)[3][4]) {
-  const int lane = threadIdx.x & 63, k = lane >> 4, i16 = lane & 15;
-  float4 *st = reinterpret_cast<float4 *>(stage);
+// the same entries' int64 sums (totals past the exact fp64 range)
+__device__ __forceinline__ void pna_lane_exact(const KParams &p, int e0, int e1, int step, int dq, long long (&s)[4],
+                                               long long (&q)[4]) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) st[lane * 4 + j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
-  wave_lds_sync();
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const float4 x = st[(t * 16 + i16) * 4 + k];  // candidate 16 t + i16, features 16 b + 4k .. + 3
-    f16x4 bh, bl;
-    split4(x, bh, bl);
-#pragma unroll
-    for (int s3 = 0; s3 < 3; ++s3) {
-      const f16x4 ah = __builtin_bit_cast(f16x4, w.aa[b][s3][0][lane]);
-      const f16x4 al = __builtin_bit_cast(f16x4, w.aa[b][s3][1][lane]);
-      D[s3][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, D[s3][t], 0, 0, 0);
-      D[s3][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, D[s3][t], 0, 0, 0);
-      D[s3][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, D[s3][t], 0, 0, 0);
-    }
-  }
-  wave_lds_sync();  // the next block rewrites the stage
-}
-
-// Long bucket lists (> PNA_BIG entries): one half of the walk (as pna_walk)
-// by the whole wave — lane i takes entries i, i + 64, ... — and a butterfly
-// over the lanes: the fp64 sums of exact count x record products are exact
-// in any order and min / max are order-free, so the features are the
-// per-lane walk's bit for bit.  slot[0 .. 15] = the sums at the column's
-// scale, slot[16 .. 31] = min (HALF 0) / max (HALF 1).  Returns the count
-// total (HALF 0: with the degree and fingerprint terms).
-constexpr int PNA_BIG = 16;
-constexpr int PNA_BIG_SLOTS = 16;
-template <int HALF>
-__device__ __forceinline__ uint64_t pna_coop(const KParams &p, int beg, int cnt, float *slot, long long &deg,
-                                             uint64_t &fp, bool want_fp) {
-  const int lane = threadIdx.x & 63;
-  double a[16];
-  float mm[16];
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    a[d] = 0;
-    mm[d] = HALF == 0 ? __builtin_huge_valf() : -__builtin_huge_valf();
-  }
-  uint64_t csum = 0;
-  deg = 0;
-  fp = 0;
+  for (int j = 0; j < 4; ++j) s[j] = q[j] = 0;
 #pragma unroll 1
-  for (int e = beg + lane; e < beg + cnt; e += 64) {
+  for (int e = e0; e < e1; e += step) {
     const int2 be = p.bent[e];
-    const double cd = (double)(uint32_t)be.y;
-    if constexpr (HALF == 0) {
-      const long long c = (uint32_t)be.y;
-      csum += (uint64_t)c;
-      deg += c * p.rl.node_nrules[be.x];
-      if (want_fp) fp += (uint64_t)c * p.rl.node_fp[be.x];
-    }
-    const int *rec = reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna)) + HALF * 16;
-    const float *fr = reinterpret_cast<const float *>(rec + 32);
+    const long long c = (uint32_t)be.y;
+    const int *rec = reinterpret_cast<const int *>(p.node_w + rec_off(be.x, kStridePna));
 #pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a[d] = fma(cd, (double)rec[d], a[d]);
-      mm[d] = HALF == 0 ? fminf(mm[d], fr[d]) : fmaxf(mm[d], fr[d]);
+    for (int j = 0; j < 4; ++j) {
+      s[j] += c * rec[4 * dq + j];
+      q[j] += c * rec[16 + 4 * dq + j];
     }
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      a[d] += __shfl_xor(a[d], off, 64);
-      const float o = __shfl_xor(mm[d], off, 64);
-      mm[d] = HALF == 0 ? fminf(mm[d], o) : fmaxf(mm[d], o);
-    }
-    if constexpr (HALF == 0) {
-      csum += __shfl_xor(csum, off, 64);
-      deg += __shfl_xor(deg, off, 64);
-      fp += __shfl_xor(fp, off, 64);
-    }
-  }
-  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
-  const double inv = ldexp(1.0, -(int)trailer[HALF == 0 ? 1 : 4]);
-  float v = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    if (lane == d) v = (float)(a[d] * inv);
-    if (lane == 16 + d) v = mm[d];
-  }
-  if (lane < 32) slot[lane] = v;
-  return csum;
 }
 
-__global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const float *__restrict__ W) {
+// The four features of dims 4 dq .. 4 dq + 3 of tile candidate c16 into the
+// stage (block b: stage[(16 b + c16) 16 + dim], one 16-byte store each); lane
+// dq == 0 also writes the scalers and the digest term.  inv0 / inv1: the
+// sums' / squares' fixed-point scales.  mean = sum / degree and
+// std = sqrt(max(sum x^2 / degree - mean^2, 1e-6)) in the reference's
+// separately rounded fp32 operations (layers.py:103-110).
+__device__ __forceinline__ void pna_features_out(const KParams &p, const PnaAcc &A, int dq, int c16, bool live,
+                                                 int q, int ent, double inv0, double inv1, float *stage, float2 *sc) {
+  const float degf = (float)(A.deg + 1);
+  const float idcl = 1.0f / fmaxf(degf, 1e-6f);
+  float mean[4], sd[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float sum = (float)(A.s[j] * inv0), sq = (float)(A.q[j] * inv1);
+    mean[j] = __fmul_rn(sum, idcl);
+    sd[j] = sqrtf(fmaxf(__fsub_rn(__fmul_rn(sq, idcl), __fmul_rn(mean[j], mean[j])), 1e-6f));
+  }
+  float4 *st = reinterpret_cast<float4 *>(stage);
+  st[(0 * 16 + c16) * 4 + dq] = make_float4(mean[0], mean[1], mean[2], mean[3]);
+  st[(1 * 16 + c16) * 4 + dq] = live ? make_float4(A.mn[0], A.mn[1], A.mn[2], A.mn[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  st[(2 * 16 + c16) * 4 + dq] = live ? make_float4(A.mx[0], A.mx[1], A.mx[2], A.mx[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  st[(3 * 16 + c16) * 4 + dq] = make_float4(sd[0], sd[1], sd[2], sd[3]);
+  if (dq == 0) {
+    // degree scalers (layers.py:92, 103-116): degree = sum of A_fn + 1
+    const float sc1 = live ? logf(degf) / fmaxf(p.q_scale[q], 1e-6f) : 1.0f;
+    sc[c16] = make_float2(sc1, 1.0f / fmaxf(sc1, 1e-6f));
+    if (live) {
+      if (p.digest)
+        atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q),
+                  (unsigned long long)mix64((uint64_t)ent ^ mix64((uint64_t)A.deg ^ mix64(A.fp))));
+      if (A.csum >> 33) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33
+    }
+  }
+}
+
+// Lists longer than this are walked by the whole wave (16 entry slots x 4
+// dim quads, then a reduction over the slots) instead of the candidate's
+// four lanes.
+constexpr int PNA_BIG = 16;
+
+__global__ __launch_bounds__(BS, 4) void score_pna_chunk_kernel(KParams p, const float *__restrict__ W) {
   __shared__ PnaLds s_w;
   __shared__ __attribute__((aligned(16))) float s_relb[BS / 64][128];
-  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][64 * 16];  // a feature block of 64 candidates
-  __shared__ float2 s_sc[BS / 64][64];                                      // their scalers (s, 1 / s)
-  __shared__ float s_big[BS / 64][PNA_BIG_SLOTS][64];                       // long lists' features (pna_coop)
+  __shared__ __attribute__((aligned(16))) float s_stage[BS / 64][4 * 16 * 16];  // a tile's 16 x 64 features
+  __shared__ float2 s_sc[BS / 64][16];                                         // their scalers (s, 1 / s)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, k = lane >> 4, i16 = lane & 15;
+  const int c4 = lane >> 2, dq = lane & 3;  // the walks' lane roles: candidate of the tile, dim quad
   unsigned int *hdr = reinterpret_cast<unsigned int *>(p.ws);
-  check_node_table(p, reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna));
+  const unsigned int *trailer = reinterpret_cast<const unsigned int *>(p.node_w + (int64_t)p.rl.n_nodes * kStridePna);
+  check_node_table(p, trailer);
   load_pna_weights(s_w, W);
   __syncthreads();  // the only workgroup barrier: waves run independently from here
+  const double inv0 = ldexp(1.0, -(int)trailer[1]), inv1 = ldexp(1.0, -(int)trailer[4]);
+  const bool want_fp = p.digest != nullptr;
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
-  float *relb = s_relb[wv];
+  float *relb = s_relb[wv], *stage = s_stage[wv];
+  float2 *sc = s_sc[wv];
   int cur_r = -1;
   unsigned c = 0, cend = 0;  // wave-uniform: the dequeued chunk range
 #pragma unroll 1
@@ -386,113 +355,118 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
       wave_lds_sync();
       cur_r = r;
     }
-    const int nc = p.n_cand[q];
+    const int nc = __builtin_amdgcn_readfirstlane(p.n_cand[q]);
+    const int64_t qb = p.q_base[q];
+    // lane = candidate s0 + lane for the loads and the final store; lanes past
+    // the chunk's candidates carry zero features and store nothing
     const int s = s0 + lane;
-    // every lane takes part in the matrix-core layers; lanes past the chunk's
-    // candidates carry zero features and store nothing
     const bool live = s < nc;
-    int64_t qb = 0;
     int4 cr = make_int4(0, 0, 0, 0);
-    if (live) {
-      qb = p.q_base[q];
-      cr = p.cand[qb + s];
-    }
-    uint64_t csum = 0, fp = 0;
-    long long deg = 0;
-    // the first PNA_BIG_SLOTS long lists: both halves walked by the whole wave
-    int slot = -1;
-    {
-      uint64_t big = __ballot(live && cr.z > PNA_BIG);
+    if (live) cr = p.cand[qb + s];
+    float out = 0.f;
 #pragma unroll 1
-      for (int nb = 0; big && nb < PNA_BIG_SLOTS; ++nb) {
+    for (int t = 0; t < 4 && s0 + 16 * t < nc; ++t) {
+      // the tile's long lists: the whole wave, entry slot c4, dim quad dq
+      uint64_t big = __ballot(live && cr.z > PNA_BIG && (lane >> 4) == t);
+#pragma unroll 1
+      while (big) {
         const int owner = __builtin_ctzll(big);
         big &= big - 1;
         const int beg = __builtin_amdgcn_readlane(cr.y, owner), cnt = __builtin_amdgcn_readlane(cr.z, owner);
-        long long bdeg;
-        uint64_t bfp, dummy_fp;
-        long long dummy_deg;
-        const uint64_t bsum = pna_coop<0>(p, beg, cnt, s_big[wv][nb], bdeg, bfp, p.digest != nullptr);
-        pna_coop<1>(p, beg, cnt, s_big[wv][nb] + 32, dummy_deg, dummy_fp, false);
-        if (lane == owner && !(bsum >> 23)) {  // past the exact fp64 range: the lane's own walk (exact_sums)
-          slot = nb;
-          csum = bsum;
-          deg = bdeg;
-          fp = bfp;
+        PnaAcc A;
+        pna_acc_init(A);
+        pna_lane_walk(p, beg + c4, beg + cnt, 16, dq, want_fp, A);
+#pragma unroll
+        for (int off = 4; off < 64; off <<= 1) {
+          A.csum += __shfl_xor(A.csum, off, 64);
+          A.deg += __shfl_xor(A.deg, off, 64);
+          A.fp += __shfl_xor(A.fp, off, 64);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            A.mn[j] = __builtin_amdgcn_fmed3f(A.mn[j], __shfl_xor(A.mn[j], off, 64), -__builtin_huge_valf());
+            A.mx[j] = __builtin_amdgcn_fmed3f(A.mx[j], __shfl_xor(A.mx[j], off, 64), __builtin_huge_valf());
+          }
+        }
+        if (A.csum >> 23) {  // wave-uniform: the slots' exact int64 sums
+          long long es[4], eq[4];
+          pna_lane_exact(p, beg + c4, beg + cnt, 16, dq, es, eq);
+#pragma unroll
+          for (int off = 4; off < 64; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              es[j] += __shfl_xor(es[j], off, 64);
+              eq[j] += __shfl_xor(eq[j], off, 64);
+            }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            A.s[j] = (double)es[j];
+            A.q[j] = (double)eq[j];
+          }
+        } else {  // exact integers in fp64: any order
+#pragma unroll
+          for (int off = 4; off < 64; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              A.s[j] += __shfl_xor(A.s[j], off, 64);
+              A.q[j] += __shfl_xor(A.q[j], off, 64);
+            }
+        }
+        if (c4 == 0)
+          pna_features_out(p, A, dq, owner - 16 * t, true, q, __builtin_amdgcn_readlane(cr.x, owner), inv0, inv1,
+                           stage, sc);
+      }
+      // the other 16: candidate 16 t + c4 on lanes 4 c4 .. 4 c4 + 3
+      {
+        const int src = 16 * t + c4;
+        const int beg = __shfl(cr.y, src, 64), cnt = __shfl(cr.z, src, 64), ent = __shfl(cr.x, src, 64);
+        const bool liv = s0 + src < nc;
+        if (!(liv && cnt > PNA_BIG)) {  // (long lists: written by the wave walk above)
+          const int n = liv ? cnt : 0;
+          PnaAcc A;
+          pna_acc_init(A);
+          pna_lane_walk(p, beg, beg + n, 1, dq, want_fp, A);
+          if (A.csum >> 23) {
+            long long es[4], eq[4];
+            pna_lane_exact(p, beg, beg + n, 1, dq, es, eq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              A.s[j] = (double)es[j];
+              A.q[j] = (double)eq[j];
+            }
+          }
+          pna_features_out(p, A, dq, c4, liv, q, ent, inv0, inv1, stage, sc);
         }
       }
       wave_lds_sync();
-    }
-    const int wbeg = cr.y, wcnt = slot >= 0 ? 0 : cr.z;  // the lane's own walk (none for a staged list)
-    float sum[16], mm[16], mean[16];
-    asm volatile("" ::: "memory");  // keep the LDS weight reads inside the loop
-    {
-      uint64_t ws = 0, wf = 0;
-      long long wd = 0;
-      pna_walk<0, true>(p, wbeg, wcnt, ws, wd, wf, p.digest != nullptr, sum, mm);
-      if (slot >= 0) {
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-          sum[d] = s_big[wv][slot][d];
-          mm[d] = s_big[wv][slot][16 + d];
-        }
-      } else {
-        csum = ws;
-        deg = wd;
-        fp = wf;
+      // add_model on the matrix cores: per feature block one fp16 split, per
+      // scaler one 16-wide K step (three part products)
+      f32x4 D[3];
+      {
+        const float4 ab = reinterpret_cast<const float4 *>(s_w.addb)[k];
+        D[0] = (f32x4){ab.x, ab.y, ab.z, ab.w};
+        D[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        D[2] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-    }
-    if (p.digest && live)
-      atomicAdd(reinterpret_cast<unsigned long long *>(p.digest + q),
-                (unsigned long long)mix64((uint64_t)cr.x ^ mix64((uint64_t)deg ^ mix64(fp))));
-    if (live && (csum >> 33)) flag_acc_range(p);  // |int32 record| < 2^30: int64 sums exact below 2^33
-    // degree and scalers (layers.py:92, 103-116): degree = sum of A_fn + 1
-    const float degf = (float)(deg + 1);
-    const float idcl = 1.0f / fmaxf(degf, 1e-6f);  // one reciprocal for the 32 divisions by the degree
-    const float sc1 = live ? logf(degf) / fmaxf(p.q_scale[q], 1e-6f) : 1.0f;
-    s_sc[wv][lane] = make_float2(sc1, 1.0f / fmaxf(sc1, 1e-6f));
-    f32x4 D[3][4];  // per scaler {1, s, 1 / s}: W_s . features (pna_block)
-    {
-      const float4 ab = reinterpret_cast<const float4 *>(s_w.addb)[k];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        D[0][t] = (f32x4){ab.x, ab.y, ab.z, ab.w};
-        D[1][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        D[2][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-    }
+      for (int b = 0; b < 4; ++b) {
+        const float4 x = reinterpret_cast<const float4 *>(stage)[(b * 16 + i16) * 4 + k];
+        f16x4 bh, bl;
+        split4(x, bh, bl);
 #pragma unroll
-    for (int d = 0; d < 16; ++d) mean[d] = sum[d] * idcl;
-    pna_block(s_w, 0, mean, s_stage[wv], D);
-#pragma unroll
-    for (int d = 0; d < 16; ++d) mm[d] = live ? mm[d] : 0.f;  // (an empty walk's min is +inf)
-    pna_block(s_w, 1, mm, s_stage[wv], D);
-    {
-      uint64_t ws = 0, wf = 0;
-      long long wd = 0;
-      pna_walk<1, false>(p, wbeg, wcnt, ws, wd, wf, false, sum, mm);
-      if (slot >= 0) {
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-          sum[d] = s_big[wv][slot][32 + d];
-          mm[d] = s_big[wv][slot][48 + d];
+        for (int s3 = 0; s3 < 3; ++s3) {
+          const f16x4 ah = __builtin_bit_cast(f16x4, s_w.aa[b][s3][0][lane]);
+          const f16x4 al = __builtin_bit_cast(f16x4, s_w.aa[b][s3][1][lane]);
+          D[s3] = __builtin_amdgcn_mfma_f32_16x16x16f16(al, bh, D[s3], 0, 0, 0);
+          D[s3] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bl, D[s3], 0, 0, 0);
+          D[s3] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah, bh, D[s3], 0, 0, 0);
         }
       }
-    }
-#pragma unroll
-    for (int d = 0; d < 16; ++d) mm[d] = live ? mm[d] : 0.f;
-    pna_block(s_w, 2, mm, s_stage[wv], D);
-#pragma unroll
-    for (int d = 0; d < 16; ++d) sum[d] = sqrtf(fmaxf(sum[d] * idcl - mean[d] * mean[d], 1e-6f));
-    pna_block(s_w, 3, sum, s_stage[wv], D);
-    wave_lds_sync();  // s_big is rewritten by the next chunk
-    // LayerNorm over each candidate's 16 outputs (four k-lanes), ReLU, score_model
-    float out = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float2 scl = s_sc[wv][t * 16 + i16];  // the scalers of this lane's D column (candidate i16)
+      // LayerNorm over each candidate's 16 outputs (four k-lanes), ReLU, score_model
+      const float2 scl = sc[i16];
+      wave_lds_sync();  // the next tile rewrites the stage and the scalers
       f32x4 o4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o4[j] = fmaf(scl.y, D[2][t][j], fmaf(scl.x, D[1][t][j], D[0][t][j]));
+      for (int j = 0; j < 4; ++j) o4[j] = fmaf(scl.y, D[2][j], fmaf(scl.x, D[1][j], D[0][j]));
       float s4 = (o4[0] + o4[1]) + (o4[2] + o4[3]);
       s4 += __shfl_xor(s4, 16, 64);
       s4 += __shfl_xor(s4, 32, 64);
@@ -516,8 +490,8 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
       if (k == t) out = o;  // lane 16 t + i16 is candidate i16 of tile t
     }
     if (!live) continue;
-    const int t = cr.x;
-    const int64_t idx = (int64_t)q * p.g.E + t;
+    const int te = cr.x;
+    const int64_t idx = (int64_t)q * p.g.E + te;
     if (p.atomic_out) {  // deferred beside RotatE: added into the zeroed row (see sum_write_out)
       unsafeAtomicAdd(p.score + idx, out);
       continue;
@@ -525,7 +499,7 @@ __global__ __launch_bounds__(BS) void score_pna_chunk_kernel(KParams p, const fl
     if (p.feature == RNNL_FEATURE_NONE)
       p.score[idx] = out;
     else
-      p.score[idx] = out + (p.base_row ? p.base_row[t] : p.score[idx]);
+      p.score[idx] = out + (p.base_row ? p.base_row[te] : p.score[idx]);
     if (p.mask) p.mask[idx] = 1;
   }
 }

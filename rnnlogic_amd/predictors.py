@@ -1227,10 +1227,13 @@ class PredictorPlus(_HipGrounding, torch.nn.Module):
         # 11.04-11.16 vs 11.39-11.79 ms, the full split 81.38-81.63 vs
         # 82.00-82.27 (96 / 96: 13.0 / 81.4; 64 / 64: the chain outlasts
         # RotatE, 17.4 / 108 ms; tools/shard_run.py, profiles/r05_overlap_ab.txt)
-        # The PNA scoring pass is the chain's long pole beside RotatE and keeps
-        # one per CU (WN18RR 18.43 vs 20.63 ms at 128).
+        # The PNA scoring pass is the chain's long pole beside RotatE: 1.5 per
+        # CU since its walks went to four lanes per candidate (125 VGPRs; WN18RR
+        # 18.05-18.15 ms at 384 vs 18.13-18.15 at 256, 18.14-18.17 at 512,
+        # 20.5-20.7 at 128; the 233-VGPR per-candidate walk: 18.2 at 256,
+        # 19.1 at 128, 18.6 at 384 — tools/lines_ab.py)
         self.overlap_ground_wg = 128
-        self.overlap_score_wg = 128 if aggregator == "sum" else 256
+        self.overlap_score_wg = 128 if aggregator == "sum" else 384
         # the score rows' zero fill: issued before the rule encoder (beside it)
         # or by the forward call, after the encoder (beside rotate_hr and the
         # grounding's start).  SUM: by the call — FB15k-237 step 80.5-80.8 ->

@@ -39,11 +39,29 @@ def sha(t):
     return hashlib.sha1(t.detach().contiguous().cpu().numpy().tobytes()).hexdigest()[:12]
 
 
+if os.environ.get("AB_ONLY_WN"):  # the WN18RR lines alone (PNA changes)
+    with contextlib.redirect_stdout(sys.stderr):
+        wmodel, wh, wr, wgraph, _, _ = bench.wn18rr_model(dev, full=True)
+    if os.environ.get("AB_PNA_WG"):
+        wmodel.overlap_score_wg = int(os.environ["AB_PNA_WG"])
+        tag += " wg%d" % wmodel.overlap_score_wg
+    wn_step = stepper(wmodel, wh, wr)
+    wn_step()
+    d = sha(wn_step()[0])
+    for rd in range(rounds):
+        wms = [bench.isolated_ground_ms(wmodel, wgraph, wh, wr, dev) for _ in range(4)][1:]
+        wn = [bench.time_forward(wn_step, 10) * 1e3 for _ in range(2)]
+        print("%s r%d: WN step %s, ground+pna %s ms | wn %s" % (tag, rd, " ".join("%.3f" % x for x in wn),
+                                                                 " ".join("%.3f" % x for x in wms), d), flush=True)
+    sys.exit(0)
 with contextlib.redirect_stdout(sys.stderr):
     graph, test_set, model, rows = bench.build_workload("bias")
     rgraph, _, rmodel, rrows = bench.build_workload("RotatE")
     wmodel, wh, wr, wgraph, _, _ = bench.wn18rr_model(dev, full=True)
 model, rmodel = model.to(dev).eval(), rmodel.to(dev).eval()
+if os.environ.get("AB_PNA_WG"):  # the PNA scoring pass's workgroups beside RotatE
+    wmodel.overlap_score_wg = int(os.environ["AB_PNA_WG"])
+    tag += " wg%d" % wmodel.overlap_score_wg
 h, r = rows_of(rows)
 rh, rr = rows_of(rrows)
 fb_step, rot_step, wn_step = stepper(model, h, r), stepper(rmodel, rh, rr), stepper(wmodel, wh, wr)
