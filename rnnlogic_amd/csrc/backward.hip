@@ -415,8 +415,13 @@ __global__ __launch_bounds__(BWB) void node_accum_kernel(KParams p, const float 
   const long long nchunks = (long long)*reinterpret_cast<const unsigned long long *>(hdr + H_CHUNKS);
   // bad (a non-finite dL/dy): fp64 sums in the same words instead, so that
   // NaN / inf reach exactly the nodes the reference's would
+  // each dL/dy is rounded to the fixed-point grid once and multiplied by the
+  // integer count: a (node, candidate) pair split over several bucket entries
+  // (phase A's raw duplicates, which vary with the LDS hash's insertion order)
+  // then sums to exactly its merged entry's k x fix(dL/dy)
   auto add = [&](const int2 be, const float (&g)[16]) {
     const double k = (double)(uint32_t)be.y;
+    const long long ki = (long long)(uint32_t)be.y;
     const unsigned ln = (unsigned)(be.x - lo);
 #pragma unroll
     for (int d = 0; d < 16; ++d) {
@@ -425,7 +430,7 @@ __global__ __launch_bounds__(BWB) void node_accum_kernel(KParams p, const float 
       if (bad)
         atomicAdd(reinterpret_cast<double *>(w), k * (double)g[d]);
       else
-        atomicAdd(w, (unsigned long long)llrint(ldexp(k * (double)g[d], sc)));
+        atomicAdd(w, (unsigned long long)(ki * llrint(ldexp((double)g[d], sc))));
     }
   };
   const long long nw = (long long)gridDim.x * BW_WAVES;

@@ -17,13 +17,16 @@
 //       one rounding; deg = 1 + sum of count x rules at the node.
 //   pna_grad_stats_kernel / pna_grad_nodes_kernel / pna_grad_rules_kernel
 //       the backward: per node G1 = sum count x dL/dwsum, G2 likewise for
-//       wsq, and the min / max gradients as torch's scatter_reduce amin /
-//       amax backward takes them (split evenly among a candidate's tied
-//       entries, then among a node's tied rules) — all int64 fixed point at
-//       one scale per launch, so the sums do not depend on the order of the
-//       adds; then per rule dL/dx = G1 + 2 x G2 + its min / max shares.
+//       wsq, and each candidate's min / max gradient to one node tied at the
+//       min / max (the smallest; the reference's dense .min(1) / .max(1)
+//       route it to one index), split evenly among that node's tied rules —
+//       all int64 fixed point at one scale per launch, each gradient rounded
+//       to it once per candidate, so the sums depend neither on the order of
+//       the adds nor on how a (node, candidate) pair is split over bucket
+//       entries; then per rule dL/dx = G1 + 2 x G2 + its min / max shares.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <string>
 
 #include "fwd.h"
@@ -186,13 +189,18 @@ __device__ __forceinline__ unsigned long long pg_fix(double v, int sc) {
 
 // One wave per candidate (grid-stride over the C candidates), lane = (entry
 // slot j, dim d) as pna_features_kernel: per bucket entry (node n, count k)
-// G1[n] += k dL/dwsum, G2[n] += k dL/dwsq, and the candidate's min / max
-// gradient to its entries tied at the min / max (scatter_reduce amin / amax
-// split it evenly among them): Gmin[n] += dL/dmn / ties.  A wave's adds go to
-// 64 distinct (entry, dim) words (a lane per candidate had every lane of a
-// wave add into the same few shared nodes: 2.2 ms per WN18RR batch).  Four
-// int64 tables at the launch's scale; the first nl nodes from `lo` (a
-// one-relation launch's head trie) summed in LDS and written as this
+// G1[n] += k fix(dL/dwsum), G2[n] += k fix(dL/dwsq) — each gradient on the
+// fixed-point grid once, times the integer count, so a (node, candidate) pair
+// split over several bucket entries (phase A's raw duplicates, which vary
+// with its LDS hash's insertion order) sums exactly as its merged entry — and
+// the candidate's min / max gradient whole to the smallest trie node among
+// its entries tied at the min / max (the reference's dense .min(1) / .max(1)
+// route it to one index, layers.py:100-101; a node's duplicate entries tie
+// with each other, so it gets the gradient once whatever the split).  A
+// wave's adds go to 64 distinct (entry, dim) words (a lane per candidate had
+// every lane of a wave add into the same few shared nodes: 2.2 ms per WN18RR
+// batch).  Four int64 tables at the launch's scale; the first nl nodes from
+// `lo` (a one-relation launch's head trie) summed in LDS and written as this
 // workgroup's partial rows (summed by pna_grad_rules_kernel), the rest by
 // int64 HBM atomics.
 __global__ __launch_bounds__(PG_BS) void pna_grad_nodes_kernel(
@@ -219,33 +227,29 @@ __global__ __launch_bounds__(PG_BS) void pna_grad_nodes_kernel(
     for (int64_t c = (int64_t)blockIdx.x * (PG_BS / 64) + (threadIdx.x >> 6); c < C; c += nw) {
       const int q = cand_row(cand_off, p.nq, c);
       const int4 cr = p.cand[p.q_base[q] + (c - cand_off[q])];
-      const float g1 = d_wsum[c * 16 + d], g2 = d_wsq[c * 16 + d];
+      const long long f1 = (long long)pg_fix((double)d_wsum[c * 16 + d], sc);
+      const long long f2 = (long long)pg_fix((double)d_wsq[c * 16 + d], sc);
       const float vmn = mn[c * 16 + d], vmx = mx[c * 16 + d];
-      int tmn = 0, tmx = 0;  // the candidate's entries tied at its min / max (dim d)
+      int nmn = INT_MAX, nmx = INT_MAX;  // the smallest node tied at the candidate's min / max (dim d)
 #pragma unroll 1
       for (int e = cr.y + j; e < cr.y + cr.z; e += 4) {
         const int2 be = p.bent[e];
         const float *fr = reinterpret_cast<const float *>(node_w + (uint32_t)be.x * (uint32_t)kStridePna) + 32;
-        const double k = (double)(uint32_t)be.y;
-        tmn += fr[d] == vmn;
-        tmx += fr[16 + d] == vmx;
-        if (g1 != 0.f) add(0, be.x, d, pg_fix(k * (double)g1, sc));
-        if (g2 != 0.f) add(1, be.x, d, pg_fix(k * (double)g2, sc));
+        const long long k = (long long)(uint32_t)be.y;
+        if (fr[d] == vmn) nmn = min(nmn, be.x);
+        if (fr[16 + d] == vmx) nmx = min(nmx, be.x);
+        if (f1) add(0, be.x, d, (unsigned long long)(k * f1));
+        if (f2) add(1, be.x, d, (unsigned long long)(k * f2));
       }
-      tmn += __shfl_xor(tmn, 16, 64);
-      tmn += __shfl_xor(tmn, 32, 64);
-      tmx += __shfl_xor(tmx, 16, 64);
-      tmx += __shfl_xor(tmx, 32, 64);
-      const float gmn = tmn ? d_mn[c * 16 + d] / (float)tmn : 0.f;
-      const float gmx = tmx ? d_mx[c * 16 + d] / (float)tmx : 0.f;
-      if (__ballot(gmn != 0.f || gmx != 0.f))
-#pragma unroll 1
-        for (int e = cr.y + j; e < cr.y + cr.z; e += 4) {
-          const int n = p.bent[e].x;
-          const float *fr = reinterpret_cast<const float *>(node_w + (uint32_t)n * (uint32_t)kStridePna) + 32;
-          if (gmn != 0.f && fr[d] == vmn) add(2, n, d, pg_fix((double)gmn, sc));
-          if (gmx != 0.f && fr[16 + d] == vmx) add(3, n, d, pg_fix((double)gmx, sc));
-        }
+      nmn = min(nmn, __shfl_xor(nmn, 16, 64));
+      nmn = min(nmn, __shfl_xor(nmn, 32, 64));
+      nmx = min(nmx, __shfl_xor(nmx, 16, 64));
+      nmx = min(nmx, __shfl_xor(nmx, 32, 64));
+      if (j == 0) {
+        const float gmn = d_mn[c * 16 + d], gmx = d_mx[c * 16 + d];
+        if (gmn != 0.f && nmn != INT_MAX) add(2, nmn, d, pg_fix((double)gmn, sc));
+        if (gmx != 0.f && nmx != INT_MAX) add(3, nmx, d, pg_fix((double)gmx, sc));
+      }
     }
   __syncthreads();
   long long *row = gpart + (int64_t)blockIdx.x * 4 * nl * 16;

@@ -196,13 +196,15 @@ __global__ __launch_bounds__(BS) void predictor_backward_kernel(KParams p, const
       const int4 cr = p.cand[qb + s];
       const double g = (double)gq[cr.x];
       if (g == 0.0) continue;
+      // the gradient on the fixed-point grid once, times each entry's integer
+      // count: split and merged (node, candidate) entries sum alike
+      const long long gf = bad ? 0 : llrint(ldexp(g, sc));
       for (int e = cr.y; e < cr.y + cr.z; ++e) {
         const int2 be = p.bent[e];
-        const double t = (double)(uint32_t)be.y * g;
         if (bad)
-          atomicAdd(reinterpret_cast<double *>(&s_g[be.x - root]), t);
+          atomicAdd(reinterpret_cast<double *>(&s_g[be.x - root]), (double)(uint32_t)be.y * g);
         else
-          atomicAdd(&s_g[be.x - root], (unsigned long long)llrint(ldexp(t, sc)));
+          atomicAdd(&s_g[be.x - root], (unsigned long long)((long long)(uint32_t)be.y * gf));
       }
     }
     __syncthreads();

@@ -554,6 +554,7 @@ class Predictor(_HipGrounding, torch.nn.Module):
         self._native_rules = {}
         self._lin_cache = {}
         self._roots = {}
+        self._pf = {}  # queued lookahead groundings belong to the old rules
 
     # ------------------------------------------------------------------ native plumbing
     def node_weights(self, device):
@@ -1025,9 +1026,11 @@ class _PnaStats(torch.autograd.Function):
     reaching it, and (not differentiable) its degree, row and entity —
     rnnl_pna_features after rnnl_node_weights(PNA) of the embedding table
     `emb` (num_rules x 16) and rnnl_ground.  Backward:
-    rnnl_pna_features_backward (per node count x gradient sums, min / max as
-    torch's scatter_reduce amin / amax backward; int64 fixed point, run-to-run
-    bitwise).  The grounding stays in the model's workspace between the two;
+    rnnl_pna_features_backward (per node count x gradient sums; a
+    candidate's min / max gradient to one tied node, as the reference's
+    .min(1) / .max(1) route it to one index; int64 fixed point, independent of
+    the order of the adds and of how a (node, candidate) pair is split over
+    bucket entries: run-to-run bitwise).  The grounding stays in the model's workspace between the two;
     if another launch has reused it by then, the rows are grounded again."""
 
     @staticmethod
