@@ -11,7 +11,11 @@ per-node gradients and the EM Predictor's are int64 fixed-point sums at
 one scale per launch (backward.hip node_accum_kernel, predictor.hip
 predictor_backward_kernel), and relation_emb's gradient of a one-relation
 batch is W0[:, 16:]^T dL/db0 in a fixed order (rel_grad_kernel); the PNA
-statistics' backward sums in int64 fixed point too (pna_grad.hip).
+statistics' backward sums in int64 fixed point too (pna_grad.hip).  Each
+gradient is rounded to the fixed-point grid once per candidate and multiplied
+by the integer path count, so the sums do not depend on how the grounding
+split a (node, candidate) pair over bucket entries either (that split follows
+the LDS hash's insertion order and varies from run to run).
 """
 import pytest
 import torch
@@ -73,6 +77,8 @@ CASES = {
     # config 5's EM rule-weight Predictor
     "fb_em_predictor": ("FB15k-237", "pred", dict(entity_feature="bias"), None),
     "kinship_lstm_sum_none": ("kinship", "plus", dict(type="lstm", entity_feature="none", aggregator="sum"), None),
+    # config 3: PNA statistics in HIP, FuncToNode's dense layers in torch
+    "wn_emb_pna_rotate": ("wn18rr", "plus", dict(type="emb", entity_feature="RotatE", aggregator="pna"), 500),
 }
 
 
@@ -88,12 +94,12 @@ def test_training_is_bitwise_repeatable(case, dev):
 
 def test_pna_statistics_backward_is_bitwise_repeatable(dev):
     """The PNA path (config 3) trains its dense layers (Linear(192, 16),
-    score_model) through torch GEMMs whose weight gradients reduce over every
-    candidate — the BLAS library may split that reduction with atomics, so
-    end-to-end training is not bitwise repeatable there.  The package's own
-    part is: the statistics' forward and backward (csrc/pna_grad.hip, int64
-    fixed-point node sums) give bitwise-equal rule-embedding gradients for the
-    same incoming gradients, over WN18RR training batches (edge removal)."""
+    score_model) through torch GEMMs (end to end: the wn_emb_pna_rotate case
+    above).  The package's own part alone: the statistics' forward and
+    backward (csrc/pna_grad.hip, int64 fixed-point node sums, each gradient
+    rounded once per candidate) give bitwise-equal rule-embedding gradients
+    for the same incoming gradients, over WN18RR training batches (edge
+    removal), each grounded afresh."""
     import contextlib
     import io
 
