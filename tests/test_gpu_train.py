@@ -20,13 +20,16 @@ from conftest import GOLDEN, TRAIN_CASES, TRAIN_SPECS
 
 pytestmark = pytest.mark.gpu
 
-LOSS_TOL = 2e-5      # step-0 loss, relative
-# gradients: fp32 accumulation order differs (index_add vs the reference's
-# expanded index_select backward), and RotatE's d|x|/dx = x/|x| amplifies the
-# rounding of near-zero distances, so the absolute tolerance scales with the
-# tensor's gradient magnitude
-GRAD_RTOL, GRAD_ATOL_MIN, GRAD_ATOL_REL = 2e-4, 2e-6, 2e-3
-LATER_LOSS_TOL = 5e-4  # steps 1-2 follow Adam updates of step-0 gradients (relative)
+# Tolerances at about 10x the largest error observed on the MI355X (round 6,
+# `pytest -s` prints every one): step-0 losses <= 2.0e-7 relative; step-0
+# gradients max |err| / max |g| <= 1.5e-6 for the rule part, the LSTM and
+# score_model, 5.8e-5 for RotatE's tables (the backward's rsq(s) instead of a
+# correctly rounded 1 / sqrt(s), and d|x|/dx = x/|x| amplifying the rounding
+# of near-zero distances); the absolute floor covers score_model's output
+# bias, whose exact gradient (a sum of softmax residuals) is ~0.
+LOSS_TOL = 2e-6      # step-0 loss, relative
+GRAD_RTOL, GRAD_ATOL_MIN, GRAD_ATOL_REL = 2e-4, 2e-6, 5e-4
+LATER_LOSS_TOL = 5e-4  # steps 1-2 follow Adam updates of step-0 gradients (relative; observed <= 1.2e-4)
 
 
 @pytest.fixture(scope="module")
@@ -106,7 +109,7 @@ def test_step1_loss_from_reference_gradients(case, dev):
         return
     print("%s step 1 after the reference's step-0 gradients: loss %.9g, reference %.9g, relative delta %.3g"
           % (case, l1.item(), want, abs(l1.item() - want) / abs(want)))
-    assert abs(l1.item() - want) <= LOSS_TOL / 10 * abs(want), (case, l1.item(), want)
+    assert abs(l1.item() - want) <= 2e-6 * abs(want), (case, l1.item(), want)
 
 
 @pytest.mark.parametrize("fused", [True, False], ids=["fused_backward", "autograd_coo"])
@@ -174,6 +177,9 @@ def test_train_steps_match_reference(case, fused, dev):
                     g = prm.grad.detach().reshape(prm.shape[0], -1)
                     rows = z["gs/%s/rows" % n]
                     want = z["gs/%s/vals" % n]
+                    got_rows = g[torch.from_numpy(rows).to(dev)].cpu().numpy()
+                    print("  grad %s (sampled rows): max |err| / max |g| = %.3g"
+                          % (n, float(np.abs(got_rows - want).max()) / max(float(np.abs(want).max()), 1e-30)))
                     atol = max(GRAD_ATOL_MIN, GRAD_ATOL_REL * float(np.abs(want).max()))
                     np.testing.assert_allclose(g[torch.from_numpy(rows).to(dev)].cpu().numpy(), want, atol=atol,
                                                rtol=GRAD_RTOL, err_msg="%s grad %s (sampled rows)" % (case, n))
@@ -187,7 +193,9 @@ def test_train_steps_match_reference(case, fused, dev):
                     assert prm.grad is None or float(prm.grad.abs().max()) == 0.0, (case, n)
                     continue
                 g = prm.grad.detach().cpu().numpy()
-                atol = max(GRAD_ATOL_MIN, GRAD_ATOL_REL * float(np.abs(z[key]).max()))
+                gmax = float(np.abs(z[key]).max())
+                print("  grad %s: max |err| / max |g| = %.3g" % (n, float(np.abs(g - z[key]).max()) / max(gmax, 1e-30)))
+                atol = max(GRAD_ATOL_MIN, GRAD_ATOL_REL * gmax)
                 np.testing.assert_allclose(g, z[key], atol=atol, rtol=GRAD_RTOL, err_msg="%s grad %s" % (case, n))
         optim.step()
         optim.zero_grad()
