@@ -629,9 +629,13 @@ int rnnl_predictorplus_backward(rnnl_graph g, rnnl_rules r, const rnnl_predictor
  * paths, sets the workspace header's range bits (rnnl_forward_status:
  * RNNL_ERR_RANGE).
  * rnnl_pna_features_backward: d_x (n_rules x 16, written whole) from the
- * gradients of the four statistics — per node sum count x gradient, min / max
- * split evenly among tied entries then tied rules (torch scatter_reduce amin /
- * amax), int64 fixed point at one scale per launch: run-to-run bitwise.
+ * gradients of the four statistics — per node sum count x gradient (each
+ * gradient rounded to the fixed-point grid once per candidate, times the
+ * integer count), a candidate's min / max gradient whole to the smallest trie
+ * node tied at its min / max (the reference's .min(1) / .max(1) route it to
+ * one index, layers.py:100-101) and split evenly among that node's tied
+ * rules; int64 fixed point at one scale per launch: run-to-run bitwise,
+ * whatever the split of a (node, candidate) pair over bucket entries.
  * head >= 0: every row is of that relation (only its trie is touched), -1:
  * any rows.  scratch: rnnl_pna_features_backward_scratch bytes. */
 int rnnl_pna_features(rnnl_rules r, const void *node_w, void *workspace, int32_t n_queries, int32_t capacity_scale,
