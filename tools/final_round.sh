@@ -4,7 +4,7 @@
 # (tools/profile_round.sh) and the per-kernel VALU counts (tools/pmc_valu.sh).
 # Usage (GPU box, repo root): COMMIT=<id> bash tools/final_round.sh rNN
 set -o pipefail
-tag=${1:-r05}
+tag=${1:-r06}
 mkdir -p gpurun_out/$tag
 # the library rebuilt from source on the box (build() as the driver runs it), logged
 ( set -x; rm -rf rnnlogic_amd/_build oracle/_build; hipcc --version | head -2; \
