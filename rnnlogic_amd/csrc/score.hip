@@ -951,6 +951,20 @@ constexpr int SUM_CK = 8;  // chunks per dequeue on large launches
 // FB15k-237 split: 0.9M chunks) the spill-free 4-waves/SIMD build with the
 // cooperative long-list gather (ground + score alone 12.9 -> 10.4 ms).
 constexpr int SOLO_FEW_ROWS = 8192;
+// Launches with about one chunk per wave or fewer (up to SOLO_FEW_ROWS rows;
+// one reference batch per call) keep a wave per chunk, so occupancy buys
+// nothing there and the register budget goes to the entry walk: the
+// 8-waves/SIMD build spilled ~90 VGPRs to scratch inside it (kinship step
+// 0.570 -> 0.515 ms at 4 waves / 128 VGPRs, no spills; 0.531 at 5).  A/B knobs.
+#ifndef RNNL_FEW_WPE
+#define RNNL_FEW_WPE 4
+#endif
+#ifndef RNNL_SMALL_WPE
+#define RNNL_SMALL_WPE 4
+#endif
+#ifndef RNNL_SMALL_OVERLAP_WPE
+#define RNNL_SMALL_OVERLAP_WPE 4
+#endif
 #ifndef RNNL_SOLO_WPE
 #define RNNL_SOLO_WPE 4
 #endif
@@ -1148,13 +1162,14 @@ void launch_score(const KParams &p0, const RulesDev &rl, hipStream_t st, int gri
   else if (p.digest)
     hipLaunchKernelGGL((score_sum_chunk_kernel<true, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (p.atomic_out && small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, RNNL_SMALL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p,
+                       W);
   else if (p.atomic_out)
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, RNNL_OVERLAP_COOP, RNNL_OVERLAP_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (small)
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, true, RNNL_SMALL_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else if (nq <= SOLO_FEW_ROWS)  // about one chunk per wave: occupancy (8 waves/SIMD) over spill-free waves
-    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, 8>), dim3(cgrid), dim3(BS), 0, st, p, W);
+    hipLaunchKernelGGL((score_sum_chunk_kernel<false, false, RNNL_FEW_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
   else
     hipLaunchKernelGGL((score_sum_chunk_kernel<false, RNNL_SOLO_COOP, RNNL_SOLO_WPE>), dim3(cgrid), dim3(BS), 0, st, p, W);
 }

@@ -40,6 +40,9 @@ def step():
         return model.forward_rows(h, r, None)
 
 
+for pm in (0, 1):  # the SUM scoring pass's pair memo off / on (rnnl_debug_pair_memo)
+    _native.call("rnnl_debug_pair_memo", pm)
+    print("kinship step, pair memo %d: %.3f ms" % (pm, bench.time_forward(step, 50) * 1e3))
 ms = bench.time_forward(step, 50) * 1e3
 with torch.no_grad():
     prof = torch.zeros(13, dtype=torch.int64, device=dev)
