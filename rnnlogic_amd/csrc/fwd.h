@@ -115,6 +115,7 @@ struct KParams {
   unsigned char *slots;
   int64_t *q_base;   // per query: first pool index of its run
   float *q_scale;    // per query: PNA mean log-degree
+  const int32_t *order;  // nullable: the grounding's dequeue order (heaviest estimated queries first)
   int32_t atomic_out;  // deferred scoring into a zeroed score matrix: atomic adds
   int4 *cand;        // per pool index: candidate record (entity, bucket start, bucket length, 0)
                      // (the first n_cand entries of a query's run)
@@ -178,7 +179,7 @@ constexpr int PTAB_MIN_BITS = RNNL_PTAB_MIN_BITS;
 // Workspace layout, shared by host sizing and the launch.
 struct Layout {
   int64_t nslots, fcap, pcap, pool_cap;
-  int64_t off_qbase, off_qscale, off_cand, off_bent, off_slots, off_chunk, chunk_cap, off_memo, off_ptab, ptab_bits,
+  int64_t off_qbase, off_qscale, off_order, off_cand, off_bent, off_slots, off_chunk, chunk_cap, off_memo, off_ptab, ptab_bits,
       total;
 };
 
@@ -200,6 +201,8 @@ inline Layout make_layout(int64_t nq, int64_t scale, int64_t n_nodes = 0) {
   L.off_qbase = o = align256(o);
   o += 8 * std::max<int64_t>(nq, 1);
   L.off_qscale = o = align256(o);
+  o += 4 * std::max<int64_t>(nq, 1);
+  L.off_order = o = align256(o);
   o += 4 * std::max<int64_t>(nq, 1);
   L.off_cand = o = align256(o);
   o += 16 * L.pool_cap;

@@ -739,7 +739,10 @@ __global__ __launch_bounds__(G, G >= 512 ? 4 : 1) void ground_kernel(KParams p) 
   __syncthreads();
 #pragma unroll 1
   while (true) {
-    if (tid == 0) S.q = (int)atomicAdd(&hdr[H_DEQUEUE], 1u);
+    if (tid == 0) {
+      const int qi = (int)atomicAdd(&hdr[H_DEQUEUE], 1u);
+      S.q = qi < p.nq && p.order ? p.order[qi] : qi;
+    }
     __syncthreads();
     const int q = S.q;
     if (q >= p.nq) break;
@@ -1181,6 +1184,7 @@ int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all
   p.slots = base + Ly.off_slots;
   p.q_base = reinterpret_cast<int64_t *>(base + Ly.off_qbase);
   p.q_scale = reinterpret_cast<float *>(base + Ly.off_qscale);
+  p.order = nullptr;  // set by launch_ground on launches of more rows than workgroups
   p.cand = reinterpret_cast<int4 *>(base + Ly.off_cand);
   p.bent = reinterpret_cast<int2 *>(base + Ly.off_bent);
   p.memo = reinterpret_cast<float *>(base + Ly.off_memo);
@@ -1207,8 +1211,93 @@ int setup_params(const char *who, rnnl_graph g, rnnl_rules r, const int64_t *all
 // Kernel sequences shared by the one-call forward and its two halves.
 // `grid` caps the persistent workgroups (0: one per workspace slot, the
 // default occupancy); a smaller grid leaves CUs to a concurrent kernel.
-void launch_ground(const KParams &p, int agg, hipStream_t st, int grid) {
+// The grounding's dequeue order (RNNL_HEAVY_FIRST; 0 = row order): rows by
+// an estimate of their work, heaviest first, so that the launch does not end
+// on a workgroup that dequeued a heavy query late — the FB15k-237 split's
+// heaviest queries cost ~14x the mean, and in row order the launch's tail is
+// ~0.35 ms of ~6.1 (tools/tail_sim.py, from the C oracle's per-query work).
+// The estimate is the head's out-degree times the relation's trie size
+// (log-correlation 0.79 with the work); the rows are counting-sorted by its
+// log2 bucket, descending (two passes of many workgroups).  Only the
+// order of the queries changes: every query's outputs are its own, so the
+// results are the same.
+#ifndef RNNL_HEAVY_FIRST
+#define RNNL_HEAVY_FIRST 1
+#endif
+constexpr int ORDER_BS = 256, ORDER_BUCKETS = 64;
+
+// the row's log2 work bucket, heaviest = 0
+__device__ __forceinline__ int order_bucket(const KParams &p, int q) {
+  const int h = (int)p.all_h[q], r = (int)p.all_r[q];
+  const long long deg = (long long)p.g.off[(int64_t)(h + 1) * p.g.R] - p.g.off[(int64_t)h * p.g.R];
+  const int root = p.rl.head_root[r];
+  const unsigned long long w = root < 0 ? 0ull : (unsigned long long)(deg + 1) * (unsigned)p.rl.head_nodes[r];
+  return ORDER_BUCKETS - 1 - min(ORDER_BUCKETS - 1, 63 - __clzll(w | 1ull));
+}
+
+// pass 1: each row's bucket (kept in `bk`) and the buckets' sizes (`cnt`, zeroed by the caller)
+__global__ __launch_bounds__(ORDER_BS) void order_count_kernel(KParams p, unsigned char *__restrict__ bk,
+                                                               int *__restrict__ cnt) {
+  __shared__ int s_hist[ORDER_BUCKETS];
+  if (threadIdx.x < ORDER_BUCKETS) s_hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int q = blockIdx.x * ORDER_BS + threadIdx.x;
+  if (q < p.nq) {
+    const int b = order_bucket(p, q);
+    bk[q] = (unsigned char)b;
+    atomicAdd(&s_hist[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < ORDER_BUCKETS && s_hist[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], s_hist[threadIdx.x]);
+}
+
+// pass 2: rows scattered by bucket, heaviest buckets first (`cnt` becomes
+// the buckets' fill counters past their starts)
+__global__ __launch_bounds__(ORDER_BS) void order_fill_kernel(KParams p, const unsigned char *__restrict__ bk,
+                                                              int *__restrict__ cnt, int32_t *__restrict__ order) {
+  __shared__ int s_base[ORDER_BUCKETS], s_hist[ORDER_BUCKETS], s_off[ORDER_BUCKETS];
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < ORDER_BUCKETS; ++b) {
+      s_base[b] = acc;
+      acc += cnt[b];
+    }
+  }
+  if (threadIdx.x < ORDER_BUCKETS) s_hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int q = blockIdx.x * ORDER_BS + threadIdx.x;
+  int b = 0, k = 0;
+  if (q < p.nq) {
+    b = bk[q];
+    k = atomicAdd(&s_hist[b], 1);  // this block's rows of bucket b
+  }
+  __syncthreads();
+  if (threadIdx.x < ORDER_BUCKETS && s_hist[threadIdx.x])  // one global reservation per (block, bucket)
+    s_off[threadIdx.x] = atomicAdd(&cnt[ORDER_BUCKETS + threadIdx.x], s_hist[threadIdx.x]);
+  __syncthreads();
+  if (q < p.nq) order[s_base[b] + s_off[b] + k] = q;
+}
+
+void launch_ground(const KParams &p0, int agg, hipStream_t st, int grid) {
+  KParams p = p0;
   const unsigned g = (unsigned)(grid > 0 ? std::min(grid, p.nslots) : p.nslots);
+  // with the chip to itself (beside RotatE the chain has slack), more rows
+  // than workgroups, and a graph of more than one phase-B window (kinship's
+  // and UMLS's queries cost alike: there the pass's three dispatches only
+  // add ~10 us).  tools/ab_order.sh: WN18RR ground + PNA alone 4.64-5.08 ->
+  // 4.12-4.19 ms, FB15k-237 bias 9.27 -> 9.23-9.25 ms, the RotatE steps
+  // unchanged within the box's noise.
+  if (RNNL_HEAVY_FIRST && grid <= 0 && p.nq > (int)g && p.g.E > WIN) {
+    int32_t *order = reinterpret_cast<int32_t *>(p.ws + make_layout(p.nq, 1).off_order);
+    // the row buckets and the counters in the slot scratch (free until the grounding starts)
+    int *cnt = reinterpret_cast<int *>(p.slots);
+    unsigned char *bk = p.slots + 4 * 2 * ORDER_BUCKETS;
+    (void)hipMemsetAsync(cnt, 0, sizeof(int) * 2 * ORDER_BUCKETS, st);
+    const unsigned nb = (unsigned)((p.nq + ORDER_BS - 1) / ORDER_BS);
+    hipLaunchKernelGGL(order_count_kernel, dim3(nb), dim3(ORDER_BS), 0, st, p, bk, cnt);
+    hipLaunchKernelGGL(order_fill_kernel, dim3(nb), dim3(ORDER_BS), 0, st, p, (const unsigned char *)bk, cnt, order);
+    p.order = order;
+  }
   // few rows (a reference batch per call): one 1024-lane workgroup per query,
   // so the batch's heaviest query — the launch's critical path — expands
   // four times the frontier items and edges per pass; beside another kernel
